@@ -1,0 +1,192 @@
+"""Generate tests/golden/* by running the REFERENCE's own code in this container.
+
+Run:  python -m oracle.gen_golden          (needs /root/reference; CPU only)
+
+* MMBT fixtures: the reference ``src/mmbt.py`` MultimodalBertClf with the
+  golden_stubs/ third-party stand-ins, weights loaded from oracle/weights.py
+  (strict), inputs synthetic (seeded).  Every forward variant
+  (src/mmbt.py:245-259) is recorded with the control indices the reference drew
+  from the global RNG (src/mmbt.py:199), plus image features, embeddings, pooled
+  output, CE loss (eval) and a train-mode (BN batch stats, dropout 0) loss with
+  per-tensor grad norms.
+* framework fixture: the reference ``Model_.train_loop`` (src/framework.py:213)
+  with ``_construct_default_callbacks`` (src/training_loop.py:23-47) driving
+  oracle/tiny_model.TinyMMBT for 2 epochs x 3 steps; history + checkpoint keys.
+
+Only arrays (inputs / outputs) are written -- no reference source.
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+REF = "/root/reference"
+OUT = os.path.join(REPO, "tests", "golden")
+
+
+def _import_reference(cfg, dropout):
+    # transformers must resolve the real (absent) torchvision before the stub is visible
+    import transformers.models.bert.modeling_bert  # noqa: F401
+    sys.path[:0] = [os.path.join(HERE, "golden_stubs"), REF]
+    os.environ.setdefault("DATA_DIR", tempfile.gettempdir())
+    if not hasattr(np, "Inf"):
+        np.Inf = np.inf  # numpy 2 removed the alias src/callbacks.py:205-215 uses
+    import torchvision.models as tvm
+    from pytorch_pretrained_bert import modeling as ppb
+    tvm.BLOCKS = tuple(cfg.resnet_blocks)
+    ppb.CONFIG.update(num_hidden_layers=cfg.n_layers, vocab_size=cfg.vocab,
+                      hidden_dropout_prob=dropout, attention_probs_dropout_prob=dropout)
+    from src import mmbt, framework, training_loop  # the reference's own modules
+    return mmbt, framework, training_loop
+
+
+def _args(cfg):
+    a = types.SimpleNamespace()
+    a.img_embed_pool_type, a.num_image_embeds = "avg", cfg.num_image_embeds
+    a.img_hidden_sz, a.hidden_sz, a.dropout = cfg.img_hidden, cfg.hidden, 0.0
+    a.bert_model, a.n_classes = "bert-base-uncased", cfg.n_classes
+    a.vocab = types.SimpleNamespace(stoi={"[CLS]": cfg.cls_id, "[SEP]": cfg.sep_id})
+    return a
+
+
+def make_inputs(cfg, B, T, lens, seed):
+    """Synthetic batch in collate_fn order (src/dataset.py:420-438)."""
+    g = torch.Generator().manual_seed(seed)
+    txt = torch.randint(1000, cfg.vocab, (B, T), generator=g)
+    mask = (torch.arange(T)[None, :] < torch.as_tensor(lens)[:, None]).long()
+    txt = txt * mask
+    segment = mask.clone()  # segment = 1 on real tokens (src/dataset.py:403)
+    img = torch.randn(B, 3, 224, 224, generator=g)
+    y = torch.randint(0, cfg.n_classes, (B,), generator=g)
+    return (txt, segment, mask, img), y
+
+
+def gen_mmbt(tag, cfg, B, T, lens, seed=0, wseed=0):
+    from oracle.weights import make_state_dict, checksum
+    mmbt, _, _ = _import_reference(cfg, 0.0)
+    torch.manual_seed(1234)
+    model = mmbt.MultimodalBertClf(_args(cfg))
+    sd = make_state_dict(wseed, cfg)
+    ref_keys = list(model.state_dict().keys())
+    model.load_state_dict(sd, strict=True)
+    x, y = make_inputs(cfg, B, T, lens, seed)
+    rec = {}
+    hooks = [model.enc.img_encoder.register_forward_hook(lambda m, i, o: rec.__setitem__("feats", o.detach())),
+             model.enc.img_embeddings.register_forward_hook(lambda m, i, o: rec.__setitem__("img_emb", o.detach())),
+             model.enc.txt_embeddings.register_forward_hook(lambda m, i, o: rec.__setitem__("txt_emb", o.detach())),
+             model.enc.pooler.register_forward_hook(lambda m, i, o: rec.__setitem__("pooled", o.detach()))]
+    out = {"text": x[0].numpy(), "segment": x[1].numpy(), "mask": x[2].numpy(), "y": y.numpy(),
+           "img_sum": np.float64(x[3].double().sum()), "weight_checksum": np.float64(checksum(sd)),
+           "seed": np.int64(seed), "wseed": np.int64(wseed)}
+    model.eval()
+    with torch.no_grad():
+        logits = model(*x)
+        out["logits_full"] = logits.numpy()
+        out["pooled_full"] = rec["pooled"].numpy()
+        out["feats"] = rec["feats"].numpy()
+        out["img_emb"] = rec["img_emb"].numpy()
+        te = rec["txt_emb"]
+        out["txt_emb_head"], out["txt_emb_tail"] = te[:, :4].numpy(), te[:, -4:].numpy()
+        out["txt_emb_sum"] = te.double().sum((1, 2)).numpy()
+        out["loss_eval"] = np.float64(model.compute_loss(logits, y, eval=True))
+        out["logits_img_only"] = model.forward_img_only(*x).numpy()
+        out["logits_txt_only"] = model.forward_txt_only(*x).numpy()
+        real_randperm = torch.randperm
+        for modal in ("image", "text"):
+            drawn = []
+
+            def rp(n, *a, **k):
+                r = real_randperm(n, *a, **k)
+                drawn.append(r.clone())
+                return r
+            torch.randperm = rp
+            try:
+                torch.manual_seed(77 if modal == "image" else 78)
+                out[f"logits_control_{modal}"] = model.forward_control(*x, modal).numpy()
+            finally:
+                torch.randperm = real_randperm
+            n = cfg.num_image_embeds + 1 if modal == "image" else T
+            idx = np.zeros(n + 1, dtype=np.int64)
+            idx[1:] = np.sort(drawn[0][:n].numpy() + 1)
+            out[f"indices_control_{modal}"] = idx
+    for h in hooks:
+        h.remove()
+    # train-mode step: BN batch statistics, dropout 0 (deterministic) -> loss + grad norms
+    model.train()
+    model.zero_grad()
+    loss = model.compute_loss(model(*x), y)
+    loss.backward()
+    names = [n for n, p in model.named_parameters()]
+    out["loss_train"] = np.float64(loss.detach())
+    out["grad_norms"] = np.array([float(p.grad.double().norm()) if p.grad is not None else 0.0
+                                  for _, p in model.named_parameters()])
+    out["clf_weight_grad"] = model.clf.weight.grad.numpy()
+    out["img_proj_bias_grad"] = model.enc.img_embeddings.img_embeddings.bias.grad.numpy()
+    os.makedirs(OUT, exist_ok=True)
+    np.savez_compressed(os.path.join(OUT, f"mmbt_{tag}.npz"), **out)
+    with open(os.path.join(OUT, f"mmbt_{tag}_keys.json"), "w") as f:
+        json.dump({"state_dict_keys": ref_keys, "named_parameters": names}, f)
+    print(f"wrote mmbt_{tag}: loss_eval={out['loss_eval']:.6f} loss_train={out['loss_train']:.6f}")
+
+
+def gen_framework():
+    from oracle.weights import SMALL
+    from oracle.tiny_model import TinyMMBT, tiny_batches, acc
+    _, framework, training_loop = _import_reference(SMALL, 0.0)
+    model = TinyMMBT()
+    opt = torch.optim.SGD(model.parameters(), lr=0.05, momentum=0.9)
+    sched = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, "max", patience=0, factor=0.5)
+    train, val, test = tiny_batches(3, seed=1), tiny_batches(2, seed=2), tiny_batches(2, seed=3)
+    H = {}
+    with tempfile.TemporaryDirectory() as d:
+        cbs = training_loop._construct_default_callbacks(model, opt, H, d, checkpoint_monitor="val_acc")
+        for c in cbs:
+            c.set_save_path(d)
+            c.set_model(model, ignore=False)
+            c.set_optimizer(opt)
+        m = framework.Model_(model=model, optimizer=opt, scheduler=sched,
+                             data_forming_func=lambda x, y, phase="train": (x, y), metrics=[acc])
+        for c in cbs:
+            c.set_model_pytoune(m)
+        m.train_loop(train, valid_generator=val, test_generator=test, steps_per_epoch=len(train),
+                     validation_steps=len(val), test_steps=len(test), epochs=2, callbacks=cbs, patience=10,
+                     epoch_start=1, scheduler_step_on="epoch", auc=False, vilt=False, mmbt=True,
+                     freeze_img=2, freeze_txt=3, gradient_accumulation_steps=2, scheduler_metric="val_acc")
+        files = sorted(os.listdir(d))
+        ck = torch.load(os.path.join(d, "model_last_epoch.pt"), weights_only=True)
+        import pandas as pd
+        csv_cols = list(pd.read_csv(os.path.join(d, "history.csv")).columns)
+    hist = {k: [float(v) if not isinstance(v, str) else v for v in vals] for k, vals in H.items()}
+    res = {"history": hist, "files": files, "ckpt_keys": sorted(ck.keys()),
+           "model_keys": list(ck["model"].keys()), "optimizer_state_keys": sorted(ck["optimizer"].keys()),
+           "csv_columns": csv_cols,
+           "final_params": {k: v.tolist() for k, v in model.state_dict().items()}}
+    with open(os.path.join(OUT, "framework_tiny.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print("wrote framework_tiny.json", files)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--what", default="all", choices=["all", "small", "full", "framework"])
+    a = ap.parse_args()
+    sys.path.insert(0, REPO)
+    from oracle.weights import SMALL, FULL
+    # each generator imports the reference fresh with its own stub config -> run each in a subprocess
+    if a.what == "all":
+        import subprocess
+        for w in ("small", "full", "framework"):
+            subprocess.check_call([sys.executable, "-m", "oracle.gen_golden", "--what", w], cwd=REPO)
+    elif a.what == "small":
+        gen_mmbt("small_t16", SMALL, B=2, T=16, lens=[16, 9], seed=0)
+    elif a.what == "full":
+        gen_mmbt("full_t508", FULL, B=2, T=508, lens=[508, 300], seed=1)
+    else:
+        gen_framework()

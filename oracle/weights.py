@@ -1,0 +1,185 @@
+"""Seeded weight recipe for MMBT (test infrastructure only, see oracle/__init__).
+
+Produces an ``OrderedDict`` whose keys/shapes are exactly the reference
+``MultimodalBertClf.state_dict()`` (src/mmbt.py:237-262):
+
+* ``enc.txt_embeddings.*``      pytorch_pretrained_bert BertEmbeddings (src/mmbt.py:91)
+* ``enc.img_embeddings.*``      ImageBertEmbeddings (src/mmbt.py:47-56); the word /
+                                position / token-type / LayerNorm tensors are the SAME
+                                tensors as the text embeddings (shared modules,
+                                src/mmbt.py:52-55), emitted under both names.
+* ``enc.img_encoder.model.N.*`` resnet152 children[:-2] (src/mmbt.py:19-21)
+* ``enc.encoder.layer.i.*``     BertEncoder (src/mmbt.py:95)
+* ``enc.pooler.dense.*``        BertPooler (src/mmbt.py:96)
+* ``clf.*``                     nn.Linear(hidden, n_classes) (src/mmbt.py:242)
+
+Every tensor is drawn from its own generator seeded by (seed, crc32(name)), so
+the values do not depend on key order or on which subset is generated.
+The recipe is the build's own (no pretrained weights exist offline): BERT
+weights N(0, std), biases and LayerNorm params perturbed away from 0/1 so that
+bias/affine bugs cannot hide; ResNet convs He-normal (fan_out), BN affine and
+running stats perturbed, last BN of each bottleneck damped to keep the eval-mode
+residual stream bounded.
+"""
+import math
+import zlib
+from collections import OrderedDict
+from dataclasses import dataclass, field
+
+import torch
+
+
+@dataclass(frozen=True)
+class MMBTConfig:
+    n_layers: int = 12
+    hidden: int = 768
+    heads: int = 12
+    inter: int = 3072
+    vocab: int = 30522
+    max_pos: int = 512
+    type_vocab: int = 2
+    n_classes: int = 101
+    num_image_embeds: int = 3
+    img_hidden: int = 2048
+    resnet_blocks: tuple = (3, 8, 36, 3)
+    cls_id: int = 101   # bert-base-uncased "[CLS]"
+    sep_id: int = 102   # bert-base-uncased "[SEP]"
+    ln_eps: float = 1e-12
+    bert_std: float = 0.02
+
+
+FULL = MMBTConfig()
+# reduced configs keep the per-layer shapes (768/12/3072) so kernels see real widths
+SMALL = MMBTConfig(n_layers=2, vocab=4096, resnet_blocks=(1, 1, 1, 1))
+
+
+def _gen(seed, name):
+    g = torch.Generator()
+    g.manual_seed((int(seed) * 1000003 + zlib.crc32(name.encode())) & 0x7FFFFFFFFFFF)
+    return g
+
+
+def resnet_key_shapes(cfg):
+    """(name, shape, kind) for torchvision resnet152 children[:-2] as Sequential indices."""
+    out = [("0.weight", (64, 3, 7, 7), "conv")]
+    out += [(f"1.{n}", (64,), k) for n, k in (("weight", "bn_w"), ("bias", "bn_b"),
+            ("running_mean", "bn_rm"), ("running_var", "bn_rv"))]
+    out += [("1.num_batches_tracked", (), "bn_nbt")]
+    inplanes = 64
+    for li, (planes, nblk) in enumerate(zip((64, 128, 256, 512), cfg.resnet_blocks)):
+        for b in range(nblk):
+            p = f"{4 + li}.{b}"
+            width, outp = planes, planes * 4
+            convs = [("conv1", (width, inplanes, 1, 1), "bn1"),
+                     ("conv2", (width, width, 3, 3), "bn2"),
+                     ("conv3", (outp, width, 1, 1), "bn3")]
+            for cname, shp, bname in convs:
+                out.append((f"{p}.{cname}.weight", shp, "conv"))
+                c = shp[0]
+                last = "_last" if bname == "bn3" else ""
+                out += [(f"{p}.{bname}.weight", (c,), "bn_w" + last), (f"{p}.{bname}.bias", (c,), "bn_b"),
+                        (f"{p}.{bname}.running_mean", (c,), "bn_rm"),
+                        (f"{p}.{bname}.running_var", (c,), "bn_rv"),
+                        (f"{p}.{bname}.num_batches_tracked", (), "bn_nbt")]
+            if b == 0:
+                out.append((f"{p}.downsample.0.weight", (outp, inplanes, 1, 1), "conv"))
+                out += [(f"{p}.downsample.1.weight", (outp,), "bn_w"), (f"{p}.downsample.1.bias", (outp,), "bn_b"),
+                        (f"{p}.downsample.1.running_mean", (outp,), "bn_rm"),
+                        (f"{p}.downsample.1.running_var", (outp,), "bn_rv"),
+                        (f"{p}.downsample.1.num_batches_tracked", (), "bn_nbt")]
+            inplanes = outp
+    return out
+
+
+def bert_emb_key_shapes(cfg):
+    H = cfg.hidden
+    return [("word_embeddings.weight", (cfg.vocab, H), "emb"),
+            ("position_embeddings.weight", (cfg.max_pos, H), "emb"),
+            ("token_type_embeddings.weight", (cfg.type_vocab, H), "emb"),
+            ("LayerNorm.weight", (H,), "ln_w"), ("LayerNorm.bias", (H,), "ln_b")]
+
+
+def bert_layer_key_shapes(cfg, i):
+    H, I = cfg.hidden, cfg.inter
+    p = f"layer.{i}"
+    return [(f"{p}.attention.self.query.weight", (H, H), "w"), (f"{p}.attention.self.query.bias", (H,), "b"),
+            (f"{p}.attention.self.key.weight", (H, H), "w"), (f"{p}.attention.self.key.bias", (H,), "b"),
+            (f"{p}.attention.self.value.weight", (H, H), "w"), (f"{p}.attention.self.value.bias", (H,), "b"),
+            (f"{p}.attention.output.dense.weight", (H, H), "w"), (f"{p}.attention.output.dense.bias", (H,), "b"),
+            (f"{p}.attention.output.LayerNorm.weight", (H,), "ln_w"),
+            (f"{p}.attention.output.LayerNorm.bias", (H,), "ln_b"),
+            (f"{p}.intermediate.dense.weight", (I, H), "w"), (f"{p}.intermediate.dense.bias", (I,), "b"),
+            (f"{p}.output.dense.weight", (H, I), "w"), (f"{p}.output.dense.bias", (H,), "b"),
+            (f"{p}.output.LayerNorm.weight", (H,), "ln_w"), (f"{p}.output.LayerNorm.bias", (H,), "ln_b")]
+
+
+def key_shapes(cfg=FULL):
+    """All state_dict entries in reference order: (key, shape, kind, alias_of)."""
+    H = cfg.hidden
+    out = []
+    for n, s, k in bert_emb_key_shapes(cfg):
+        out.append((f"enc.txt_embeddings.{n}", s, k, None))
+    out.append(("enc.img_embeddings.img_embeddings.weight", (H, cfg.img_hidden), "w", None))
+    out.append(("enc.img_embeddings.img_embeddings.bias", (H,), "b", None))
+    for n in ("position_embeddings.weight", "token_type_embeddings.weight", "word_embeddings.weight",
+              "LayerNorm.weight", "LayerNorm.bias"):
+        out.append((f"enc.img_embeddings.{n}", None, None, f"enc.txt_embeddings.{n}"))
+    for n, s, k in resnet_key_shapes(cfg):
+        out.append((f"enc.img_encoder.model.{n}", s, k, None))
+    for i in range(cfg.n_layers):
+        for n, s, k in bert_layer_key_shapes(cfg, i):
+            out.append((f"enc.encoder.{n}", s, k, None))
+    out.append(("enc.pooler.dense.weight", (H, H), "w", None))
+    out.append(("enc.pooler.dense.bias", (H,), "b", None))
+    out.append(("clf.weight", (cfg.n_classes, H), "w", None))
+    out.append(("clf.bias", (cfg.n_classes,), "b", None))
+    return out
+
+
+def _draw(name, shape, kind, seed, cfg):
+    g = _gen(seed, name)
+    if kind == "bn_nbt":
+        return torch.zeros((), dtype=torch.long)
+    t = torch.empty(shape, dtype=torch.float32)
+    if kind in ("w", "emb"):
+        t.normal_(0.0, cfg.bert_std, generator=g)
+    elif kind == "b":
+        t.normal_(0.0, cfg.bert_std, generator=g)
+    elif kind == "ln_w":
+        t.normal_(1.0, 0.05, generator=g)
+    elif kind == "ln_b":
+        t.normal_(0.0, 0.05, generator=g)
+    elif kind == "conv":
+        fan_out = shape[0] * shape[2] * shape[3]
+        t.normal_(0.0, math.sqrt(2.0 / fan_out), generator=g)
+    elif kind == "bn_w":
+        t.normal_(1.0, 0.05, generator=g)
+    elif kind == "bn_w_last":
+        t.normal_(0.3, 0.02, generator=g)
+    elif kind == "bn_b":
+        t.normal_(0.0, 0.05, generator=g)
+    elif kind == "bn_rm":
+        t.normal_(0.0, 0.1, generator=g)
+    elif kind == "bn_rv":
+        t.uniform_(0.5, 1.5, generator=g)
+    else:
+        raise ValueError(kind)
+    return t
+
+
+def make_state_dict(seed=0, cfg=FULL):
+    sd = OrderedDict()
+    for key, shape, kind, alias in key_shapes(cfg):
+        sd[key] = sd[alias] if alias is not None else _draw(key, shape, kind, seed, cfg)
+    return sd
+
+
+def checksum(sd):
+    """float64 sum of |w| over unique tensors -- catches RNG drift between machines."""
+    seen, tot = set(), 0.0
+    for v in sd.values():
+        if id(v) in seen or not v.is_floating_point():
+            continue
+        seen.add(id(v))
+        tot += float(v.double().abs().sum())
+    return tot
