@@ -1,0 +1,198 @@
+/*
+ * mmu.h -- C-ABI of libmmu_hip.so, the MI355X (gfx950) kernels of the MMBT
+ * multimodal train / uncertainty-eval hot path.
+ *
+ * Reference being replaced (wooginawunan/multi-modal-uncertainty @ /root/reference,
+ * pure PyTorch; its math lives in torchvision + pytorch_pretrained_bert 0.6.x):
+ * every entry point below names the reference call it replaces (file:line).
+ *
+ * Conventions
+ *   - Plain pointers + int64 sizes; no framework types.  All device buffers are
+ *     owned by the caller; the library never allocates or frees device memory.
+ *   - Work is enqueued on the caller's `stream` (a hipStream_t); no device sync.
+ *   - Return 0 on success, nonzero on a bad argument / launch failure; the
+ *     message is in mmu_last_error() (thread-local).
+ *   - bf16 = IEEE bfloat16 bits (uint16), f32 = float.  Master weights, biases,
+ *     LayerNorm params and all gradients of parameters are f32.
+ *   - "additive key mask" = per (row, key) float added to the attention scores,
+ *     0 for a real token and -10000 for a pad (src/mmbt.py:101-112).
+ */
+#ifndef MMU_H
+#define MMU_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* mmu_stream_t; /* hipStream_t */
+
+enum { MMU_BF16 = 0, MMU_F32 = 1 };
+
+/* ------------------------------------------------------------------ status */
+int mmu_version(void);
+const char* mmu_last_error(void);
+
+/* ------------------------------------------------------------------ GEMM
+ * C[m,n] (op)= sum_k A(m,k) * B(n,k), batched over `batch` with element strides.
+ *   A(m,k) = A[m*lda + k] if a_kmajor else A[k*lda + m]      (bf16)
+ *   B(n,k) = B[n*ldb + k] if b_kmajor else B[k*ldb + n]      (bf16)
+ * Replaces the nn.Linear forward / backward products of pytorch_pretrained_bert
+ * BertSelfAttention (query/key/value), BertSelfOutput.dense, BertIntermediate.dense,
+ * BertOutput.dense (encoder call: src/mmbt.py:124-126) and the image projection
+ * ImageBertEmbeddings.img_embeddings (src/mmbt.py:51,71).
+ * Constraints: N % 128 == 0; K % 64 == 0 when an operand is K-major;
+ *              M % 128 == 0 when A is M-major (not K-major).
+ */
+enum {
+  MMU_EPI_STORE = 0,        /* C = acc (+bias[n]) (+C if accumulate)                     */
+  MMU_EPI_BIAS_GELU = 1,    /* aux = bf16(acc+bias); C = gelu_erf(acc+bias)              */
+  MMU_EPI_BIAS_DROP_RES = 2,/* C = residual + dropout(acc+bias)                          */
+  MMU_EPI_DGELU = 3,        /* C = acc * gelu'(aux)                                      */
+  MMU_EPI_ADD_RES = 4       /* C = acc + residual                                        */
+};
+typedef struct mmu_epilogue {
+  int32_t kind;
+  int32_t accumulate;       /* STORE only: C += result (f32 C)                         */
+  const float* bias;        /* [N] f32 or NULL                                          */
+  int64_t bias_bstride;
+  const void* residual;     /* bf16 [M, ldr]                                            */
+  int64_t ldr, res_bstride;
+  void* aux;                /* bf16 [M, ldx]: GELU pre-activation (written or read)     */
+  int64_t ldx, aux_bstride;
+  float* colsum;            /* f32 partial column sums of the final C, [2*ceil(M/128), N] per batch */
+  int64_t colsum_bstride;
+  float drop_p;             /* BIAS_DROP_RES                                            */
+  uint64_t seed;            /* dropout stream: element (m, n) uses counter m*N+n        */
+} mmu_epilogue;
+
+int mmu_gemm(const void* A, int64_t lda, int a_kmajor,
+             const void* B, int64_t ldb, int b_kmajor,
+             void* C, int64_t ldc, int c_dtype,
+             int64_t M, int64_t N, int64_t K,
+             int64_t batch, int64_t strideA, int64_t strideB, int64_t strideC,
+             const mmu_epilogue* epi, mmu_stream_t stream);
+
+/* Sum `parts` rows of a [parts, N] f32 partial table into out[N] (+= if accumulate). */
+int mmu_colsum_reduce(const float* partial, int64_t parts, int64_t N, float* out,
+                      int accumulate, mmu_stream_t stream);
+/* Column sums of a bf16 [M, N] matrix into out[N] f32 (+= if accumulate), via
+ * `partial` workspace of [ceil(M/256), N] f32 (bias grad of the fused QKV projection). */
+int mmu_colsum_bf16(const void* X, int64_t M, int64_t N, int64_t ldx, float* partial,
+                    float* out, int accumulate, mmu_stream_t stream);
+
+/* ------------------------------------------------------------------ attention
+ * softmax(Q K^T / sqrt(64) + keymask) (dropout) V for 12 x 64 heads, Q/K/V read from
+ * the token-major fused projection QKV[rows, ld_qkv] (q at col h*64, k at 768+h*64,
+ * v at 1536+h*64).  Replaces pytorch_pretrained_bert BertSelfAttention scores /
+ * softmax / dropout / context (inside the encoder call src/mmbt.py:124-126).
+ *   O   [rows, ld_o] bf16 (col h*64)   LSE [batch*heads, L] f32 (natural log-sum-exp
+ *   of the scaled+masked scores).  keymask [batch, L] f32 additive.
+ */
+int mmu_attention_fwd(const void* QKV, int64_t ld_qkv, const float* keymask,
+                      void* O, int64_t ld_o, float* LSE,
+                      int64_t batch, int64_t L, int64_t heads,
+                      float drop_p, uint64_t seed, mmu_stream_t stream);
+/* dQKV [rows, ld_dqkv] bf16 from dO; `delta` workspace [batch*heads, L] f32. */
+int mmu_attention_bwd(const void* QKV, int64_t ld_qkv, const float* keymask,
+                      const void* O, int64_t ld_o, const void* dO, int64_t ld_do,
+                      const float* LSE, float* delta, void* dQKV, int64_t ld_dqkv,
+                      int64_t batch, int64_t L, int64_t heads,
+                      float drop_p, uint64_t seed, mmu_stream_t stream);
+
+/* ------------------------------------------------------------------ LayerNorm
+ * y = LN(x) * w + b over the last dim (768), eps; x, y bf16 [rows, H]; saves
+ * mean/rstd f32 [rows].  BertLayerNorm of BertSelfOutput / BertOutput
+ * (src/mmbt.py:124-126).
+ */
+int mmu_layernorm_fwd(const void* X, const float* w, const float* b, void* Y,
+                      float* mean, float* rstd, int64_t rows, int64_t H, float eps,
+                      mmu_stream_t stream);
+/* Backward of y = LN(x): dX = LN'(dY) (+ dRes), optional dXdrop = dropout_bwd(dX)
+ * (same (seed, m*H+n) stream as the producing BIAS_DROP_RES epilogue), and partial
+ * column sums [ceil(rows/rows_per_part), H] for dgamma, dbeta and dbias
+ * (= column sum of dXdrop, or of dX when no dropout output). */
+int mmu_layernorm_bwd(const void* dY, const void* X, const float* mean, const float* rstd,
+                      const float* w, void* dX, void* dXdrop, float drop_p, uint64_t seed,
+                      float* part_dw, float* part_db, float* part_dbias,
+                      int64_t rows, int64_t H, int64_t rows_per_part, mmu_stream_t stream);
+
+/* ------------------------------------------------------------------ embeddings
+ * Modality-token embed + text gather + concat/gather, one pass
+ * (ImageBertEmbeddings src/mmbt.py:58-83, BertEmbeddings src/mmbt.py:121,
+ *  torch.cat src/mmbt.py:122, control gather src/mmbt.py:198-229).
+ * Source sequence s of length S = n_img+2+T: s=0 [CLS], 1..n_img image proj rows,
+ * n_img+1 [SEP] (positions 0..n_img+1, token type 0), then text t at position t,
+ * type seg[b,t].  Output row (v,b,j) embeds source position idx[v*Lout + j]
+ * (idx == NULL: identity, Lout == S) and is LayerNorm'ed.  X [V*B*Lout, H] bf16;
+ * keymask [V*B, Lout] f32 additive; mean/rstd (optional) f32 [V*B*Lout] for backward.
+ * Dropout after the LN: drop_img on the image-segment rows (ImageBertEmbeddings.dropout,
+ * args.dropout), drop_txt on text rows (BertEmbeddings.dropout 0.1); counter row*768+col.
+ * Tables f32: word [vocab,H], pos [maxpos,H], type [2,H]; proj f32 [B, n_img, H].
+ */
+int mmu_embed_fwd(const int64_t* ids, const int64_t* seg, const int64_t* txt_mask,
+                  const float* proj, const float* word, const float* pos, const float* type,
+                  const float* ln_w, const float* ln_b, float eps,
+                  int64_t cls_id, int64_t sep_id,
+                  const int64_t* idx, int64_t V, int64_t B, int64_t T, int64_t n_img, int64_t Lout,
+                  int64_t H, float drop_txt, float drop_img, uint64_t seed,
+                  void* X, float* keymask, float* mean, float* rstd, mmu_stream_t stream);
+/* Backward of mmu_embed_fwd for the identity variant (training): recomputes the
+ * pre-LN sums, LN backward, then scatters: word rows by atomics, position / type
+ * / [CLS] / [SEP] by batch reduction, image rows to dproj f32 [B, n_img, H].
+ * ws: f32 workspace of B*S*H + 2*ceil(B*S/64)*H floats. */
+int mmu_embed_bwd(const void* dX, const int64_t* ids, const int64_t* seg,
+                  const float* proj, const float* word, const float* pos, const float* type,
+                  const float* ln_w, const float* mean, const float* rstd,
+                  int64_t cls_id, int64_t sep_id, int64_t B, int64_t T, int64_t n_img, int64_t H,
+                  float drop_txt, float drop_img, uint64_t seed, float* d_word, float* d_pos, float* d_type, float* d_ln_w, float* d_ln_b,
+                  float* d_proj, float* ws, mmu_stream_t stream);
+
+/* AdaptiveAvgPool2d((n,1)) + flatten + transpose of the ResNet map
+ * (src/mmbt.py:30,42-44): fmap NHWC bf16 [B,Hh,Ww,C] -> out f32 [B,n,C]; and its backward. */
+int mmu_row_pool_fwd(const void* fmap, int64_t B, int64_t Hh, int64_t Ww, int64_t C, int64_t n,
+                     float* out, mmu_stream_t stream);
+int mmu_row_pool_bwd(const float* dout, int64_t B, int64_t Hh, int64_t Ww, int64_t C, int64_t n,
+                     void* dfmap, mmu_stream_t stream);
+
+/* ------------------------------------------------------------------ BertAdam
+ * Fused multi-tensor BertAdam (pytorch_pretrained_bert 0.6.x, constructed at
+ * train.py:142-147; stepped at src/framework.py:303): per-tensor clip
+ * (max_grad_norm), m/v update without bias correction, decoupled weight decay
+ * (group 0 only), lr * warmup_linear(step/t_total) with the per-tensor step read
+ * before its increment, optional bf16 copy of the updated weight for the GEMMs.
+ * table (int64, device): 7 per tensor {offset, numel, group (0 decay / 1 no decay),
+ *   bf16_offset (-1 = none), active (0 = skipped like a None grad), first_chunk,
+ *   n_chunks}, followed by 3 per chunk {tensor, start, len}.
+ * steps int32 [n_tensors] (device, incremented); ws f32 >= n_chunks + 2*n_tensors.
+ */
+int mmu_bertadam_step(float* params, const float* grads, float* m, float* v, void* bf16_copy,
+                      const int64_t* table, int32_t* steps, int64_t n_tensors, int64_t n_chunks,
+                      float lr_decay, float lr_nodecay, float wd, float warmup, float t_total,
+                      float b1, float b2, float eps, float max_grad_norm,
+                      float* ws, int64_t ws_floats, mmu_stream_t stream);
+
+/* ------------------------------------------------------------------ uncertainty
+ * logits f32 [S, R, C] (R = members x passes per sample) ->
+ * p_bar f32 [S, C] = mean_r softmax(logits[s, r]); per-sample nll [S] = -log p_bar[y];
+ * conf [S], correct [S].  ECE is then binned from conf/correct (mmu_ece_bins).
+ * North-star metrics; softmax-then-mean convention of
+ * notebooks/food101_robustness.py:25-36.
+ */
+int mmu_uncertainty(const float* logits, const int64_t* y, int64_t S, int64_t R, int64_t C,
+                    float* p_bar, float* nll, float* conf, float* correct, mmu_stream_t stream);
+/* 15-style equal-width bins: out f32 [3*n_bins] = (count, sum conf, sum correct). */
+int mmu_ece_bins(const float* conf, const float* correct, int64_t S, int64_t n_bins,
+                 float* out, mmu_stream_t stream);
+
+/* ------------------------------------------------------------------ timing
+ * Device-time of every mmu_gemm launch while enabled, bracketed by HIP events on
+ * the launch stream (bench.py roofline).  Reads back (host sync) only in _read.
+ */
+int mmu_timing_enable(int on);
+int mmu_timing_read(double* total_ms, int64_t* launches, double* flops);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMU_H */

@@ -1,0 +1,486 @@
+// Flash-style BERT self-attention (12 heads x 64) for gfx950, fwd + bwd.
+//
+// Replaces pytorch_pretrained_bert BertSelfAttention's scores / softmax / dropout /
+// context product (called inside the encoder, src/mmbt.py:124-126).  Semantics:
+//   P = softmax(Q K^T / 8 + keymask),  O = dropout(P) V     (keymask: 0 or -10000)
+// Keys beyond L (tile tails) are excluded exactly (-inf), rows beyond L are not stored.
+//
+// All products use v_mfma_f32_32x32x16_bf16 in the "swapped" orientation: the
+// score tile is S^T = K Q^T (keys on registers, queries on lanes), so each lane
+// owns one query row: softmax max/sum are in-lane plus one xor-32 shuffle, and
+// P feeds the next MFMA straight from its accumulator registers (no LDS trip).
+//   fwd : S^T = K.Q^T ; O^T += V^T.P^T           (V^T fragment by ds_read_b64_tr_b16)
+//   dQ  : S^T, dP^T = V.dO^T ; dQ^T += K^T.dS^T
+//   dKdV: S = Q.K^T, dP = dO.V^T (keys on lanes) ; dV += P^T.dO ; dK += dS^T.Q
+// LDS tiles are [rows][64 d] bf16 (128-B rows) with the 16-B chunk index XORed by
+// f(row) = ((row>>1)&1)<<2 | ((row>>3)&3): conflict-free for both the row reads
+// (ds_read_b128) and the transposed reads (checked by enumeration).
+//
+// Dropout: element (q, key) of head-row bh draws 16 bits from
+// lowbias32(((q*Lp + key) >> 1) ^ seed_bh), low/high half by key parity; dropped
+// when < round(p*65536).  fwd, dQ and dKdV regenerate identical masks.
+#include "mmu_common.h"
+#include "mmu_internal.h"
+
+namespace mmu {
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+constexpr float NEG_INF = -__builtin_huge_valf();
+
+static __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+static __device__ __forceinline__ uint32_t seed_for(uint64_t seed, int bh) {
+  return lowbias32((uint32_t)seed ^ lowbias32((uint32_t)(seed >> 32) + 0x9E3779B9u * (uint32_t)(bh + 1)));
+}
+// keep bits for keys (key, key+1) of query q (key even)
+static __device__ __forceinline__ uint32_t drop_pair(uint32_t sbh, uint32_t q, uint32_t key, uint32_t Lp) {
+  return lowbias32(((q * Lp + key) >> 1) ^ sbh);
+}
+static __device__ __forceinline__ bool keep_elem(uint32_t sbh, uint32_t q, uint32_t key, uint32_t Lp, uint32_t thr) {
+  uint32_t h = drop_pair(sbh, q, key & ~1u, Lp);
+  return ((h >> ((key & 1) * 16)) & 0xFFFFu) >= thr;
+}
+
+static __device__ __forceinline__ int fsw(int r) { return (((r >> 1) & 1) << 2) | ((r >> 3) & 3); }
+static __device__ __forceinline__ int tile_off(int row, int chunk) { return row * 128 + ((chunk ^ fsw(row)) << 4); }
+
+// operand fragment of v_mfma_f32_32x32x16_bf16, K-contiguous tile: lane l holds
+// tile[row0 + (l&31)][16ks + 8(l>>5) + j]
+static __device__ __forceinline__ bf16x8 row_frag(const char* s, int row0, int ks, int l) {
+  return *(const bf16x8*)(s + tile_off(row0 + (l & 31), 2 * ks + (l >> 5)));
+}
+// transposed fragment matching an accumulator used as the other operand: lane l holds
+// tile[row0 + 16s + 8(j>>2) + 4h + (j&3)][col0 + (l&31)], h = l>>5  (row0 includes 16s)
+static __device__ __forceinline__ bf16x8 tr_frag(const char* s, int row0, int col0, int l) {
+  const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3, h = g >> 1;
+  const int col = col0 + 16 * (g & 1) + 4 * p;  // element column
+  const int r0 = row0 + 4 * h + q, r1 = r0 + 8;
+  const int cb = col * 2;
+  const char* a0 = s + tile_off(r0, cb >> 4) + (cb & 15);
+  const char* a1 = s + tile_off(r1, cb >> 4) + (cb & 15);
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((MMU_LDS(bf16x4)*)a0);
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((MMU_LDS(bf16x4)*)a1);
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+// 8 accumulator registers (8s..8s+7) -> bf16 operand fragment
+static __device__ __forceinline__ bf16x8 acc_frag(const f32x16& a, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = f2bf(a[8 * s + j]);
+  return r;
+}
+static __device__ __forceinline__ bf16x8 scale_frag(uint4 u, float sc) {
+  bf16x8 v = *(bf16x8*)&u;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = f2bf(bf2f(v[j]) * sc);
+  return v;
+}
+
+// ---- cooperative [ROWS][64] tile loader (register staged), rows >= L zero-filled
+template <int ROWS, int NT>
+struct TileLoader {
+  static constexpr int PER = ROWS * 8 / NT;  // 16-B chunks per thread
+  uint4 r[PER];
+  __device__ __forceinline__ void load(const bf16* base, int64_t ld, int row0, int L, int t) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int idx = t + NT * i, row = idx >> 3, c = idx & 7;
+      r[i] = (row0 + row < L) ? *(const uint4*)(base + (int64_t)(row0 + row) * ld + 8 * c) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(char* s, int t, float sc = 1.0f) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int idx = t + NT * i, row = idx >> 3, c = idx & 7;
+      uint4 v = r[i];
+      if (sc != 1.0f) { bf16x8 f = scale_frag(v, sc); v = *(uint4*)&f; }
+      *(uint4*)(s + tile_off(row, c)) = v;
+    }
+  }
+};
+
+// =============================================================================== forward
+// grid (ceil(L/128), batch*heads), 256 threads; wave w owns queries [blk*128 + 32w, +32)
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
+  constexpr int KV = 64, TILE = KV * 128;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE + 2 * KV * 4];
+  float* maskL = (float*)(smem + 4 * TILE);
+  const int t = threadIdx.x, l = t & 63, w = t >> 6, h = l >> 5;
+  const int bh = blockIdx.y, b = bh / p.heads, hd = bh - b * p.heads;
+  const int L = p.L, HD = p.heads * 64;
+  const int q0w = blockIdx.x * 128 + 32 * w, q = q0w + (l & 31);
+  const bool wave_live = q0w < L;
+  const bf16* base = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64;
+  const bf16* Kb = base + HD;
+  const bf16* Vb = base + 2 * HD;
+  const float* km = p.keymask + (int64_t)b * L;
+  const uint32_t sbh = seed_for(p.seed, bh), Lp = (uint32_t)((L + 1) & ~1);
+  const uint32_t thr = (uint32_t)(p.drop_p * 65536.0f + 0.5f);
+
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    uint4 u = q < L ? *(const uint4*)(base + (int64_t)q * p.ld_qkv + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
+    qf[ks] = scale_frag(u, 0.125f);
+  }
+  f32x16 o[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
+  float m_run = NEG_INF, l_run = 0.f;
+
+  TileLoader<KV, 256> lk, lv;
+  const int nkv = (L + KV - 1) / KV;
+  lk.load(Kb, p.ld_qkv, 0, L, t);
+  lv.load(Vb, p.ld_qkv, 0, L, t);
+  lk.store(smem, t);
+  lv.store(smem + TILE, t);
+  if (t < KV) maskL[t] = t < L ? km[t] * LOG2E : NEG_INF;
+  __syncthreads();
+
+  for (int j = 0; j < nkv; ++j) {
+    const int stg = j & 1;
+    const char* Ks = smem + stg * 2 * TILE;
+    const char* Vs = Ks + TILE;
+    const float* mk = maskL + stg * KV;
+    const bool more = j + 1 < nkv;
+    float mnext = 0.f;
+    if (more) {
+      lk.load(Kb, p.ld_qkv, (j + 1) * KV, L, t);
+      lv.load(Vb, p.ld_qkv, (j + 1) * KV, L, t);
+      if (t < KV) { int key = (j + 1) * KV + t; mnext = key < L ? km[key] * LOG2E : NEG_INF; }
+    }
+    if (wave_live) {
+      f32x16 sc[2];
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[st][i] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          sc[st] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ks, 32 * st, ks, l), qf[ks], sc[st], 0, 0, 0);
+      }
+      float mx = NEG_INF;
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          int key = 32 * st + (r & 3) + 8 * (r >> 2) + 4 * h;
+          float s = sc[st][r] * LOG2E + mk[key];
+          sc[st][r] = s;
+          mx = fmaxf(mx, s);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m_run, mx);
+      const float alpha = m_run == NEG_INF ? 0.f : exp2f(m_run - mnew);
+      float rs = 0.f;
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float e = exp2f(sc[st][r] - mnew);
+          sc[st][r] = e;
+          rs += e;
+        }
+      rs += __shfl_xor(rs, 32, 64);
+      l_run = l_run * alpha + rs;
+      m_run = mnew;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+      if (thr) {
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const uint32_t key = j * KV + 32 * st + 8 * g + 4 * h;
+            uint32_t h0 = drop_pair(sbh, q, key, Lp), h1 = drop_pair(sbh, q, key + 2, Lp);
+            if ((h0 & 0xFFFFu) < thr) sc[st][4 * g + 0] = 0.f;
+            if ((h0 >> 16) < thr) sc[st][4 * g + 1] = 0.f;
+            if ((h1 & 0xFFFFu) < thr) sc[st][4 * g + 2] = 0.f;
+            if ((h1 >> 16) < thr) sc[st][4 * g + 3] = 0.f;
+          }
+      }
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 pf = acc_frag(sc[st], s2);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt)
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Vs, 32 * st + 16 * s2, 32 * dt, l), pf, o[dt], 0, 0, 0);
+        }
+    }
+    if (more) {
+      char* dK = smem + (stg ^ 1) * 2 * TILE;
+      lk.store(dK, t);
+      lv.store(dK + TILE, t);
+      if (t < KV) maskL[(stg ^ 1) * KV + t] = mnext;
+    }
+    __syncthreads();
+  }
+  if (!wave_live || q >= L) return;
+  const float inv = (p.drop_p > 0.f ? 1.0f / (1.0f - p.drop_p) : 1.0f) / l_run;
+  bf16* ob = p.out + ((int64_t)b * L + q) * p.ld_out + hd * 64;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 v = {f2bf(o[dt][4 * g] * inv), f2bf(o[dt][4 * g + 1] * inv), f2bf(o[dt][4 * g + 2] * inv),
+                  f2bf(o[dt][4 * g + 3] * inv)};
+      *(bf16x4*)(ob + 32 * dt + 8 * g + 4 * h) = v;
+    }
+  if (h == 0) p.lse[(int64_t)bh * L + q] = m_run * LN2 + logf(l_run);
+}
+
+// =============================================================================== backward
+// delta[bh, q] = sum_d dO[q, d] * O[q, d]   (one wave per (bh, 8 rows))
+__global__ __launch_bounds__(256) void attn_delta_kernel(AttnParams p) {
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int bh = blockIdx.y, b = bh / p.heads, hd = bh - b * p.heads;
+  const int row = blockIdx.x * 32 + w * 8 + (l >> 3);
+  if (row >= p.L) return;
+  const int c = (l & 7) * 8;
+  const int64_t tok = (int64_t)b * p.L + row;
+  bf16x8 a = *(const bf16x8*)(p.o + tok * p.ld_o + hd * 64 + c);
+  bf16x8 d = *(const bf16x8*)(p.dout + tok * p.ld_do + hd * 64 + c);
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s += bf2f(a[e]) * bf2f(d[e]);
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  s += __shfl_xor(s, 4, 64);
+  if ((l & 7) == 0) p.delta[(int64_t)bh * p.L + row] = s;
+}
+
+// dQ: grid (ceil(L/128), batch*heads), 256 threads, wave owns 32 queries; loops over 64-key tiles
+__global__ __launch_bounds__(256) void attn_dq_kernel(AttnParams p) {
+  constexpr int KV = 64, TILE = KV * 128;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE + 2 * KV * 4];
+  float* maskL = (float*)(smem + 4 * TILE);
+  const int t = threadIdx.x, l = t & 63, w = t >> 6, h = l >> 5;
+  const int bh = blockIdx.y, b = bh / p.heads, hd = bh - b * p.heads;
+  const int L = p.L, HD = p.heads * 64;
+  const int q0w = blockIdx.x * 128 + 32 * w, q = q0w + (l & 31);
+  const bool wave_live = q0w < L, qv = q < L;
+  const bf16* base = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64;
+  const bf16* Kb = base + HD;
+  const bf16* Vb = base + 2 * HD;
+  const float* km = p.keymask + (int64_t)b * L;
+  const uint32_t sbh = seed_for(p.seed, bh), Lp = (uint32_t)((L + 1) & ~1);
+  const uint32_t thr = (uint32_t)(p.drop_p * 65536.0f + 0.5f);
+  const float zs = p.drop_p > 0.f ? 1.0f / (1.0f - p.drop_p) : 1.0f;
+
+  bf16x8 qf[4], df[4];
+  const bf16* dob = p.dout + ((int64_t)b * L + q) * p.ld_do + hd * 64;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    uint4 u = qv ? *(const uint4*)(base + (int64_t)q * p.ld_qkv + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
+    qf[ks] = scale_frag(u, 0.125f);
+    uint4 v = qv ? *(const uint4*)(dob + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
+    df[ks] = *(bf16x8*)&v;
+  }
+  const float lse2 = qv ? p.lse[(int64_t)bh * L + q] * LOG2E : __builtin_huge_valf();
+  const float dlt = qv ? p.delta[(int64_t)bh * L + q] : 0.f;
+  f32x16 dq[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { dq[0][i] = 0.f; dq[1][i] = 0.f; }
+
+  TileLoader<KV, 256> lk, lv;
+  const int nkv = (L + KV - 1) / KV;
+  lk.load(Kb, p.ld_qkv, 0, L, t);
+  lv.load(Vb, p.ld_qkv, 0, L, t);
+  lk.store(smem, t);
+  lv.store(smem + TILE, t);
+  if (t < KV) maskL[t] = t < L ? km[t] * LOG2E : NEG_INF;
+  __syncthreads();
+  for (int j = 0; j < nkv; ++j) {
+    const int stg = j & 1;
+    const char* Ks = smem + stg * 2 * TILE;
+    const char* Vs = Ks + TILE;
+    const float* mk = maskL + stg * KV;
+    const bool more = j + 1 < nkv;
+    float mnext = 0.f;
+    if (more) {
+      lk.load(Kb, p.ld_qkv, (j + 1) * KV, L, t);
+      lv.load(Vb, p.ld_qkv, (j + 1) * KV, L, t);
+      if (t < KV) { int key = (j + 1) * KV + t; mnext = key < L ? km[key] * LOG2E : NEG_INF; }
+    }
+    if (wave_live) {
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        f32x16 sc, dp;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { sc[i] = 0.f; dp[i] = 0.f; }
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ks, 32 * st, ks, l), qf[ks], sc, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Vs, 32 * st, ks, l), df[ks], dp, 0, 0, 0);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const uint32_t key = j * KV + 32 * st + 8 * g + 4 * h;
+          uint32_t h0 = 0xFFFFFFFFu, h1 = 0xFFFFFFFFu;
+          if (thr) { h0 = drop_pair(sbh, q, key, Lp); h1 = drop_pair(sbh, q, key + 2, Lp); }
+          const uint32_t bits[4] = {h0 & 0xFFFFu, h0 >> 16, h1 & 0xFFFFu, h1 >> 16};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g + e;
+            const int kl = 32 * st + (r & 3) + 8 * (r >> 2) + 4 * h;
+            float pr = exp2f(sc[r] * LOG2E + mk[kl] - lse2);
+            float dpv = bits[e] >= thr ? dp[r] * zs : 0.f;
+            sc[r] = pr * (dpv - dlt);  // dS^T
+          }
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 sf = acc_frag(sc, s2);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt)
+            dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Ks, 32 * st + 16 * s2, 32 * dt, l), sf, dq[dt], 0, 0, 0);
+        }
+      }
+    }
+    if (more) {
+      char* dK = smem + (stg ^ 1) * 2 * TILE;
+      lk.store(dK, t);
+      lv.store(dK + TILE, t);
+      if (t < KV) maskL[(stg ^ 1) * KV + t] = mnext;
+    }
+    __syncthreads();
+  }
+  if (!qv) return;
+  bf16* ob = p.out + ((int64_t)b * L + q) * p.ld_out + hd * 64;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 v = {f2bf(dq[dt][4 * g] * 0.125f), f2bf(dq[dt][4 * g + 1] * 0.125f), f2bf(dq[dt][4 * g + 2] * 0.125f),
+                  f2bf(dq[dt][4 * g + 3] * 0.125f)};
+      *(bf16x4*)(ob + 32 * dt + 8 * g + 4 * h) = v;
+    }
+}
+
+// dK, dV: grid (ceil(L/64), batch*heads), 128 threads; wave owns 32 keys; loops over 32-query tiles
+__global__ __launch_bounds__(128) void attn_dkdv_kernel(AttnParams p) {
+  constexpr int QT = 32, TILE = QT * 128;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE + 2 * 2 * QT * 4];
+  float* rowL = (float*)(smem + 4 * TILE);  // [stage][2][QT]: lse2, delta
+  const int t = threadIdx.x, l = t & 63, w = t >> 6, h = l >> 5;
+  const int bh = blockIdx.y, b = bh / p.heads, hd = bh - b * p.heads;
+  const int L = p.L, HD = p.heads * 64;
+  const int k0w = blockIdx.x * 64 + 32 * w, key = k0w + (l & 31);
+  const bool wave_live = k0w < L, kv = key < L;
+  const bf16* base = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64;
+  const bf16* dob = p.dout + (int64_t)b * L * p.ld_do + hd * 64;
+  const uint32_t sbh = seed_for(p.seed, bh), Lp = (uint32_t)((L + 1) & ~1);
+  const uint32_t thr = (uint32_t)(p.drop_p * 65536.0f + 0.5f);
+  const float zs = p.drop_p > 0.f ? 1.0f / (1.0f - p.drop_p) : 1.0f;
+  const float mkey = kv ? p.keymask[(int64_t)b * L + key] * LOG2E : NEG_INF;
+
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    uint4 u = kv ? *(const uint4*)(base + (int64_t)key * p.ld_qkv + HD + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
+    uint4 v = kv ? *(const uint4*)(base + (int64_t)key * p.ld_qkv + 2 * HD + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
+    kf[ks] = *(bf16x8*)&u;
+    vf[ks] = *(bf16x8*)&v;
+  }
+  f32x16 dk[2], dv[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { dk[0][i] = 0.f; dk[1][i] = 0.f; dv[0][i] = 0.f; dv[1][i] = 0.f; }
+
+  TileLoader<QT, 128> lq, ld;
+  const int nq = (L + QT - 1) / QT;
+  auto load_rows = [&](int i0, float& a, float& c) {
+    int qq = i0 + (t & 31);
+    a = qq < L ? p.lse[(int64_t)bh * L + qq] * LOG2E : __builtin_huge_valf();
+    c = qq < L ? p.delta[(int64_t)bh * L + qq] : 0.f;
+  };
+  float ra = 0.f, rc = 0.f;
+  lq.load(base, p.ld_qkv, 0, L, t);
+  ld.load(dob, p.ld_do, 0, L, t);
+  load_rows(0, ra, rc);
+  lq.store(smem, t, 0.125f);
+  ld.store(smem + TILE, t);
+  if (t < QT) { rowL[t] = ra; rowL[QT + t] = rc; }
+  __syncthreads();
+  for (int i = 0; i < nq; ++i) {
+    const int stg = i & 1;
+    const char* Qs = smem + stg * 2 * TILE;
+    const char* Ds = Qs + TILE;
+    const float* lse2 = rowL + stg * 2 * QT;
+    const float* dlt = lse2 + QT;
+    const bool more = i + 1 < nq;
+    if (more) {
+      lq.load(base, p.ld_qkv, (i + 1) * QT, L, t);
+      ld.load(dob, p.ld_do, (i + 1) * QT, L, t);
+      load_rows((i + 1) * QT, ra, rc);
+    }
+    if (wave_live) {
+      f32x16 sc, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { sc[r] = 0.f; dp[r] = 0.f; }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Qs, 0, ks, l), kf[ks], sc, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ds, 0, ks, l), vf[ks], dp, 0, 0, 0);
+      }
+      f32x16 pz;  // dropped P (for dV)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ql = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const uint32_t qq = (uint32_t)(i * QT + ql);
+        float pr = exp2f(sc[r] * LOG2E + mkey - lse2[ql]);
+        bool keep = thr ? keep_elem(sbh, qq, (uint32_t)key, Lp, thr) : true;
+        float z = keep ? zs : 0.f;
+        pz[r] = pr * z;
+        sc[r] = pr * (dp[r] * z - dlt[ql]);  // dS
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 pf = acc_frag(pz, s2), sf = acc_frag(sc, s2);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf, tr_frag(Ds, 16 * s2, 32 * dt, l), dv[dt], 0, 0, 0);
+          dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sf, tr_frag(Qs, 16 * s2, 32 * dt, l), dk[dt], 0, 0, 0);
+        }
+      }
+    }
+    if (more) {
+      char* dQ = smem + (stg ^ 1) * 2 * TILE;
+      lq.store(dQ, t, 0.125f);
+      ld.store(dQ + TILE, t);
+      if (t < QT) { rowL[(stg ^ 1) * 2 * QT + t] = ra; rowL[(stg ^ 1) * 2 * QT + QT + t] = rc; }
+    }
+    __syncthreads();
+  }
+  if (!wave_live) return;
+  // dK/dV accumulators: rows = key (registers), cols = d (lanes)
+  bf16* outb = p.out + (int64_t)b * L * p.ld_out + hd * 64;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kk = k0w + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (kk < L) {
+        const int64_t off = (int64_t)kk * p.ld_out + 32 * dt + (l & 31);
+        outb[off + HD] = f2bf(dk[dt][r]);
+        outb[off + 2 * HD] = f2bf(dv[dt][r]);
+      }
+    }
+}
+
+void attention_fwd_launch(const AttnParams& p, hipStream_t s) {
+  dim3 grid((p.L + 127) / 128, p.batch * p.heads);
+  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, s, p);
+}
+
+void attention_bwd_launch(const AttnParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(attn_delta_kernel, dim3((p.L + 31) / 32, p.batch * p.heads), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(attn_dq_kernel, dim3((p.L + 127) / 128, p.batch * p.heads), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(attn_dkdv_kernel, dim3((p.L + 63) / 64, p.batch * p.heads), dim3(128), 0, s, p);
+}
+
+}  // namespace mmu

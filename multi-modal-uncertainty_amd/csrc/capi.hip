@@ -1,0 +1,292 @@
+// extern "C" boundary of libmmu_hip.so (declared in include/mmu.h).
+// Validates arguments, flattens structs into kernel params, launches on the caller's
+// stream, and reports failures through a thread-local message (mmu_last_error).
+#include <stdarg.h>
+#include <stdio.h>
+#include <mutex>
+#include <string>
+#include <vector>
+#include "mmu_internal.h"
+
+using namespace mmu;
+
+static thread_local std::string g_err;
+
+static int fail(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return 1;
+}
+
+static int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail("%s: launch failed: %s", what, hipGetErrorString(e));
+  return 0;
+}
+
+// ------------------------------------------------------------------ timing of mmu_gemm
+namespace {
+struct Timing {
+  std::mutex mu;
+  bool on = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pool, used;
+  std::vector<double> flops;
+} g_t;
+
+std::pair<hipEvent_t, hipEvent_t> take_events() {
+  std::lock_guard<std::mutex> lk(g_t.mu);
+  std::pair<hipEvent_t, hipEvent_t> ev;
+  if (!g_t.pool.empty()) {
+    ev = g_t.pool.back();
+    g_t.pool.pop_back();
+  } else {
+    (void)hipEventCreate(&ev.first);
+    (void)hipEventCreate(&ev.second);
+  }
+  return ev;
+}
+}  // namespace
+
+extern "C" {
+
+int mmu_version(void) { return 1; }
+const char* mmu_last_error(void) { return g_err.c_str(); }
+
+int mmu_timing_enable(int on) {
+  std::lock_guard<std::mutex> lk(g_t.mu);
+  g_t.on = on != 0;
+  for (auto& e : g_t.used) g_t.pool.push_back(e);
+  g_t.used.clear();
+  g_t.flops.clear();
+  return 0;
+}
+
+int mmu_timing_read(double* total_ms, int64_t* launches, double* flops) {
+  std::lock_guard<std::mutex> lk(g_t.mu);
+  double tot = 0.0, fl = 0.0;
+  for (size_t i = 0; i < g_t.used.size(); ++i) {
+    (void)hipEventSynchronize(g_t.used[i].second);
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, g_t.used[i].first, g_t.used[i].second) != hipSuccess) return fail("timing: elapsed");
+    tot += ms;
+    fl += g_t.flops[i];
+  }
+  *total_ms = tot;
+  *launches = (int64_t)g_t.used.size();
+  *flops = fl;
+  return 0;
+}
+
+int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb, int b_kmajor, void* C,
+             int64_t ldc, int c_dtype, int64_t M, int64_t N, int64_t K, int64_t batch, int64_t strideA,
+             int64_t strideB, int64_t strideC, const mmu_epilogue* epi, mmu_stream_t stream) {
+  if (!A || !B || !C) return fail("mmu_gemm: null operand");
+  if (M <= 0 || N <= 0 || K <= 0 || batch <= 0) return fail("mmu_gemm: bad shape M=%ld N=%ld K=%ld", M, N, K);
+  if (N % 128) return fail("mmu_gemm: N=%ld must be a multiple of 128", N);
+  if ((a_kmajor || b_kmajor) && K % 64) return fail("mmu_gemm: K=%ld must be a multiple of 64 for a K-major operand", K);
+  if (!a_kmajor && M % 128) return fail("mmu_gemm: M=%ld must be a multiple of 128 when A is M-major", M);
+  if ((lda % 8) || (ldb % 8) || (ldc % 4)) return fail("mmu_gemm: leading dims must be 16-B aligned");
+  if (c_dtype != MMU_BF16 && c_dtype != MMU_F32) return fail("mmu_gemm: bad c_dtype");
+  GemmParams p{};
+  p.A = (const bf16*)A; p.B = (const bf16*)B; p.C = C;
+  p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
+  p.sA = strideA; p.sB = strideB; p.sC = strideC;
+  p.tiles_m = (int)((M + 127) / 128);
+  p.tiles_n = (int)(N / 128);
+  int kind = MMU_EPI_STORE;
+  if (epi) {
+    kind = epi->kind;
+    p.accumulate = epi->accumulate;
+    p.bias = epi->bias; p.bias_bstride = epi->bias_bstride;
+    p.residual = epi->residual; p.ldr = epi->ldr; p.res_bstride = epi->res_bstride;
+    p.aux = epi->aux; p.ldx = epi->ldx; p.aux_bstride = epi->aux_bstride;
+    p.colsum = epi->colsum; p.colsum_bstride = epi->colsum_bstride;
+    p.drop_p = epi->drop_p; p.seed = epi->seed;
+  }
+  p.kind = kind;
+  if (kind < 0 || kind > MMU_EPI_ADD_RES) return fail("mmu_gemm: bad epilogue kind %d", kind);
+  if (kind != MMU_EPI_STORE && c_dtype != MMU_BF16) return fail("mmu_gemm: fused epilogues write bf16");
+  if ((kind == MMU_EPI_BIAS_GELU || kind == MMU_EPI_DGELU) && !p.aux) return fail("mmu_gemm: epilogue needs aux");
+  if ((kind == MMU_EPI_BIAS_DROP_RES || kind == MMU_EPI_ADD_RES) && !p.residual)
+    return fail("mmu_gemm: epilogue needs residual");
+  if (p.accumulate && c_dtype != MMU_F32) return fail("mmu_gemm: accumulate needs f32 C");
+  if (p.drop_p < 0.f || p.drop_p >= 1.f) return fail("mmu_gemm: drop_p out of range");
+  hipStream_t s = (hipStream_t)stream;
+  bool timed;
+  std::pair<hipEvent_t, hipEvent_t> ev;
+  {
+    std::lock_guard<std::mutex> lk(g_t.mu);
+    timed = g_t.on;
+  }
+  if (timed) {
+    ev = take_events();
+    (void)hipEventRecord(ev.first, s);
+  }
+  gemm_launch(p, a_kmajor != 0, b_kmajor != 0, c_dtype == MMU_F32, (int)batch, s);
+  if (timed) {
+    (void)hipEventRecord(ev.second, s);
+    std::lock_guard<std::mutex> lk(g_t.mu);
+    g_t.used.push_back(ev);
+    g_t.flops.push_back(2.0 * (double)M * (double)N * (double)K * (double)batch);
+  }
+  return check_launch("mmu_gemm");
+}
+
+int mmu_colsum_reduce(const float* partial, int64_t parts, int64_t N, float* out, int accumulate,
+                      mmu_stream_t stream) {
+  if (!partial || !out || parts <= 0 || N <= 0) return fail("mmu_colsum_reduce: bad args");
+  colsum_reduce_launch(partial, parts, N, out, accumulate, (hipStream_t)stream);
+  return check_launch("mmu_colsum_reduce");
+}
+
+int mmu_colsum_bf16(const void* X, int64_t M, int64_t N, int64_t ldx, float* partial, float* out, int accumulate,
+                    mmu_stream_t stream) {
+  if (!X || !partial || !out || M <= 0 || N <= 0 || N % 8 || ldx % 8) return fail("mmu_colsum_bf16: bad args");
+  colsum_bf16_launch((const bf16*)X, M, N, ldx, partial, out, accumulate, (hipStream_t)stream);
+  return check_launch("mmu_colsum_bf16");
+}
+
+static int attn_common(int64_t ld_qkv, int64_t batch, int64_t L, int64_t heads, float drop_p) {
+  if (batch <= 0 || L <= 0 || heads <= 0) return fail("attention: bad shape");
+  if (ld_qkv < 3 * heads * 64 || ld_qkv % 8) return fail("attention: ld_qkv too small / unaligned");
+  if (drop_p < 0.f || drop_p >= 1.f) return fail("attention: drop_p out of range");
+  if ((int64_t)batch * heads > 65535 * 64) return fail("attention: batch*heads too large");
+  return 0;
+}
+
+int mmu_attention_fwd(const void* QKV, int64_t ld_qkv, const float* keymask, void* O, int64_t ld_o, float* LSE,
+                      int64_t batch, int64_t L, int64_t heads, float drop_p, uint64_t seed, mmu_stream_t stream) {
+  if (!QKV || !keymask || !O || !LSE) return fail("mmu_attention_fwd: null pointer");
+  if (attn_common(ld_qkv, batch, L, heads, drop_p)) return 1;
+  if (ld_o < heads * 64 || ld_o % 4) return fail("mmu_attention_fwd: bad ld_o");
+  if (batch * heads > 65535) return fail("mmu_attention_fwd: batch*heads > 65535");
+  AttnParams p{};
+  p.qkv = (const bf16*)QKV; p.ld_qkv = ld_qkv; p.keymask = keymask; p.out = (bf16*)O; p.ld_out = ld_o;
+  p.lse = LSE; p.batch = (int)batch; p.L = (int)L; p.heads = (int)heads; p.drop_p = drop_p; p.seed = seed;
+  attention_fwd_launch(p, (hipStream_t)stream);
+  return check_launch("mmu_attention_fwd");
+}
+
+int mmu_attention_bwd(const void* QKV, int64_t ld_qkv, const float* keymask, const void* O, int64_t ld_o,
+                      const void* dO, int64_t ld_do, const float* LSE, float* delta, void* dQKV, int64_t ld_dqkv,
+                      int64_t batch, int64_t L, int64_t heads, float drop_p, uint64_t seed, mmu_stream_t stream) {
+  if (!QKV || !keymask || !O || !dO || !LSE || !delta || !dQKV) return fail("mmu_attention_bwd: null pointer");
+  if (attn_common(ld_qkv, batch, L, heads, drop_p)) return 1;
+  if (ld_dqkv < 3 * heads * 64 || ld_do % 8 || ld_o % 8 || ld_dqkv % 4) return fail("mmu_attention_bwd: bad ld");
+  if (batch * heads > 65535) return fail("mmu_attention_bwd: batch*heads > 65535");
+  AttnParams p{};
+  p.qkv = (const bf16*)QKV; p.ld_qkv = ld_qkv; p.keymask = keymask; p.o = (const bf16*)O; p.ld_o = ld_o;
+  p.dout = (const bf16*)dO; p.ld_do = ld_do; p.lse = (float*)LSE; p.delta = delta; p.out = (bf16*)dQKV;
+  p.ld_out = ld_dqkv; p.batch = (int)batch; p.L = (int)L; p.heads = (int)heads; p.drop_p = drop_p; p.seed = seed;
+  attention_bwd_launch(p, (hipStream_t)stream);
+  return check_launch("mmu_attention_bwd");
+}
+
+int mmu_layernorm_fwd(const void* X, const float* w, const float* b, void* Y, float* mean, float* rstd, int64_t rows,
+                      int64_t H, float eps, mmu_stream_t stream) {
+  if (!X || !w || !b || !Y || !mean || !rstd) return fail("mmu_layernorm_fwd: null pointer");
+  if (rows <= 0 || H % 256 || H > 1024) return fail("mmu_layernorm_fwd: H=%ld must be 256/512/768/1024", H);
+  layernorm_fwd_launch((const bf16*)X, w, b, (bf16*)Y, mean, rstd, rows, H, eps, (hipStream_t)stream);
+  return check_launch("mmu_layernorm_fwd");
+}
+
+int mmu_layernorm_bwd(const void* dY, const void* X, const float* mean, const float* rstd, const float* w, void* dX,
+                      void* dXdrop, float drop_p, uint64_t seed, float* part_dw, float* part_db, float* part_dbias,
+                      int64_t rows, int64_t H, int64_t rows_per_part, mmu_stream_t stream) {
+  if (!dY || !X || !mean || !rstd || !w || !dX) return fail("mmu_layernorm_bwd: null pointer");
+  if (rows <= 0 || H % 256 || H > 1024 || rows_per_part <= 0) return fail("mmu_layernorm_bwd: bad shape");
+  if (drop_p < 0.f || drop_p >= 1.f) return fail("mmu_layernorm_bwd: drop_p out of range");
+  layernorm_bwd_launch((const bf16*)dY, (const bf16*)X, mean, rstd, w, (bf16*)dX, (bf16*)dXdrop, drop_p, seed, part_dw,
+                       part_db, part_dbias, rows, H, rows_per_part, (hipStream_t)stream);
+  return check_launch("mmu_layernorm_bwd");
+}
+
+int mmu_embed_fwd(const int64_t* ids, const int64_t* seg, const int64_t* txt_mask, const float* proj, const float* word,
+                  const float* pos, const float* type, const float* ln_w, const float* ln_b, float eps, int64_t cls_id,
+                  int64_t sep_id, const int64_t* idx, int64_t V, int64_t B, int64_t T, int64_t n_img, int64_t Lout,
+                  int64_t H, float drop_txt, float drop_img, uint64_t seed, void* X, float* keymask, float* mean,
+                  float* rstd, mmu_stream_t stream) {
+  if (H != 768) return fail("mmu_embed_fwd: H must be 768");
+  if (!word || !pos || !type || !ln_w || !ln_b || !X || !keymask || !proj) return fail("mmu_embed_fwd: null pointer");
+  if (T > 0 && (!ids || !seg)) return fail("mmu_embed_fwd: text ids/segments missing");
+  if (V <= 0 || B <= 0 || Lout <= 0 || n_img <= 0) return fail("mmu_embed_fwd: bad shape");
+  if (!idx && Lout != n_img + 2 + T) return fail("mmu_embed_fwd: identity variant needs Lout == n_img+2+T");
+  EmbedParams p{};
+  p.ids = ids; p.seg = seg; p.txt_mask = txt_mask; p.idx = idx; p.proj = proj; p.word = word; p.pos = pos;
+  p.type = type; p.ln_w = ln_w; p.ln_b = ln_b; p.eps = eps; p.cls_id = cls_id; p.sep_id = sep_id; p.V = V; p.B = B;
+  p.T = T; p.n_img = n_img; p.Lout = Lout; p.H = H; p.X = (bf16*)X;
+  if (drop_txt < 0.f || drop_txt >= 1.f || drop_img < 0.f || drop_img >= 1.f) return fail("mmu_embed_fwd: bad dropout");
+  p.drop_txt = drop_txt; p.drop_img = drop_img; p.seed = seed; p.keymask = keymask; p.mean = mean; p.rstd = rstd;
+  embed_fwd_launch(p, (hipStream_t)stream);
+  return check_launch("mmu_embed_fwd");
+}
+
+int mmu_embed_bwd(const void* dX, const int64_t* ids, const int64_t* seg, const float* proj, const float* word,
+                  const float* pos, const float* type, const float* ln_w, const float* mean, const float* rstd,
+                  int64_t cls_id, int64_t sep_id, int64_t B, int64_t T, int64_t n_img, int64_t H, float drop_txt,
+                  float drop_img, uint64_t seed, float* d_word,
+                  float* d_pos, float* d_type, float* d_ln_w, float* d_ln_b, float* d_proj, float* ws,
+                  mmu_stream_t stream) {
+  if (H != 768) return fail("mmu_embed_bwd: H must be 768");
+  if (!dX || !ids || !seg || !proj || !word || !pos || !type || !ln_w || !mean || !rstd || !d_word || !d_pos ||
+      !d_type || !d_ln_w || !d_ln_b || !d_proj || !ws)
+    return fail("mmu_embed_bwd: null pointer");
+  EmbedBwdParams q{};
+  q.dX = (const bf16*)dX; q.ids = ids; q.seg = seg; q.proj = proj; q.word = word; q.pos = pos; q.type = type;
+  q.ln_w = ln_w; q.mean = mean; q.rstd = rstd; q.cls_id = cls_id; q.sep_id = sep_id; q.B = B; q.T = T;
+  q.n_img = n_img; q.H = H; q.drop_txt = drop_txt; q.drop_img = drop_img; q.seed = seed; q.d_word = d_word; q.d_pos = d_pos; q.d_type = d_type; q.d_ln_w = d_ln_w;
+  q.d_ln_b = d_ln_b; q.d_proj = d_proj; q.ws = ws;
+  embed_bwd_launch(q, (hipStream_t)stream);
+  return check_launch("mmu_embed_bwd");
+}
+
+int mmu_row_pool_fwd(const void* fmap, int64_t B, int64_t Hh, int64_t Ww, int64_t C, int64_t n, float* out,
+                     mmu_stream_t stream) {
+  if (!fmap || !out || C % 8 || n <= 0 || n > Hh) return fail("mmu_row_pool_fwd: bad args");
+  row_pool_fwd_launch((const bf16*)fmap, B, Hh, Ww, C, n, out, (hipStream_t)stream);
+  return check_launch("mmu_row_pool_fwd");
+}
+
+int mmu_row_pool_bwd(const float* dout, int64_t B, int64_t Hh, int64_t Ww, int64_t C, int64_t n, void* dfmap,
+                     mmu_stream_t stream) {
+  if (!dout || !dfmap || C % 8 || n <= 0 || n > Hh) return fail("mmu_row_pool_bwd: bad args");
+  row_pool_bwd_launch(dout, B, Hh, Ww, C, n, (bf16*)dfmap, (hipStream_t)stream);
+  return check_launch("mmu_row_pool_bwd");
+}
+
+int mmu_bertadam_step(float* params, const float* grads, float* m, float* v, void* bf16_copy, const int64_t* table,
+                      int32_t* steps, int64_t n_tensors, int64_t n_chunks, float lr_decay, float lr_nodecay, float wd,
+                      float warmup, float t_total, float b1, float b2, float eps, float max_grad_norm, float* ws,
+                      int64_t ws_floats, mmu_stream_t stream) {
+  if (!params || !grads || !m || !v || !table || !steps || !ws) return fail("mmu_bertadam_step: null pointer");
+  if (n_tensors <= 0 || n_chunks <= 0) return fail("mmu_bertadam_step: empty table");
+  if (ws_floats < n_chunks + 2 * n_tensors) return fail("mmu_bertadam_step: workspace too small");
+  AdamParams p{};
+  p.params = params; p.grads = grads; p.m = m; p.v = v; p.bf16_copy = (bf16*)bf16_copy; p.table = table;
+  p.steps = steps; p.n_tensors = n_tensors; p.total = n_chunks; p.lr_decay = lr_decay; p.lr_nodecay = lr_nodecay;
+  p.wd = wd; p.warmup = warmup; p.t_total = t_total; p.b1 = b1; p.b2 = b2; p.eps = eps;
+  p.max_grad_norm = max_grad_norm; p.ws = ws; p.ws_floats = ws_floats;
+  const char* e = nullptr;
+  if (bertadam_launch(p, (hipStream_t)stream, &e)) return fail("mmu_bertadam_step: %s", e ? e : "failed");
+  return check_launch("mmu_bertadam_step");
+}
+
+int mmu_uncertainty(const float* logits, const int64_t* y, int64_t S, int64_t R, int64_t C, float* p_bar, float* nll,
+                    float* conf, float* correct, mmu_stream_t stream) {
+  if (!logits || !y || !p_bar || !nll || !conf || !correct) return fail("mmu_uncertainty: null pointer");
+  if (S <= 0 || R <= 0 || C <= 0 || C > 1024) return fail("mmu_uncertainty: bad shape (C <= 1024)");
+  uncertainty_launch(logits, y, S, R, C, p_bar, nll, conf, correct, (hipStream_t)stream);
+  return check_launch("mmu_uncertainty");
+}
+
+int mmu_ece_bins(const float* conf, const float* correct, int64_t S, int64_t n_bins, float* out, mmu_stream_t stream) {
+  if (!conf || !correct || !out || S <= 0 || n_bins <= 0) return fail("mmu_ece_bins: bad args");
+  ece_bins_launch(conf, correct, S, n_bins, out, (hipStream_t)stream);
+  return check_launch("mmu_ece_bins");
+}
+
+}  // extern "C"

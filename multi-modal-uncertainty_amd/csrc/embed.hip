@@ -1,0 +1,268 @@
+// Modality-token embedding + text gather + concat / control gather (gfx950).
+//
+// One pass builds the encoder input rows the reference assembles from
+//   ImageBertEmbeddings   src/mmbt.py:58-83   ([CLS] | Linear(img) | [SEP], pos 0..N+1, type 0, LN)
+//   BertEmbeddings        src/mmbt.py:121     (word[id] + pos[t] + type[seg], LN)
+//   torch.cat             src/mmbt.py:122     (img tokens then text)
+//   encoder_input[:, idx] src/mmbt.py:229     (forward_control gather, one index set per call)
+// and the additive key mask (src/mmbt.py:101-112,203-216) for every output row, so
+// the [B, L, 768] activation is written exactly once, already in its final order.
+// Also: AdaptiveAvgPool2d((N,1)) of the ResNet map (src/mmbt.py:30,42-44) and the
+// embedding backward (LN backward + word-row atomics + batch reductions).
+#include "mmu_common.h"
+#include "mmu_internal.h"
+
+namespace mmu {
+
+
+static __device__ __forceinline__ void add_row(float (&acc)[3][4], const float* __restrict__ src, int l) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    float4 a = *(const float4*)(src + 256 * i + 4 * l);
+    acc[i][0] += a.x; acc[i][1] += a.y; acc[i][2] += a.z; acc[i][3] += a.w;
+  }
+}
+
+// pre-LN embedding sum of source position s for batch row b (H == 768)
+static __device__ __forceinline__ void embed_sum(float (&e)[3][4], const EmbedParams& p, int64_t b, int64_t s,
+                                                 int l, float& km) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) e[i][k] = 0.f;
+  const int64_t H = p.H, nimg = p.n_img;
+  km = 0.f;
+  if (s <= nimg + 1) {
+    if (s == 0) add_row(e, p.word + p.cls_id * H, l);
+    else if (s == nimg + 1) add_row(e, p.word + p.sep_id * H, l);
+    else add_row(e, p.proj + (b * nimg + (s - 1)) * H, l);
+    add_row(e, p.pos + s * H, l);
+    add_row(e, p.type, l);
+  } else {
+    const int64_t t = s - nimg - 2;
+    const int64_t id = p.ids[b * p.T + t], sg = p.seg[b * p.T + t];
+    add_row(e, p.word + id * H, l);
+    add_row(e, p.pos + t * H, l);
+    add_row(e, p.type + sg * H, l);
+    if (p.txt_mask && p.txt_mask[b * p.T + t] == 0) km = -10000.0f;
+  }
+}
+
+__global__ __launch_bounds__(256) void embed_fwd_kernel(EmbedParams p) {
+  const int l = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t total = p.V * p.B * p.Lout;
+  if (row >= total) return;
+  const int64_t j = row % p.Lout, vb = row / p.Lout, b = vb % p.B, v = vb / p.B;
+  const int64_t s = p.idx ? p.idx[v * p.Lout + j] : j;
+  float e[3][4], km;
+  embed_sum(e, p, b, s, l, km);
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sum += e[i][k];
+  const float mu = wave_sum(sum) / 768.f;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { float d = e[i][k] - mu; q += d * d; }
+  const float rs = rsqrtf(wave_sum(q) / 768.f + p.eps);
+  // dropout: ImageBertEmbeddings.dropout (p = args.dropout) on the image-segment rows,
+  // BertEmbeddings.dropout (0.1) on text rows; element counter row*768 + col
+  const float dp = s <= p.n_img + 1 ? p.drop_img : p.drop_txt;
+  const uint32_t thr = (uint32_t)(dp * 65536.0f + 0.5f);
+  const float dsc = dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int c = 256 * i + 4 * l;
+    float4 w = *(const float4*)(p.ln_w + c), bb = *(const float4*)(p.ln_b + c);
+    float y[4] = {(e[i][0] - mu) * rs * w.x + bb.x, (e[i][1] - mu) * rs * w.y + bb.y,
+                  (e[i][2] - mu) * rs * w.z + bb.z, (e[i][3] - mu) * rs * w.w + bb.w};
+    if (thr) {
+      const uint32_t keep = mmu_keep4(p.seed, (uint64_t)(row * 768 + c) >> 2, thr);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) y[k] = ((keep >> k) & 1) ? y[k] * dsc : 0.f;
+    }
+    *(bf16x4*)(p.X + row * 768 + c) = bf16x4{f2bf(y[0]), f2bf(y[1]), f2bf(y[2]), f2bf(y[3])};
+  }
+  if (l == 0) {
+    p.keymask[row] = km;
+    if (p.mean) { p.mean[row] = mu; p.rstd[row] = rs; }
+  }
+}
+
+void embed_fwd_launch(const EmbedParams& p, hipStream_t s) {
+  const int64_t total = p.V * p.B * p.Lout;
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3((unsigned)((total + 3) / 4)), dim3(256), 0, s, p);
+}
+
+// ---------------------------------------------------------------- backward
+// phase 1: per row LN backward -> dsum (ws), word-row atomics for text rows, dproj for image rows,
+//          per-64-row partial sums of dgamma / dbeta
+__global__ __launch_bounds__(256) void embed_bwd_rows_kernel(EmbedBwdParams q, EmbedParams p) {
+  __shared__ float red[2][4][768];
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t S = q.n_img + 2 + q.T, rows = q.B * S, H = 768;
+  float* dsum = q.ws;
+  float* part = q.ws + rows * H;
+  const int64_t nparts = (rows + 63) / 64;
+  float aw[3][4], ab[3][4], w[3][4];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { aw[i][k] = ab[i][k] = 0.f; w[i][k] = q.ln_w[256 * i + 4 * l + k]; }
+  for (int64_t row = (int64_t)blockIdx.x * 64 + wv; row < (int64_t)blockIdx.x * 64 + 64 && row < rows; row += 4) {
+    const int64_t b = row / S, s = row % S;
+    float e[3][4], km;
+    embed_sum(e, p, b, s, l, km);
+    const float mu = q.mean[row], rs = q.rstd[row];
+    const float dp = s <= q.n_img + 1 ? q.drop_img : q.drop_txt;
+    const uint32_t thr = (uint32_t)(dp * 65536.0f + 0.5f);
+    const float dsc = dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f;
+    float g[3][4], xh[3][4], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      bf16x4 d = *(const bf16x4*)(q.dX + row * H + 256 * i + 4 * l);
+      const uint32_t keep = thr ? mmu_keep4(q.seed, (uint64_t)(row * H + 256 * i + 4 * l) >> 2, thr) : 0xFu;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float dy = ((keep >> k) & 1) ? bf2f(d[k]) * dsc : 0.f;
+        xh[i][k] = (e[i][k] - mu) * rs;
+        g[i][k] = dy * w[i][k];
+        s1 += g[i][k];
+        s2 += g[i][k] * xh[i][k];
+        aw[i][k] += dy * xh[i][k];
+        ab[i][k] += dy;
+      }
+    }
+    s1 = wave_sum(s1) / 768.f;
+    s2 = wave_sum(s2) / 768.f;
+    const bool text = s >= q.n_img + 2, img = s >= 1 && s <= q.n_img;
+    float* wrow = text ? q.d_word + q.ids[b * q.T + (s - q.n_img - 2)] * H : nullptr;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int c = 256 * i + 4 * l;
+      float dx[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dx[k] = rs * (g[i][k] - s1 - xh[i][k] * s2);
+      *(float4*)(dsum + row * H + c) = make_float4(dx[0], dx[1], dx[2], dx[3]);
+      if (text) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) atomicAdd(wrow + c + k, dx[k]);
+      } else if (img) {
+        *(float4*)(q.d_proj + (b * q.n_img + (s - 1)) * H + c) = make_float4(dx[0], dx[1], dx[2], dx[3]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      red[0][wv][256 * i + 4 * l + k] = aw[i][k];
+      red[1][wv][256 * i + 4 * l + k] = ab[i][k];
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 768; c += 256) {
+    part[(int64_t)blockIdx.x * H + c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+    part[(nparts + blockIdx.x) * H + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+  }
+}
+
+// phase 2: per source position s, sum dsum over the batch into position / token-type / [CLS]/[SEP] rows
+__global__ __launch_bounds__(256) void embed_bwd_batch_kernel(EmbedBwdParams q) {
+  const int64_t S = q.n_img + 2 + q.T, H = 768;
+  const int64_t s = blockIdx.x;
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= H) return;
+  const float* dsum = q.ws;
+  float tot = 0.f, t1 = 0.f;
+  const bool text = s >= q.n_img + 2;
+  for (int64_t b = 0; b < q.B; ++b) {
+    const float v = dsum[(b * S + s) * H + c];
+    tot += v;
+    if (text && q.seg[b * q.T + (s - q.n_img - 2)] != 0) t1 += v;
+  }
+  const int64_t posr = text ? s - q.n_img - 2 : s;
+  atomicAdd(q.d_pos + posr * H + c, tot);
+  atomicAdd(q.d_type + c, tot - t1);
+  if (text) atomicAdd(q.d_type + H + c, t1);
+  if (s == 0) atomicAdd(q.d_word + q.cls_id * H + c, tot);
+  if (s == q.n_img + 1) atomicAdd(q.d_word + q.sep_id * H + c, tot);
+}
+
+void embed_bwd_launch(const EmbedBwdParams& q, hipStream_t s) {
+  EmbedParams p{};
+  p.ids = q.ids; p.seg = q.seg; p.txt_mask = nullptr; p.idx = nullptr;
+  p.proj = q.proj; p.word = q.word; p.pos = q.pos; p.type = q.type;
+  p.cls_id = q.cls_id; p.sep_id = q.sep_id; p.V = 1; p.B = q.B; p.T = q.T; p.n_img = q.n_img;
+  p.Lout = q.n_img + 2 + q.T; p.H = 768;
+  const int64_t rows = q.B * p.Lout, nparts = (rows + 63) / 64;
+  hipLaunchKernelGGL(embed_bwd_rows_kernel, dim3((unsigned)nparts), dim3(256), 0, s, q, p);
+  hipLaunchKernelGGL(embed_bwd_batch_kernel, dim3((unsigned)p.Lout, 3), dim3(256), 0, s, q);
+  float* part = q.ws + rows * 768;
+  colsum_reduce_launch(part, nparts, 768, q.d_ln_w, 1, s);
+  colsum_reduce_launch(part + nparts * 768, nparts, 768, q.d_ln_b, 1, s);
+}
+
+// ---------------------------------------------------------------- AdaptiveAvgPool2d((n,1))
+// bin i covers rows [floor(i*Hh/n), ceil((i+1)*Hh/n)), all columns
+__global__ __launch_bounds__(256) void row_pool_fwd_kernel(const bf16* __restrict__ f, int64_t B, int Hh, int Ww,
+                                                           int64_t C, int n, float* __restrict__ out) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;  // over B * C/8
+  const int64_t c8 = C / 8;
+  if (idx >= B * c8) return;
+  const int64_t b = idx / c8, c = (idx % c8) * 8;
+  for (int i = 0; i < n; ++i) {
+    const int y0 = (i * Hh) / n, y1 = ((i + 1) * Hh + n - 1) / n;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int y = y0; y < y1; ++y)
+      for (int x = 0; x < Ww; ++x) {
+        bf16x8 v = *(const bf16x8*)(f + ((b * Hh + y) * Ww + x) * C + c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += bf2f(v[e]);
+      }
+    const float inv = 1.0f / ((y1 - y0) * Ww);
+    float* o = out + (b * n + i) * C + c;
+    *(float4*)o = make_float4(acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
+    *(float4*)(o + 4) = make_float4(acc[4] * inv, acc[5] * inv, acc[6] * inv, acc[7] * inv);
+  }
+}
+
+__global__ __launch_bounds__(256) void row_pool_bwd_kernel(const float* __restrict__ d, int64_t B, int Hh, int Ww,
+                                                           int64_t C, int n, bf16* __restrict__ df) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;  // over B*Hh * C/8
+  const int64_t c8 = C / 8;
+  if (idx >= B * Hh * c8) return;
+  const int64_t by = idx / c8, c = (idx % c8) * 8, b = by / Hh;
+  const int y = (int)(by % Hh);
+  float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < n; ++i) {
+    const int y0 = (i * Hh) / n, y1 = ((i + 1) * Hh + n - 1) / n;
+    if (y < y0 || y >= y1) continue;
+    const float inv = 1.0f / ((y1 - y0) * Ww);
+    const float* s = d + (b * n + i) * C + c;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] += s[e] * inv;
+  }
+  bf16x8 v;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = f2bf(g[e]);
+  for (int x = 0; x < Ww; ++x) *(bf16x8*)(df + ((b * Hh + y) * Ww + x) * C + c) = v;
+}
+
+void row_pool_fwd_launch(const bf16* fmap, int64_t B, int64_t Hh, int64_t Ww, int64_t C, int64_t n, float* out,
+                         hipStream_t s) {
+  const int64_t tot = B * (C / 8);
+  hipLaunchKernelGGL(row_pool_fwd_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, fmap, B, (int)Hh,
+                     (int)Ww, C, (int)n, out);
+}
+void row_pool_bwd_launch(const float* dout, int64_t B, int64_t Hh, int64_t Ww, int64_t C, int64_t n, bf16* dfmap,
+                         hipStream_t s) {
+  const int64_t tot = B * Hh * (C / 8);
+  hipLaunchKernelGGL(row_pool_bwd_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, dout, B, (int)Hh,
+                     (int)Ww, C, (int)n, dfmap);
+}
+
+}  // namespace mmu

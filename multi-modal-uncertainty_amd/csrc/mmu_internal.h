@@ -1,0 +1,103 @@
+// Internal launcher interfaces between capi.cpp and the .hip translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/mmu.h"
+
+typedef __bf16 bf16;
+
+namespace mmu {
+
+struct GemmParams {
+  const bf16* A;
+  const bf16* B;
+  void* C;
+  int64_t lda, ldb, ldc, M, N, K, sA, sB, sC;
+  int tiles_m, tiles_n;
+  // epilogue (flattened mmu_epilogue)
+  int kind, accumulate;
+  const float* bias;
+  int64_t bias_bstride;
+  const void* residual;
+  int64_t ldr, res_bstride;
+  void* aux;
+  int64_t ldx, aux_bstride;
+  float* colsum;
+  int64_t colsum_bstride;
+  float drop_p;
+  uint64_t seed;
+};
+
+void gemm_launch(const GemmParams& p, bool a_kmajor, bool b_kmajor, bool f32out, int batch, hipStream_t s);
+void colsum_reduce_launch(const float* part, int64_t parts, int64_t N, float* out, int acc, hipStream_t s);
+void colsum_bf16_launch(const bf16* X, int64_t M, int64_t N, int64_t ld, float* part, float* out, int acc,
+                        hipStream_t s);
+
+struct AttnParams {
+  const bf16* qkv;
+  int64_t ld_qkv;
+  const float* keymask;
+  const bf16* o;
+  int64_t ld_o;
+  const bf16* dout;
+  int64_t ld_do;
+  float* lse;
+  float* delta;
+  bf16* out;   // O (fwd) or dQKV (bwd)
+  int64_t ld_out;
+  int batch, L, heads;
+  float drop_p;
+  uint64_t seed;
+};
+void attention_fwd_launch(const AttnParams& p, hipStream_t s);
+void attention_bwd_launch(const AttnParams& p, hipStream_t s);
+
+void layernorm_fwd_launch(const bf16* X, const float* w, const float* b, bf16* Y, float* mean, float* rstd,
+                          int64_t rows, int64_t H, float eps, hipStream_t s);
+void layernorm_bwd_launch(const bf16* dY, const bf16* X, const float* mean, const float* rstd, const float* w,
+                          bf16* dX, bf16* dXdrop, float drop_p, uint64_t seed, float* pdw, float* pdb,
+                          float* pdbias, int64_t rows, int64_t H, int64_t rows_per_part, hipStream_t s);
+
+struct EmbedParams {
+  const int64_t *ids, *seg, *txt_mask, *idx;
+  const float *proj, *word, *pos, *type, *ln_w, *ln_b;
+  float eps, drop_txt, drop_img;
+  uint64_t seed;
+  int64_t cls_id, sep_id, V, B, T, n_img, Lout, H;
+  bf16* X;
+  float *keymask, *mean, *rstd;
+};
+void embed_fwd_launch(const EmbedParams& p, hipStream_t s);
+struct EmbedBwdParams {
+  const bf16* dX;
+  const int64_t *ids, *seg;
+  const float *proj, *word, *pos, *type, *ln_w, *mean, *rstd;
+  int64_t cls_id, sep_id, B, T, n_img, H;
+  float drop_txt, drop_img;
+  uint64_t seed;
+  float *d_word, *d_pos, *d_type, *d_ln_w, *d_ln_b, *d_proj, *ws;
+};
+void embed_bwd_launch(const EmbedBwdParams& p, hipStream_t s);
+void row_pool_fwd_launch(const bf16* fmap, int64_t B, int64_t Hh, int64_t Ww, int64_t C, int64_t n, float* out,
+                         hipStream_t s);
+void row_pool_bwd_launch(const float* dout, int64_t B, int64_t Hh, int64_t Ww, int64_t C, int64_t n, bf16* dfmap,
+                         hipStream_t s);
+
+struct AdamParams {
+  float *params, *m, *v;
+  const float* grads;
+  bf16* bf16_copy;
+  const int64_t* table;
+  int32_t* steps;
+  int64_t n_tensors, total;
+  float lr_decay, lr_nodecay, wd, warmup, t_total, b1, b2, eps, max_grad_norm;
+  float* ws;
+  int64_t ws_floats;
+};
+int bertadam_launch(const AdamParams& p, hipStream_t s, const char** err);
+
+void uncertainty_launch(const float* logits, const int64_t* y, int64_t S, int64_t R, int64_t C, float* p_bar,
+                        float* nll, float* conf, float* correct, hipStream_t s);
+void ece_bins_launch(const float* conf, const float* correct, int64_t S, int64_t n_bins, float* out, hipStream_t s);
+
+}  // namespace mmu

@@ -1,0 +1,118 @@
+// Fused multi-tensor BertAdam (gfx950).
+//
+// pytorch_pretrained_bert 0.6.x BertAdam as constructed at train.py:142-147:
+// per-tensor clip_grad_norm_(p, max_grad_norm), m/v moments without bias
+// correction, decoupled weight decay added to the update, lr * warmup_linear(
+// step / t_total) with the step read BEFORE its increment.  Three launches over the
+// flat f32 parameter / gradient / moment buffers (HBM-bound, ~28 B per element):
+//   1. per-chunk sum of squares of the gradient
+//   2. per tensor: norm -> clip coefficient, scheduled lr, step += 1
+//   3. per chunk: moment + parameter update, optional bf16 weight copy for the GEMMs
+// Tensor table (7 int64 each): offset, numel, group, bf16_offset, active,
+// first_chunk, n_chunks.  Chunk table (3 int64 each): tensor, start, len.
+#include "mmu_common.h"
+#include "mmu_internal.h"
+
+namespace mmu {
+
+struct AdamDev {
+  float *params, *m, *v;
+  const float* grads;
+  bf16* bf16_copy;
+  const int64_t* table;
+  const int64_t* chunks;
+  int32_t* steps;
+  int64_t n_tensors, n_chunks;
+  float lr_decay, lr_nodecay, wd, warmup, t_total, b1, b2, eps, max_grad_norm;
+  float* ws;  // [n_chunks] partial sq-norms, then [n_tensors][2] (coef, lr_eff)
+};
+
+__global__ __launch_bounds__(256) void adam_sqnorm_kernel(AdamDev a) {
+  const int64_t ci = blockIdx.x;
+  const int64_t tid = a.chunks[3 * ci], start = a.chunks[3 * ci + 1], len = a.chunks[3 * ci + 2];
+  if (!a.table[7 * tid + 4]) {
+    if (threadIdx.x == 0) a.ws[ci] = 0.f;
+    return;
+  }
+  const float* g = a.grads + a.table[7 * tid] + start;
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < len; i += 256) { float x = g[i]; s += x * x; }
+  __shared__ float red[4];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) a.ws[ci] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void adam_coef_kernel(AdamDev a) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.n_tensors) return;
+  const int64_t* T = a.table + 7 * t;
+  float* out = a.ws + a.n_chunks + 2 * t;
+  if (!T[4]) { out[0] = 1.f; out[1] = 0.f; return; }
+  double sq = 0.0;
+  for (int64_t c = T[5]; c < T[5] + T[6]; ++c) sq += a.ws[c];
+  const double nrm = sqrt(sq);
+  double coef = 1.0;
+  if (a.max_grad_norm > 0.f) {
+    const double cc = a.max_grad_norm / (nrm + 1e-6);
+    if (cc < 1.0) coef = cc;
+  }
+  const int32_t st = a.steps[t];
+  double sched = 1.0;
+  if (a.t_total > 0.f) {
+    const double x = (double)st / a.t_total, w = a.warmup;
+    sched = x < w ? x / w : fmax((x - 1.0) / (w - 1.0), 0.0);
+  }
+  const double lr = T[2] == 0 ? a.lr_decay : a.lr_nodecay;
+  out[0] = (float)coef;
+  out[1] = (float)(lr * sched);
+  a.steps[t] = st + 1;
+}
+
+__global__ __launch_bounds__(256) void adam_update_kernel(AdamDev a) {
+  const int64_t ci = blockIdx.x;
+  const int64_t tid = a.chunks[3 * ci], start = a.chunks[3 * ci + 1], len = a.chunks[3 * ci + 2];
+  const int64_t* T = a.table + 7 * tid;
+  if (!T[4]) return;
+  const float coef = a.ws[a.n_chunks + 2 * tid], lr = a.ws[a.n_chunks + 2 * tid + 1];
+  const float wd = T[2] == 0 ? a.wd : 0.f;
+  const int64_t off = T[0] + start;
+  float* p = a.params + off;
+  float* m = a.m + off;
+  float* v = a.v + off;
+  const float* g = a.grads + off;
+  bf16* cp = T[3] >= 0 ? a.bf16_copy + T[3] + start : nullptr;
+  const float b1 = a.b1, b2 = a.b2, c1 = 1.f - a.b1, c2 = 1.f - a.b2;
+  for (int64_t i = threadIdx.x; i < len; i += 256) {
+    const float gr = g[i] * coef;
+    const float mm = b1 * m[i] + c1 * gr;
+    const float vv = b2 * v[i] + c2 * gr * gr;
+    m[i] = mm;
+    v[i] = vv;
+    float u = mm / (sqrtf(vv) + a.eps);
+    if (wd > 0.f) u += wd * p[i];
+    const float np = p[i] - lr * u;
+    p[i] = np;
+    if (cp) cp[i] = f2bf(np);
+  }
+}
+
+int bertadam_launch(const AdamParams& P, hipStream_t s, const char** err) {
+  (void)err;
+  AdamDev a;
+  a.params = P.params; a.m = P.m; a.v = P.v; a.grads = P.grads; a.bf16_copy = P.bf16_copy;
+  a.table = P.table; a.steps = P.steps; a.n_tensors = P.n_tensors;
+  // the chunk table follows the tensor table: caller packs [7*n_tensors | 3*n_chunks]; total = n_chunks
+  a.chunks = P.table + 7 * P.n_tensors;
+  a.n_chunks = P.total;
+  a.lr_decay = P.lr_decay; a.lr_nodecay = P.lr_nodecay; a.wd = P.wd; a.warmup = P.warmup;
+  a.t_total = P.t_total; a.b1 = P.b1; a.b2 = P.b2; a.eps = P.eps; a.max_grad_norm = P.max_grad_norm;
+  a.ws = P.ws;
+  hipLaunchKernelGGL(adam_sqnorm_kernel, dim3((unsigned)a.n_chunks), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(adam_coef_kernel, dim3((unsigned)((a.n_tensors + 255) / 256)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(adam_update_kernel, dim3((unsigned)a.n_chunks), dim3(256), 0, s, a);
+  return 0;
+}
+
+}  // namespace mmu

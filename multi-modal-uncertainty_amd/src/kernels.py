@@ -1,0 +1,177 @@
+"""torch-tensor front-end of the HIP kernels (pointers + current HIP stream).
+
+Every function enqueues on ``torch.cuda.current_stream()`` of the tensors'
+device and raises if a tensor is not on a HIP device or has the wrong
+dtype/layout -- there is no CPU fallback ("no fallback").
+"""
+import ctypes
+
+import torch
+
+from . import _native as N
+from ._native import Epilogue, EPI_STORE, EPI_BIAS_GELU, EPI_BIAS_DROP_RES, EPI_DGELU, EPI_ADD_RES  # noqa: F401
+
+
+def _dev_check(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise N.NativeError("mmu kernels need tensors on a HIP (cuda) device; got CPU tensor "
+                                f"{tuple(t.shape)} {t.dtype}")
+
+
+def _stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _want(t, dtype, name):
+    if t.dtype != dtype:
+        raise N.NativeError(f"{name}: expected {dtype}, got {t.dtype}")
+
+
+def epilogue(kind=EPI_STORE, bias=None, residual=None, aux=None, colsum=None, drop_p=0.0, seed=0, accumulate=False,
+             ldr=0, ldx=0, bias_bstride=0, res_bstride=0, aux_bstride=0, colsum_bstride=0):
+    e = Epilogue()
+    e.kind, e.accumulate = kind, int(accumulate)
+    e.bias, e.bias_bstride = _ptr(bias), bias_bstride
+    e.residual, e.ldr, e.res_bstride = _ptr(residual), ldr or (residual.shape[-1] if residual is not None else 0), \
+        res_bstride
+    e.aux, e.ldx, e.aux_bstride = _ptr(aux), ldx or (aux.shape[-1] if aux is not None else 0), aux_bstride
+    e.colsum, e.colsum_bstride = _ptr(colsum), colsum_bstride
+    e.drop_p, e.seed = float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF
+    return e
+
+
+def gemm(A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, M, N_, K, epi=None, batch=1, sA=0, sB=0, sC=0):
+    """C[m,n] = sum_k A(m,k) B(n,k) (+ fused epilogue); see mmu_gemm in include/mmu.h."""
+    _dev_check(A, B, C)
+    _want(A, torch.bfloat16, "gemm A")
+    _want(B, torch.bfloat16, "gemm B")
+    cdt = N.MMU_F32 if C.dtype == torch.float32 else N.MMU_BF16
+    if C.dtype not in (torch.float32, torch.bfloat16):
+        raise N.NativeError("gemm C must be f32 or bf16")
+    N.call("mmu_gemm", _ptr(A), lda, int(a_kmajor), _ptr(B), ldb, int(b_kmajor), _ptr(C), ldc, cdt, M, N_, K,
+           batch, sA, sB, sC, ctypes.byref(epi) if epi is not None else None, _stream(C))
+    return C
+
+
+def colsum_partial_rows(M):
+    """rows of the partial column-sum table a GEMM epilogue writes for M output rows"""
+    return 2 * ((M + 127) // 128)
+
+
+def colsum_reduce(partial, out, accumulate=False):
+    _dev_check(partial, out)
+    N.call("mmu_colsum_reduce", _ptr(partial), partial.shape[0], partial.shape[1], _ptr(out), int(accumulate),
+           _stream(out))
+
+
+def colsum_bf16(X, out, partial=None, accumulate=False):
+    _dev_check(X, out)
+    M, N_ = X.shape
+    if partial is None:
+        partial = torch.empty(((M + 255) // 256, N_), dtype=torch.float32, device=X.device)
+    N.call("mmu_colsum_bf16", _ptr(X), M, N_, X.stride(0), _ptr(partial), _ptr(out), int(accumulate), _stream(X))
+
+
+def attention_fwd(qkv, keymask, O, lse, batch, L, heads=12, drop_p=0.0, seed=0):
+    _dev_check(qkv, keymask, O, lse)
+    _want(qkv, torch.bfloat16, "attention qkv")
+    N.call("mmu_attention_fwd", _ptr(qkv), qkv.stride(0), _ptr(keymask), _ptr(O), O.stride(0), _ptr(lse), batch, L,
+           heads, float(drop_p), int(seed), _stream(qkv))
+
+
+def attention_bwd(qkv, keymask, O, dO, lse, delta, dqkv, batch, L, heads=12, drop_p=0.0, seed=0):
+    _dev_check(qkv, keymask, O, dO, lse, delta, dqkv)
+    N.call("mmu_attention_bwd", _ptr(qkv), qkv.stride(0), _ptr(keymask), _ptr(O), O.stride(0), _ptr(dO), dO.stride(0),
+           _ptr(lse), _ptr(delta), _ptr(dqkv), dqkv.stride(0), batch, L, heads, float(drop_p), int(seed),
+           _stream(qkv))
+
+
+def layernorm_fwd(X, w, b, Y, mean, rstd, eps=1e-12):
+    _dev_check(X, w, b, Y, mean, rstd)
+    rows, H = X.shape
+    N.call("mmu_layernorm_fwd", _ptr(X), _ptr(w), _ptr(b), _ptr(Y), _ptr(mean), _ptr(rstd), rows, H, float(eps),
+           _stream(X))
+
+
+LN_ROWS_PER_PART = 64
+
+
+def layernorm_bwd(dY, X, mean, rstd, w, dX, dXdrop=None, drop_p=0.0, seed=0, part_dw=None, part_db=None,
+                  part_dbias=None):
+    _dev_check(dY, X, mean, rstd, w, dX)
+    rows, H = X.shape
+    N.call("mmu_layernorm_bwd", _ptr(dY), _ptr(X), _ptr(mean), _ptr(rstd), _ptr(w), _ptr(dX), _ptr(dXdrop),
+           float(drop_p), int(seed), _ptr(part_dw), _ptr(part_db), _ptr(part_dbias), rows, H, LN_ROWS_PER_PART,
+           _stream(X))
+
+
+def ln_parts(rows):
+    return (rows + LN_ROWS_PER_PART - 1) // LN_ROWS_PER_PART
+
+
+def embed_fwd(ids, seg, txt_mask, proj, word, pos, typ, ln_w, ln_b, eps, cls_id, sep_id, idx, V, B, T, n_img, Lout,
+              X, keymask, mean=None, rstd=None, drop_txt=0.0, drop_img=0.0, seed=0):
+    _dev_check(proj, word, pos, typ, ln_w, ln_b, X, keymask)
+    N.call("mmu_embed_fwd", _ptr(ids), _ptr(seg), _ptr(txt_mask), _ptr(proj), _ptr(word), _ptr(pos), _ptr(typ),
+           _ptr(ln_w), _ptr(ln_b), float(eps), int(cls_id), int(sep_id), _ptr(idx), V, B, T, n_img, Lout, 768,
+           float(drop_txt), float(drop_img), int(seed), _ptr(X), _ptr(keymask), _ptr(mean), _ptr(rstd), _stream(X))
+
+
+def embed_bwd(dX, ids, seg, proj, word, pos, typ, ln_w, mean, rstd, cls_id, sep_id, B, T, n_img, d_word, d_pos,
+              d_type, d_ln_w, d_ln_b, d_proj, drop_txt=0.0, drop_img=0.0, seed=0):
+    _dev_check(dX, proj, word, d_word, d_proj)
+    S = n_img + 2 + T
+    rows = B * S
+    ws = torch.empty(rows * 768 + 2 * ((rows + 63) // 64) * 768, dtype=torch.float32, device=dX.device)
+    N.call("mmu_embed_bwd", _ptr(dX), _ptr(ids), _ptr(seg), _ptr(proj), _ptr(word), _ptr(pos), _ptr(typ),
+           _ptr(ln_w), _ptr(mean), _ptr(rstd), int(cls_id), int(sep_id), B, T, n_img, 768, float(drop_txt),
+           float(drop_img), int(seed), _ptr(d_word),
+           _ptr(d_pos), _ptr(d_type), _ptr(d_ln_w), _ptr(d_ln_b), _ptr(d_proj), _ptr(ws), _stream(dX))
+
+
+def row_pool_fwd(fmap_nhwc, n, out):
+    _dev_check(fmap_nhwc, out)
+    B, Hh, Ww, C = fmap_nhwc.shape
+    N.call("mmu_row_pool_fwd", _ptr(fmap_nhwc), B, Hh, Ww, C, n, _ptr(out), _stream(out))
+
+
+def row_pool_bwd(dout, n, dfmap_nhwc):
+    _dev_check(dout, dfmap_nhwc)
+    B, Hh, Ww, C = dfmap_nhwc.shape
+    N.call("mmu_row_pool_bwd", _ptr(dout), B, Hh, Ww, C, n, _ptr(dfmap_nhwc), _stream(dout))
+
+
+def bertadam_step(params, grads, m, v, bf16_copy, table, steps, n_tensors, n_chunks, lr_decay, lr_nodecay, wd,
+                  warmup, t_total, b1, b2, eps, max_grad_norm, ws):
+    _dev_check(params, grads, m, v, table, steps, ws)
+    N.call("mmu_bertadam_step", _ptr(params), _ptr(grads), _ptr(m), _ptr(v), _ptr(bf16_copy), _ptr(table),
+           _ptr(steps), n_tensors, n_chunks, float(lr_decay), float(lr_nodecay), float(wd), float(warmup),
+           float(t_total), float(b1), float(b2), float(eps), float(max_grad_norm), _ptr(ws), ws.numel(),
+           _stream(params))
+
+
+def uncertainty(logits, y, p_bar, nll, conf, correct):
+    _dev_check(logits, y, p_bar, nll, conf, correct)
+    S, R, C = logits.shape
+    N.call("mmu_uncertainty", _ptr(logits), _ptr(y), S, R, C, _ptr(p_bar), _ptr(nll), _ptr(conf), _ptr(correct),
+           _stream(logits))
+
+
+def ece_bins(conf, correct, n_bins, out):
+    _dev_check(conf, correct, out)
+    N.call("mmu_ece_bins", _ptr(conf), _ptr(correct), conf.numel(), n_bins, _ptr(out), _stream(conf))
+
+
+def timing_enable(on=True):
+    N.call("mmu_timing_enable", int(on))
+
+
+def timing_read():
+    ms, n, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+    N.call("mmu_timing_read", ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl))
+    return ms.value, n.value, fl.value

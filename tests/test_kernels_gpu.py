@@ -1,0 +1,337 @@
+"""Kernel-level parity of the HIP path against plain PyTorch fp32 on the same inputs.
+
+Tolerances: bf16 inputs with fp32 accumulation; outputs compared at bf16
+resolution (rel 1e-2 of the output scale) unless stated.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def K():
+    from src import kernels
+    return kernels
+
+
+def rnd(*shape, dev, scale=1.0, dtype=torch.bfloat16, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dev).to(dtype)
+
+
+def close(a, b, rtol=1e-2, atol_frac=1e-2):
+    a, b = a.float(), b.float()
+    scale = b.abs().max().item() + 1e-6
+    err = (a - b).abs().max().item()
+    assert err <= atol_frac * scale + rtol * 0, f"max err {err:.3e} vs scale {scale:.3e}"
+
+
+def op(t, kmajor, rows, K_):
+    """logical [rows, K] operand from a stored tensor (K-major: [rows,K]; else [K,rows])"""
+    return t.float() if kmajor else t.float().t()
+
+
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, False), (False, True)])
+@pytest.mark.parametrize("M,N,Kd", [(256, 128, 64), (384, 256, 192)])
+def test_gemm_layouts(dev, ak, bk, M, N, Kd):
+    k = K()
+    A = rnd(M, Kd, dev=dev, seed=1) if ak else rnd(Kd, M, dev=dev, seed=1)
+    B = rnd(N, Kd, dev=dev, seed=2) if bk else rnd(Kd, N, dev=dev, seed=2)
+    C = torch.empty(M, N, dtype=torch.float32, device=dev)
+    k.gemm(A, A.shape[1], ak, B, B.shape[1], bk, C, N, M, N, Kd)
+    ref = op(A, ak, M, Kd) @ op(B, bk, N, Kd).t()
+    torch.testing.assert_close(C, ref, rtol=1e-4, atol=1e-3)
+
+
+def test_gemm_m_tail_bias_bf16(dev):
+    k = K()
+    M, N, Kd = 200, 256, 128
+    A, B = rnd(M, Kd, dev=dev, seed=3), rnd(N, Kd, dev=dev, seed=4)
+    bias = torch.randn(N, device=dev)
+    C = torch.full((M + 8, N), 7.0, dtype=torch.bfloat16, device=dev)
+    k.gemm(A, Kd, True, B, Kd, True, C, N, M, N, Kd, epi=k.epilogue(k.EPI_STORE, bias=bias))
+    ref = A.float() @ B.float().t() + bias
+    close(C[:M], ref)
+    assert (C[M:] == 7.0).all(), "rows beyond M were written"
+
+
+def test_gemm_k_tail_weight_grad(dev):
+    k = K()
+    Ktok, M, N = 1000, 256, 384  # dW = dY^T X over a token count that is not a tile multiple
+    dY, X = rnd(Ktok, M, dev=dev, seed=5), rnd(Ktok, N, dev=dev, seed=6)
+    C = torch.ones(M, N, dtype=torch.float32, device=dev)
+    k.gemm(dY, M, False, X, N, False, C, N, M, N, Ktok, epi=k.epilogue(k.EPI_STORE, accumulate=True))
+    ref = dY.float().t() @ X.float() + 1.0
+    torch.testing.assert_close(C, ref, rtol=1e-4, atol=2e-3)
+
+
+def test_gemm_gelu_dgelu_colsum(dev):
+    k = K()
+    M, N, Kd = 300, 256, 128
+    A, B = rnd(M, Kd, dev=dev, seed=7), rnd(N, Kd, dev=dev, seed=8, scale=0.2)
+    bias = torch.randn(N, device=dev) * 0.5
+    Z = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    Hh = torch.empty_like(Z)
+    k.gemm(A, Kd, True, B, Kd, True, Hh, N, M, N, Kd, epi=k.epilogue(k.EPI_BIAS_GELU, bias=bias, aux=Z))
+    z = A.float() @ B.float().t() + bias
+    close(Z, z)
+    close(Hh, torch.nn.functional.gelu(z))
+    # dgelu with column sums
+    G = rnd(M, Kd, dev=dev, seed=9)
+    W = rnd(Kd, N, dev=dev, seed=10, scale=0.2)  # stored [K][N] -> MN-major B
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    part = torch.empty(k.colsum_partial_rows(M), N, dtype=torch.float32, device=dev)
+    k.gemm(G, Kd, True, W, N, False, out, N, M, N, Kd, epi=k.epilogue(k.EPI_DGELU, aux=Z, colsum=part))
+    zz = Z.float().requires_grad_(True)
+    g = torch.autograd.grad(torch.nn.functional.gelu(zz), zz, G.float() @ W.float())[0]
+    close(out, g)
+    cs = torch.empty(N, device=dev)
+    k.colsum_reduce(part, cs)
+    torch.testing.assert_close(cs, g.sum(0), rtol=2e-2, atol=2e-2 * g.abs().sum(0).max().item() / 50)
+
+
+def test_gemm_bias_dropout_residual(dev):
+    k = K()
+    M, N, Kd = 512, 768, 256
+    A, B = rnd(M, Kd, dev=dev, seed=11), rnd(N, Kd, dev=dev, seed=12, scale=0.1)
+    bias = torch.randn(N, device=dev) * 0.1
+    R = rnd(M, N, dev=dev, seed=13)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    k.gemm(A, Kd, True, B, Kd, True, out, N, M, N, Kd,
+           epi=k.epilogue(k.EPI_BIAS_DROP_RES, bias=bias, residual=R, drop_p=0.0))
+    y = A.float() @ B.float().t() + bias
+    close(out, R.float() + y)
+    p = 0.1
+    k.gemm(A, Kd, True, B, Kd, True, out, N, M, N, Kd,
+           epi=k.epilogue(k.EPI_BIAS_DROP_RES, bias=bias, residual=R, drop_p=p, seed=1234))
+    d = out.float() - R.float()
+    kept = (d - y / (1 - p)).abs() <= 0.05 * (y.abs() / (1 - p)) + 0.05
+    dropped = d.abs() <= 0.02 * (R.float().abs() + 1)
+    assert (kept | dropped).float().mean().item() > 0.999
+    rate = (dropped & ~kept).float().mean().item()
+    assert abs(rate - p) < 0.01, rate
+
+
+def test_gemm_batched(dev):
+    k = K()
+    Bt, M, N, Kd = 3, 128, 128, 64
+    A, B = rnd(Bt, M, Kd, dev=dev, seed=14), rnd(Bt, N, Kd, dev=dev, seed=15)
+    C = torch.empty(Bt, M, N, dtype=torch.float32, device=dev)
+    k.gemm(A, Kd, True, B, Kd, True, C, N, M, N, Kd, batch=Bt, sA=M * Kd, sB=N * Kd, sC=M * N)
+    torch.testing.assert_close(C, A.float() @ B.float().transpose(1, 2), rtol=1e-4, atol=1e-3)
+
+
+def test_gemm_rejects_bad_shapes(dev):
+    k = K()
+    from src._native import NativeError
+    A = rnd(128, 64, dev=dev)
+    B = rnd(100, 64, dev=dev)
+    C = torch.empty(128, 100, device=dev)
+    with pytest.raises(NativeError, match="multiple of 128"):
+        k.gemm(A, 64, True, B, 64, True, C, 100, 128, 100, 64)
+
+
+# ----------------------------------------------------------------------------- attention
+def attn_ref(qkv, keymask, B, L, heads=12, dropmask=None, p=0.0):
+    q, kk, v = qkv.float().view(B, L, 3, heads, 64).permute(2, 0, 3, 1, 4)
+    s = q @ kk.transpose(-1, -2) / 8.0 + keymask.view(B, 1, 1, L)
+    lse = torch.logsumexp(s, -1)
+    P = torch.softmax(s, -1)
+    if dropmask is not None:
+        P = P * dropmask / (1 - p)
+    o = (P @ v).permute(0, 2, 1, 3).reshape(B * L, heads * 64)
+    return o, lse.reshape(B * heads, L)
+
+
+def make_attn_inputs(dev, B, L, pad=True, seed=0, scale=1.0):
+    qkv = rnd(B * L, 3 * 768, dev=dev, seed=seed, scale=scale)
+    km = torch.zeros(B, L, device=dev)
+    if pad and L > 6:
+        km[0, L - L // 3:] = -10000.0
+    return qkv, km
+
+
+@pytest.mark.parametrize("B,L", [(2, 5), (2, 17), (1, 64), (2, 130), (2, 513)])
+def test_attention_fwd(dev, B, L):
+    k = K()
+    qkv, km = make_attn_inputs(dev, B, L, seed=L, scale=2.0)
+    O = torch.empty(B * L, 768, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(B * 12, L, device=dev)
+    k.attention_fwd(qkv, km, O, lse, B, L)
+    o_ref, lse_ref = attn_ref(qkv, km, B, L)
+    close(O, o_ref)
+    torch.testing.assert_close(lse, lse_ref, rtol=1e-4, atol=2e-3)
+
+
+@pytest.mark.parametrize("B,L", [(2, 5), (2, 17), (2, 130), (1, 513)])
+def test_attention_bwd(dev, B, L):
+    k = K()
+    qkv, km = make_attn_inputs(dev, B, L, seed=100 + L, scale=1.5)
+    O = torch.empty(B * L, 768, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(B * 12, L, device=dev)
+    k.attention_fwd(qkv, km, O, lse, B, L)
+    dO = rnd(B * L, 768, dev=dev, seed=200 + L)
+    dqkv = torch.zeros(B * L, 2304, dtype=torch.bfloat16, device=dev)
+    delta = torch.empty(B * 12, L, device=dev)
+    k.attention_bwd(qkv, km, O, dO, lse, delta, dqkv, B, L)
+    x = qkv.float().requires_grad_(True)
+    o_ref, _ = attn_ref(x, km, B, L)
+    (g,) = torch.autograd.grad(o_ref, x, dO.float())
+    for part in range(3):
+        close(dqkv[:, 768 * part:768 * (part + 1)], g[:, 768 * part:768 * (part + 1)], atol_frac=2e-2)
+
+
+def test_attention_dropout_consistent(dev):
+    """Recover the kernel's dropped-P matrix with one-hot V rows (L <= 64), then check
+    (a) its drop rate, (b) fwd == P*mask/(1-p) V on random V, (c) bwd matches autograd with that mask."""
+    k = K()
+    B, L, p, seed = 2, 60, 0.2, 99
+    qkv, km = make_attn_inputs(dev, B, L, pad=False, seed=5, scale=1.0)
+    probe = qkv.clone().view(B, L, 3, 12, 64)
+    eye = torch.zeros(L, 64, device=dev)
+    eye[torch.arange(L), torch.arange(L)] = 1.0
+    probe[:, :, 2] = eye.view(1, L, 1, 64).to(torch.bfloat16)
+    probe = probe.view(B * L, 2304)
+    O = torch.empty(B * L, 768, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(B * 12, L, device=dev)
+    k.attention_fwd(probe, km, O, lse, B, L, drop_p=p, seed=seed)
+    Pd = O.float().view(B, L, 12, 64).permute(0, 2, 1, 3)[..., :L]  # [B,h,q,key] = P*mask/(1-p)
+    mask = (Pd > 0).float()
+    rate = 1 - mask.mean().item()
+    assert abs(rate - p) < 0.02, rate
+    # (b) forward on the real V with the recovered mask
+    k.attention_fwd(qkv, km, O, lse, B, L, drop_p=p, seed=seed)
+    o_ref, _ = attn_ref(qkv, km, B, L, dropmask=mask, p=p)
+    close(O, o_ref, atol_frac=2e-2)
+    # (c) backward
+    dO = rnd(B * L, 768, dev=dev, seed=7)
+    dqkv = torch.zeros(B * L, 2304, dtype=torch.bfloat16, device=dev)
+    delta = torch.empty(B * 12, L, device=dev)
+    k.attention_bwd(qkv, km, O, dO, lse, delta, dqkv, B, L, drop_p=p, seed=seed)
+    x = qkv.float().requires_grad_(True)
+    o2, _ = attn_ref(x, km, B, L, dropmask=mask, p=p)
+    (g,) = torch.autograd.grad(o2, x, dO.float())
+    for part in range(3):
+        close(dqkv[:, 768 * part:768 * (part + 1)], g[:, 768 * part:768 * (part + 1)], atol_frac=3e-2)
+
+
+# ----------------------------------------------------------------------------- layernorm
+def test_layernorm_fwd_bwd(dev):
+    k = K()
+    rows, H, p, seed = 333, 768, 0.1, 77
+    X = rnd(rows, H, dev=dev, seed=20, scale=3.0)
+    w = torch.randn(H, device=dev) * 0.1 + 1
+    b = torch.randn(H, device=dev) * 0.1
+    Y = torch.empty_like(X)
+    mean, rstd = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+    k.layernorm_fwd(X, w, b, Y, mean, rstd)
+    xr = X.float().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (H,), wr, br, eps=1e-12)
+    close(Y, yr)
+    dY = rnd(rows, H, dev=dev, seed=21)
+    dX, dXd = torch.empty_like(X), torch.empty_like(X)
+    P = k.ln_parts(rows)
+    pw, pb, pbias = (torch.empty(P, H, device=dev) for _ in range(3))
+    k.layernorm_bwd(dY, X, mean, rstd, w, dX, dXd, p, seed, pw, pb, pbias)
+    gx, gw, gb = torch.autograd.grad(yr, (xr, wr, br), dY.float())
+    close(dX, gx)
+    sw, sb, sbias = torch.empty(H, device=dev), torch.empty(H, device=dev), torch.empty(H, device=dev)
+    k.colsum_reduce(pw, sw)
+    k.colsum_reduce(pb, sb)
+    k.colsum_reduce(pbias, sbias)
+    torch.testing.assert_close(sw, gw, rtol=1e-2, atol=0.05)
+    torch.testing.assert_close(sb, gb, rtol=1e-2, atol=0.05)
+    # dropout backward: every element either dX/(1-p) or 0, ~p dropped, colsum matches
+    dx, dd = dX.float(), dXd.float()
+    kept = (dd - dx / (1 - p)).abs() <= 0.02 * dx.abs() / (1 - p) + 1e-3
+    zero = dd == 0
+    assert (kept | zero).all()
+    assert abs(zero.float().mean().item() - p) < 0.01
+    torch.testing.assert_close(sbias, dd.sum(0), rtol=1e-2, atol=0.05)
+
+
+# ----------------------------------------------------------------------------- pooling / adam / uncertainty
+def test_row_pool(dev):
+    k = K()
+    B, C = 3, 2048
+    f = rnd(B, 2048, 7, 7, dev=dev, seed=30).contiguous(memory_format=torch.channels_last)
+    out = torch.empty(B, 3, C, device=dev)
+    k.row_pool_fwd(f.permute(0, 2, 3, 1), 3, out)
+    fr = f.float().requires_grad_(True)
+    ref = torch.nn.functional.adaptive_avg_pool2d(fr, (3, 1)).flatten(2).transpose(1, 2)
+    torch.testing.assert_close(out, ref, rtol=1e-3, atol=1e-3)
+    d = torch.randn(B, 3, C, device=dev)
+    df = torch.empty_like(f)
+    k.row_pool_bwd(d, 3, df.permute(0, 2, 3, 1))
+    (g,) = torch.autograd.grad(ref, fr, d)
+    close(df, g)
+
+
+def test_bertadam_matches_restatement(dev):
+    k = K()
+    from oracle.bertadam_ref import bertadam_step
+    sizes = [1000, 70000, 5, 768 * 3]
+    groups = [0, 0, 1, 1]
+    active = [1, 1, 1, 0]
+    g = torch.Generator().manual_seed(0)
+    ps = [torch.randn(n, generator=g) for n in sizes]
+    gs = [torch.randn(n, generator=g) * (3.0 if i == 1 else 0.01) for i, n in enumerate(sizes)]
+    offs = np.cumsum([0] + sizes)
+    flat_p = torch.cat(ps).to(dev)
+    flat_g = torch.cat(gs).to(dev)
+    m, v = torch.zeros_like(flat_p), torch.zeros_like(flat_p)
+    copy = torch.zeros(sum(sizes), dtype=torch.bfloat16, device=dev)
+    CH = 4096
+    chunks, tab = [], []
+    for t, n in enumerate(sizes):
+        first = len(chunks)
+        for s in range(0, n, CH):
+            chunks.append((t, s, min(CH, n - s)))
+        tab.append((offs[t], n, groups[t], offs[t] if t != 2 else -1, active[t], first, len(chunks) - first))
+    table = torch.tensor([x for r in tab for x in r] + [x for c in chunks for x in c], dtype=torch.int64, device=dev)
+    steps = torch.zeros(len(sizes), dtype=torch.int32, device=dev)
+    ws = torch.empty(len(chunks) + 2 * len(sizes), device=dev)
+    rp = [p.clone() for p in ps]
+    rm = [torch.zeros(n) for n in sizes]
+    rv = [torch.zeros(n) for n in sizes]
+    rs = [0] * len(sizes)
+    lr, warm, tt = 1e-3, 0.1, 20.0
+    for it in range(3):
+        k.bertadam_step(flat_p, flat_g, m, v, copy, table, steps, len(sizes), len(chunks), lr, lr, 0.01, warm, tt,
+                        0.9, 0.999, 1e-6, 1.0, ws)
+        act = [i for i in range(len(sizes)) if active[i]]
+        new = bertadam_step([rp[i] for i in act], [gs[i] for i in act], [rm[i] for i in act], [rv[i] for i in act],
+                            [rs[i] for i in act], lr, [0.01 if groups[i] == 0 else 0.0 for i in act], warm, tt)
+        for j, i in enumerate(act):
+            rs[i] = new[j]
+    torch.cuda.synchronize()
+    got = flat_p.cpu()
+    for t in range(len(sizes)):
+        torch.testing.assert_close(got[offs[t]:offs[t + 1]], rp[t], rtol=1e-5, atol=1e-6)
+    assert steps.cpu().tolist() == [3, 3, 3, 0]
+    torch.testing.assert_close(copy[:sizes[0]].float().cpu(), rp[0].bfloat16().float())
+
+
+def test_uncertainty_nll_ece(dev):
+    k = K()
+    from oracle import uncertainty_ref as U
+    S, R, C = 257, 15, 101
+    g = torch.Generator().manual_seed(3)
+    logits = torch.randn(S, R, C, generator=g) * 3
+    y = torch.randint(0, C, (S,), generator=g)
+    ld, yd = logits.to(dev), y.to(dev)
+    pb, nll, conf, cor = (torch.empty(S, C, device=dev), torch.empty(S, device=dev), torch.empty(S, device=dev),
+                          torch.empty(S, device=dev))
+    k.uncertainty(ld, yd, pb, nll, conf, cor)
+    bins = torch.empty(45, device=dev)
+    k.ece_bins(conf, cor, 15, bins)
+    pr = U.probs_mean(logits.numpy().transpose(1, 0, 2), member_axes=(0,))
+    np.testing.assert_allclose(pb.cpu().numpy(), pr, rtol=1e-4, atol=1e-6)
+    assert abs(nll.mean().item() - U.nll(pr, y.numpy())) < 1e-4
+    bb = bins.view(15, 3).cpu().double().numpy()
+    ece = float((np.abs(bb[:, 2] - bb[:, 1]) / S).sum())
+    assert abs(ece - U.ece(pr, y.numpy())) < 1e-4
