@@ -1,0 +1,188 @@
+"""MMBT (BERT-base + ResNet-152) training throughput on MI355X -- the BASELINE.json metric.
+
+One step = one optimizer step of the reference train loop over a synthetic Food-101
+batch (src/framework.py:276-319 with accum = 1, freeze epochs over, every one of the
+169.3 M parameters trainable): ResNet-152 + 12 fused BERT layers forward, CE loss,
+backward, (N>1: RCCL gradient all-reduce), fused BertAdam.  Global batch 256 of
+(224x224 image, 508 word-pieces -> 513 tokens) split over the N ranks.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints one JSON line (see README/DESIGN for the field definitions).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(REPO, "multi-modal-uncertainty_amd"), REPO]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+BERT_FLOP_PER_SAMPLE_LAYER_FWD = None  # filled from the shape: L*(24H^2 + 4LH)
+RESNET152_FWD_FLOP = 23.0e9            # per 224x224 sample (11.5 GMAC)
+PEAK_BF16_TFLOPS = 2500.0              # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--global-batch", type=int, default=256)
+    ap.add_argument("--text-len", type=int, default=508, help="word-pieces per sample (L = 5 + this)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=2)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def cpu_baseline(args, L_text):
+    """The oracle (fp32 CPU restatement, oracle/mmbt_ref.py) doing the same train step on host cores."""
+    from oracle import mmbt_ref as R
+    from oracle.bertadam_ref import bertadam_step
+    from oracle.weights import FULL, make_state_dict
+    torch.set_num_threads(args.cpu_threads)
+    sd = make_state_dict(0, FULL)
+    params = {}
+    for k, v in sd.items():
+        if v.is_floating_point() and id(v) not in {id(p) for p in params.values()} and "running" not in k:
+            params[k] = v.requires_grad_(True)
+    uniq = list({id(v): v for v in params.values()}.values())
+    ms = [torch.zeros_like(p) for p in uniq]
+    vs = [torch.zeros_like(p) for p in uniq]
+    steps = [0] * len(uniq)
+    B = args.cpu_batch
+    g = torch.Generator().manual_seed(0)
+    txt = torch.randint(1000, 30522, (B, L_text), generator=g)
+    mask = torch.ones(B, L_text, dtype=torch.long)
+    img = torch.randn(B, 3, 224, 224, generator=g)
+    y = torch.randint(0, 101, (B,), generator=g)
+    gen = torch.Generator().manual_seed(1)
+
+    def one():
+        nonlocal steps
+        for p in uniq:
+            p.grad = None
+        logits = R.forward(sd, txt, mask, mask, img, FULL, train=True, dropout=0.1, gen=gen)
+        R.cross_entropy(logits, y).backward()
+        with torch.no_grad():
+            steps = bertadam_step(uniq, [p.grad for p in uniq], ms, vs, steps, 5e-5, [0.01] * len(uniq), 0.1, 1000.0)
+
+    one()  # warm-up
+    t0 = time.perf_counter()
+    n = 2
+    for _ in range(n):
+        one()
+    dt = time.perf_counter() - t0
+    return {"value": round(B * n / dt, 4), "unit": "samples/s", "cores": args.cpu_threads, "kind": "port",
+            "sample": f"oracle fp32 train step (fwd+bwd+BertAdam), B={B}, L={L_text + 5}, {n} timed steps after 1 "
+                      f"warm-up, torch CPU {torch.get_num_threads()} threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    if args.global_batch % world:
+        raise SystemExit("global batch must divide evenly over ranks")
+    B = args.global_batch // world
+    T = args.text_len
+    L = T + 5
+
+    from src.mmbt import MultimodalBertClf
+    from src.optim import BertAdam
+    from src.testing import make_args, synthetic_batch
+    from src import kernels as K
+    from src.dp import GradBucketer, broadcast_parameters
+
+    torch.manual_seed(1234)
+    margs = make_args()
+    model = MultimodalBertClf(margs).to(dev)
+    named = list(model.named_parameters())
+    no_decay = ["bias", "LayerNorm.bias", "LayerNorm.weight"]
+    groups = [{"params": [p for n, p in named if not any(nd in n for nd in no_decay)], "weight_decay": 0.01},
+              {"params": [p for n, p in named if any(nd in n for nd in no_decay)], "weight_decay": 0.0}]
+    opt = BertAdam(groups, lr=5e-5, warmup=0.1, t_total=10000.0)
+    bucketer = None
+    if world > 1:
+        broadcast_parameters(model)
+        bucketer = GradBucketer(model)
+    x, y = synthetic_batch(B, T, seed=100 + rank, device=dev)
+    model.train()
+
+    def step():
+        opt.zero_grad()
+        loss = model.compute_loss(model(*x), y)
+        loss.backward()
+        if bucketer is not None:
+            bucketer.finish()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    K.timing_enable(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    gemm_ms, gemm_n, gemm_flops = K.timing_read()
+    K.timing_enable(False)
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    ms_step = 1000.0 * dt / args.steps
+    value = args.global_batch * args.steps / dt
+    H = 768
+    layer_fwd = L * (24 * H * H + 4 * L * H)
+    model_flop = 3 * (12 * layer_fwd + RESNET152_FWD_FLOP)
+    achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
+    out = {
+        "metric": "image+text samples/sec/node, MMBT Food-101 bs=256 seq=512; ECE/NLL parity",
+        "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded; random-init weights)",
+        "config": {"workload": "mmbt_train_step", "model": "MMBT bert-base-uncased + resnet152",
+                   "global_batch": args.global_batch, "per_rank_batch": B, "seq_len": 512, "tokens": L,
+                   "parallelism": f"dp{world}", "grad_accum": 1, "optimizer": "BertAdam (fused HIP)",
+                   "trainable_params": sum(p.numel() for p in model.parameters())},
+        "roofline": {"bound": "mfma", "kernel": "mmu_gemm (all BERT-layer GEMMs, fwd + bwd)",
+                     "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "launches": gemm_n, "avg_launch_ms": round(gemm_ms / max(gemm_n, 1), 4),
+                     "gemm_share_of_step": round(gemm_ms / args.steps / ms_step, 3) if ms_step else None},
+        "model_tflops_per_step_per_rank": round(B * model_flop / 1e12, 2),
+        "model_tflops_achieved": round(B * model_flop * world / (ms_step * 1e-3) / 1e12, 1),
+        "final_loss": round(float(loss.item()), 4),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args, T)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

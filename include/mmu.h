@@ -107,7 +107,10 @@ int mmu_attention_bwd(const void* QKV, int64_t ld_qkv, const float* keymask,
  */
 int mmu_layernorm_fwd(const void* X, const float* w, const float* b, void* Y,
                       float* mean, float* rstd, int64_t rows, int64_t H, float eps,
-                      mmu_stream_t stream);
+                      int64_t group_rows, int64_t param_stride, mmu_stream_t stream);
+/* group_rows / param_stride: row r uses w/b + (r / group_rows) * param_stride, so the K
+ * members of a deep ensemble normalise in one launch (group_rows <= 0: one group).
+ * mean/rstd may both be NULL (inference). */
 /* Backward of y = LN(x): dX = LN'(dY) (+ dRes), optional dXdrop = dropout_bwd(dX)
  * (same (seed, m*H+n) stream as the producing BIAS_DROP_RES epilogue), and partial
  * column sums [ceil(rows/rows_per_part), H] for dgamma, dbeta and dbias

@@ -187,10 +187,14 @@ int mmu_attention_bwd(const void* QKV, int64_t ld_qkv, const float* keymask, con
 }
 
 int mmu_layernorm_fwd(const void* X, const float* w, const float* b, void* Y, float* mean, float* rstd, int64_t rows,
-                      int64_t H, float eps, mmu_stream_t stream) {
-  if (!X || !w || !b || !Y || !mean || !rstd) return fail("mmu_layernorm_fwd: null pointer");
+                      int64_t H, float eps, int64_t group_rows, int64_t param_stride, mmu_stream_t stream) {
+  if (!X || !w || !b || !Y) return fail("mmu_layernorm_fwd: null pointer");
+  if ((mean == nullptr) != (rstd == nullptr)) return fail("mmu_layernorm_fwd: mean/rstd must both be given or NULL");
   if (rows <= 0 || H % 256 || H > 1024) return fail("mmu_layernorm_fwd: H=%ld must be 256/512/768/1024", H);
-  layernorm_fwd_launch((const bf16*)X, w, b, (bf16*)Y, mean, rstd, rows, H, eps, (hipStream_t)stream);
+  if (group_rows <= 0) group_rows = rows;
+  if (param_stride < 0) return fail("mmu_layernorm_fwd: bad param_stride");
+  layernorm_fwd_launch((const bf16*)X, w, b, (bf16*)Y, mean, rstd, rows, H, eps, group_rows, param_stride,
+                       (hipStream_t)stream);
   return check_launch("mmu_layernorm_fwd");
 }
 

@@ -14,13 +14,18 @@ namespace mmu {
 
 constexpr int MAXV = 4;  // up to 4 slabs of 256 columns -> H <= 1024
 
+// rows are grouped: row r uses the affine params of group r / group_rows (stride pstride);
+// one group == the plain LN, K groups == K ensemble members in one launch
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16* __restrict__ X, const float* __restrict__ w,
                                                      const float* __restrict__ b, bf16* __restrict__ Y,
                                                      float* __restrict__ mean, float* __restrict__ rstd,
-                                                     int64_t rows, int H, float eps) {
+                                                     int64_t rows, int H, float eps, int64_t group_rows,
+                                                     int64_t pstride) {
   const int l = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
+  w += (row / group_rows) * pstride;
+  b += (row / group_rows) * pstride;
   const int nv = H / 256;
   float v[MAXV][4];
   float s = 0.f;
@@ -48,7 +53,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16* __restrict__ X,
                   f2bf((v[i][2] - mu) * rs * ww.z + bb.z), f2bf((v[i][3] - mu) * rs * ww.w + bb.w)};
       *(bf16x4*)(Y + row * H + c) = y;
     }
-  if (l == 0) { mean[row] = mu; rstd[row] = rs; }
+  if (l == 0 && mean) { mean[row] = mu; rstd[row] = rs; }
 }
 
 // block = 4 waves; each wave walks rows_per_part/4 rows; partial sums reduced through LDS
@@ -134,9 +139,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dY
 }
 
 void layernorm_fwd_launch(const bf16* X, const float* w, const float* b, bf16* Y, float* mean, float* rstd,
-                          int64_t rows, int64_t H, float eps, hipStream_t s) {
+                          int64_t rows, int64_t H, float eps, int64_t group_rows, int64_t pstride, hipStream_t s) {
   hipLaunchKernelGGL(ln_fwd_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, X, w, b, Y, mean, rstd,
-                     rows, (int)H, eps);
+                     rows, (int)H, eps, group_rows, pstride);
 }
 
 void layernorm_bwd_launch(const bf16* dY, const bf16* X, const float* mean, const float* rstd, const float* w,

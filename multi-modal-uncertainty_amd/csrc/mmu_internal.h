@@ -53,7 +53,7 @@ void attention_fwd_launch(const AttnParams& p, hipStream_t s);
 void attention_bwd_launch(const AttnParams& p, hipStream_t s);
 
 void layernorm_fwd_launch(const bf16* X, const float* w, const float* b, bf16* Y, float* mean, float* rstd,
-                          int64_t rows, int64_t H, float eps, hipStream_t s);
+                          int64_t rows, int64_t H, float eps, int64_t group_rows, int64_t pstride, hipStream_t s);
 void layernorm_bwd_launch(const bf16* dY, const bf16* X, const float* mean, const float* rstd, const float* w,
                           bf16* dX, bf16* dXdrop, float drop_p, uint64_t seed, float* pdw, float* pdb,
                           float* pdbias, int64_t rows, int64_t H, int64_t rows_per_part, hipStream_t s);

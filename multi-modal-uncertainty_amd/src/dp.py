@@ -1,0 +1,101 @@
+"""Data-parallel MMBT training: one process per GPU, RCCL gradient all-reduce over xGMI.
+
+The reference is single-device (train.py:307-310); this is the build's DP layer
+(SURVEY §8e).  Gradients already live in ONE flat f32 buffer laid out in the
+order backward completes them (src/params.py), so buckets are plain contiguous
+slices: [classifier + pooler + layer 11 ...], ..., [layer 0 ...], [embeddings +
+image projection + ResNet].  Each fused BERT layer's backward reports when its
+weight gradients are enqueued; as soon as a bucket's layers are all done its
+all-reduce (torch.distributed backend "nccl" = RCCL) is issued.  The collective
+runs on RCCL's own stream, ordered after the producing kernels by an event, so it
+overlaps the backward of the layers below.  ``finish()`` issues what is left and
+makes the compute stream wait before the optimizer step.  Mean = sum / world size
+(the per-rank loss is a per-rank mean over equal per-rank batches).
+"""
+import torch
+import torch.distributed as dist
+
+
+class GradBucketer:
+    def __init__(self, model, bucket_bytes=64 << 20, group=None):
+        self.model = model
+        self.enc = model.enc
+        self.store = model.store
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.bucket_bytes = bucket_bytes
+        self._plan()
+        self.enc._grad_ready_hook = self._on_ready
+        self.pending = []
+        self.launched = set()
+        self.enabled = True
+
+    def _plan(self):
+        st = self.store
+        n_layers = len(self.enc._lw)
+        # flat order: clf, pooler, layer n-1 ... layer 0, embeddings, img proj, resnet (reverse)
+        layer_spans = []
+        for i in reversed(range(n_layers)):
+            names = [n for n in st.names if n.startswith(f"{self.enc._prefix}encoder.layer.{i}.")]
+            o0 = min(st.offsets[n] for n in names)
+            o1 = max(st.offsets[n] + st.params[n].numel() for n in names)
+            layer_spans.append((i, o0, o1))
+        head_end = layer_spans[0][1]
+        buckets, cur = [], None
+        for i, o0, o1 in layer_spans:
+            if cur is None:
+                cur = {"start": 0 if i == n_layers - 1 else o0, "end": o1, "layers": {i}}
+            else:
+                cur["end"] = o1
+                cur["layers"].add(i)
+            if 4 * (cur["end"] - cur["start"]) >= self.bucket_bytes:
+                buckets.append(cur)
+                cur = None
+        if cur is not None:
+            buckets.append(cur)
+        assert head_end == 0 or buckets[0]["start"] == 0
+        tail_start = buckets[-1]["end"]
+        total = st.numel()
+        step = max(self.bucket_bytes // 4, 1)
+        for s in range(tail_start, total, step):  # embeddings + projection + ResNet: issued at finish()
+            buckets.append({"start": s, "end": min(total, s + step), "layers": set()})
+        self.buckets = buckets
+        self.layer_to_bucket = {i: b for b, bk in enumerate(buckets) for i in bk["layers"]}
+        self.done_layers = set()
+
+    def _issue(self, b):
+        if b in self.launched:
+            return
+        bk = self.buckets[b]
+        view = self.store.grad[bk["start"]:bk["end"]]
+        work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self.pending.append(work)
+        self.launched.add(b)
+
+    def _on_ready(self, lw):
+        if not self.enabled or self.world == 1 or not hasattr(lw, "module"):
+            return
+        i = self.enc._lw.index(lw)
+        self.done_layers.add(i)
+        b = self.layer_to_bucket[i]
+        if self.buckets[b]["layers"] <= self.done_layers:
+            self._issue(b)
+
+    def finish(self):
+        """Issue the remaining buckets, wait for all, average."""
+        if self.world == 1:
+            return
+        for b in range(len(self.buckets)):
+            self._issue(b)
+        for w in self.pending:
+            w.wait()
+        self.store.grad.mul_(1.0 / self.world)
+        self.pending, self.launched, self.done_layers = [], set(), set()
+
+
+def broadcast_parameters(model, src=0, group=None):
+    """Start every rank from rank 0's weights (flat buffer + BN running stats)."""
+    dist.broadcast(model.store.flat, src, group=group)
+    for b in model.buffers():
+        dist.broadcast(b, src, group=group)
+    model.store.sync_compute()

@@ -1,0 +1,158 @@
+"""Fused BERT layer on the HIP kernels: forward / backward kernel sequences and the
+autograd Function the encoder stacks (replaces pytorch_pretrained_bert BertLayer,
+called through ``self.encoder(...)`` at src/mmbt.py:124-126).
+
+Forward per layer (M = B*L token rows, bf16 activations, f32 accumulation):
+  qkv = X Wqkv^T + bqkv                       mmu_gemm  (fused Q|K|V, [M, 2304])
+  O, lse = attention(qkv, keymask)            mmu_attention_fwd (dropout on P)
+  S1 = X + dropout(O Wo^T + bo)               mmu_gemm  EPI_BIAS_DROP_RES
+  A  = LN1(S1)                                mmu_layernorm_fwd
+  H  = gelu(Z), Z = A W1^T + b1               mmu_gemm  EPI_BIAS_GELU (Z kept)
+  S2 = A + dropout(H W2^T + b2)               mmu_gemm  EPI_BIAS_DROP_RES
+  Y  = LN2(S2)                                mmu_layernorm_fwd
+Backward mirrors it; weight gradients are written straight into the flat f32
+gradient buffer (src/params.py) and skipped when the layer is frozen
+(src/framework.py:284-285 toggles requires_grad).
+"""
+import torch
+
+from . import kernels as K
+
+HID, FFN, HEADS = 768, 3072, 12
+bf16 = torch.bfloat16
+
+
+class LayerWeights:
+    """Views of one BertLayer's parameters in the ParamStore (f32 masters, bf16 copies, f32 grads)."""
+
+    def __init__(self, store, prefix, layer_module):
+        self.store, self.prefix, self.module = store, prefix, layer_module
+        q = [f"{prefix}attention.self.{n}.weight" for n in ("query", "key", "value")]
+        qb = [f"{prefix}attention.self.{n}.bias" for n in ("query", "key", "value")]
+        self._names = dict(
+            wqkv=q, bqkv=qb,
+            wo=[f"{prefix}attention.output.dense.weight"], bo=[f"{prefix}attention.output.dense.bias"],
+            ln1w=[f"{prefix}attention.output.LayerNorm.weight"], ln1b=[f"{prefix}attention.output.LayerNorm.bias"],
+            w1=[f"{prefix}intermediate.dense.weight"], b1=[f"{prefix}intermediate.dense.bias"],
+            w2=[f"{prefix}output.dense.weight"], b2=[f"{prefix}output.dense.bias"],
+            ln2w=[f"{prefix}output.LayerNorm.weight"], ln2b=[f"{prefix}output.LayerNorm.bias"])
+        self._shapes = dict(wqkv=(3 * HID, HID), bqkv=(3 * HID,), wo=(HID, HID), bo=(HID,), ln1w=(HID,), ln1b=(HID,),
+                            w1=(FFN, HID), b1=(FFN,), w2=(HID, FFN), b2=(HID,), ln2w=(HID,), ln2b=(HID,))
+        self.refresh()
+
+    def refresh(self):
+        s = self.store
+        for k, names in self._names.items():
+            setattr(self, k, s.fused(names, self._shapes[k]))
+            setattr(self, "g_" + k, s.fused_grad(names, self._shapes[k]))
+        for k in ("wqkv", "wo", "w1", "w2"):
+            setattr(self, k + "16", s.fused_compute(self._names[k], self._shapes[k]))
+        self.anchor = s.params[self._names["wqkv"][0]]
+
+    def trainable(self):
+        return self.anchor.requires_grad
+
+
+def layer_forward(lw, X, keymask, B, L, p_attn, p_hid, seeds, save):
+    M = B * L
+    dev = X.device
+    qkv = torch.empty(M, 3 * HID, dtype=bf16, device=dev)
+    K.gemm(X, HID, True, lw.wqkv16, HID, True, qkv, 3 * HID, M, 3 * HID, HID, epi=K.epilogue(K.EPI_STORE, bias=lw.bqkv))
+    O = torch.empty(M, HID, dtype=bf16, device=dev)
+    lse = torch.empty(B * HEADS, L, dtype=torch.float32, device=dev)
+    K.attention_fwd(qkv, keymask, O, lse, B, L, HEADS, p_attn, seeds[0])
+    S1 = torch.empty(M, HID, dtype=bf16, device=dev)
+    K.gemm(O, HID, True, lw.wo16, HID, True, S1, HID, M, HID, HID,
+           epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw.bo, residual=X, drop_p=p_hid, seed=seeds[1]))
+    A = torch.empty(M, HID, dtype=bf16, device=dev)
+    mean1 = torch.empty(M, dtype=torch.float32, device=dev)
+    rstd1 = torch.empty(M, dtype=torch.float32, device=dev)
+    K.layernorm_fwd(S1, lw.ln1w, lw.ln1b, A, mean1, rstd1)
+    Z = torch.empty(M, FFN, dtype=bf16, device=dev)
+    Hh = torch.empty(M, FFN, dtype=bf16, device=dev)
+    K.gemm(A, HID, True, lw.w116, HID, True, Hh, FFN, M, FFN, HID, epi=K.epilogue(K.EPI_BIAS_GELU, bias=lw.b1, aux=Z))
+    S2 = torch.empty(M, HID, dtype=bf16, device=dev)
+    K.gemm(Hh, FFN, True, lw.w216, FFN, True, S2, HID, M, HID, FFN,
+           epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw.b2, residual=A, drop_p=p_hid, seed=seeds[2]))
+    Y = torch.empty(M, HID, dtype=bf16, device=dev)
+    mean2 = torch.empty(M, dtype=torch.float32, device=dev)
+    rstd2 = torch.empty(M, dtype=torch.float32, device=dev)
+    K.layernorm_fwd(S2, lw.ln2w, lw.ln2b, Y, mean2, rstd2)
+    saved = (X, qkv, O, lse, S1, mean1, rstd1, A, Z, Hh, S2, mean2, rstd2) if save else None
+    return Y, saved
+
+
+def _reduce(part, out):
+    K.colsum_reduce(part, out, accumulate=True)
+
+
+def layer_backward(lw, saved, dY, keymask, B, L, p_attn, p_hid, seeds, wgrad):
+    X, qkv, O, lse, S1, mean1, rstd1, A, Z, Hh, S2, mean2, rstd2 = saved
+    M = B * L
+    dev = dY.device
+    P = K.ln_parts(M)
+    pw = pb = pbias = None
+    if wgrad:
+        pw, pb, pbias = (torch.empty(P, HID, dtype=torch.float32, device=dev) for _ in range(3))
+    acc = K.epilogue(K.EPI_STORE, accumulate=True)
+    # ---- output LayerNorm + dropout + W2
+    dS2 = torch.empty(M, HID, dtype=bf16, device=dev)
+    dY2 = torch.empty(M, HID, dtype=bf16, device=dev)
+    K.layernorm_bwd(dY, S2, mean2, rstd2, lw.ln2w, dS2, dY2, p_hid, seeds[2], pw, pb, pbias)
+    if wgrad:
+        _reduce(pw, lw.g_ln2w)
+        _reduce(pb, lw.g_ln2b)
+        _reduce(pbias, lw.g_b2)
+        K.gemm(dY2, HID, False, Hh, FFN, False, lw.g_w2, FFN, HID, FFN, M, epi=acc)
+    dZ = torch.empty(M, FFN, dtype=bf16, device=dev)
+    part1 = torch.empty(K.colsum_partial_rows(M), FFN, dtype=torch.float32, device=dev) if wgrad else None
+    K.gemm(dY2, HID, True, lw.w216, FFN, False, dZ, FFN, M, FFN, HID, epi=K.epilogue(K.EPI_DGELU, aux=Z, colsum=part1))
+    if wgrad:
+        _reduce(part1, lw.g_b1)
+        K.gemm(dZ, FFN, False, A, HID, False, lw.g_w1, HID, FFN, HID, M, epi=acc)
+    dA = torch.empty(M, HID, dtype=bf16, device=dev)
+    K.gemm(dZ, FFN, True, lw.w116, HID, False, dA, HID, M, HID, FFN, epi=K.epilogue(K.EPI_ADD_RES, residual=dS2))
+    # ---- attention-output LayerNorm + dropout + Wo
+    dS1 = torch.empty(M, HID, dtype=bf16, device=dev)
+    dAo = torch.empty(M, HID, dtype=bf16, device=dev)
+    K.layernorm_bwd(dA, S1, mean1, rstd1, lw.ln1w, dS1, dAo, p_hid, seeds[1], pw, pb, pbias)
+    if wgrad:
+        _reduce(pw, lw.g_ln1w)
+        _reduce(pb, lw.g_ln1b)
+        _reduce(pbias, lw.g_bo)
+        K.gemm(dAo, HID, False, O, HID, False, lw.g_wo, HID, HID, HID, M, epi=acc)
+    dO = torch.empty(M, HID, dtype=bf16, device=dev)
+    K.gemm(dAo, HID, True, lw.wo16, HID, False, dO, HID, M, HID, HID)
+    # ---- attention + fused QKV
+    dqkv = torch.empty(M, 3 * HID, dtype=bf16, device=dev)
+    delta = torch.empty(B * HEADS, L, dtype=torch.float32, device=dev)
+    K.attention_bwd(qkv, keymask, O, dO, lse, delta, dqkv, B, L, HEADS, p_attn, seeds[0])
+    if wgrad:
+        K.colsum_bf16(dqkv, lw.g_bqkv, accumulate=True)
+        K.gemm(dqkv, 3 * HID, False, X, HID, False, lw.g_wqkv, HID, 3 * HID, HID, M, epi=acc)
+    dX = torch.empty(M, HID, dtype=bf16, device=dev)
+    K.gemm(dqkv, 3 * HID, True, lw.wqkv16, HID, False, dX, HID, M, HID, 3 * HID,
+           epi=K.epilogue(K.EPI_ADD_RES, residual=dS1))
+    return dX
+
+
+class BertLayerFunction(torch.autograd.Function):
+    """One fused BertLayer; X [B*L, 768] bf16 -> Y.  ``anchor`` (the layer's query
+    weight) only makes autograd run backward when the layer is trainable."""
+
+    @staticmethod
+    def forward(ctx, X, anchor, lw, keymask, B, L, p_attn, p_hid, seeds, on_grads_ready):
+        Y, saved = layer_forward(lw, X, keymask, B, L, p_attn, p_hid, seeds, save=True)
+        ctx.saved_bufs = saved
+        ctx.meta = (lw, keymask, B, L, p_attn, p_hid, seeds, on_grads_ready)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        lw, keymask, B, L, p_attn, p_hid, seeds, hook = ctx.meta
+        wgrad = lw.trainable()
+        dX = layer_backward(lw, ctx.saved_bufs, dY.contiguous(), keymask, B, L, p_attn, p_hid, seeds, wgrad)
+        ctx.saved_bufs = None
+        if wgrad and hook is not None:
+            hook(lw)
+        return dX, None, None, None, None, None, None, None, None, None

@@ -91,11 +91,11 @@ def attention_bwd(qkv, keymask, O, dO, lse, delta, dqkv, batch, L, heads=12, dro
            _stream(qkv))
 
 
-def layernorm_fwd(X, w, b, Y, mean, rstd, eps=1e-12):
+def layernorm_fwd(X, w, b, Y, mean, rstd, eps=1e-12, group_rows=0, param_stride=0):
     _dev_check(X, w, b, Y, mean, rstd)
     rows, H = X.shape
     N.call("mmu_layernorm_fwd", _ptr(X), _ptr(w), _ptr(b), _ptr(Y), _ptr(mean), _ptr(rstd), rows, H, float(eps),
-           _stream(X))
+           int(group_rows), int(param_stride), _stream(X))
 
 
 LN_ROWS_PER_PART = 64

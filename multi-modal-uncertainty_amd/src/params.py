@@ -1,0 +1,158 @@
+"""Flat parameter / gradient / bf16-compute storage for the MMBT module tree.
+
+Every trainable tensor of the model is a view into ONE f32 master buffer and its
+``.grad`` a view into ONE f32 gradient buffer, laid out in the order backward
+finishes them (classifier, pooler, encoder layers 11..0, embeddings, ResNet
+layer4..stem).  This gives:
+  * the fused BertAdam one launch over all 169 M parameters (src/optim.py);
+  * contiguous reverse-layer gradient buckets for the RCCL all-reduce (src/dp.py);
+  * fused views (Q|K|V weight [2304,768], bias [2304]) the kernels read directly;
+  * bf16 copies of every GEMM weight, written by the optimizer kernel, resynced
+    only when the f32 masters were changed elsewhere (load_state_dict, .to()).
+Module names / shapes are untouched, so state_dict keys stay the reference's.
+"""
+import weakref
+
+import torch
+
+STORES = weakref.WeakSet()  # live stores, looked up by the fused optimizer
+
+
+class ParamStore:
+    def __init__(self, entries, compute_names):
+        """entries: [(name, Parameter)] in flat order (unique params);
+        compute_names: names (subset) that get a bf16 GEMM copy, in bf16 flat order."""
+        self.names = [n for n, _ in entries]
+        self.params = dict(entries)
+        self.compute_names = list(compute_names)
+        self.flat = self.grad = self.compute = None
+        self.offsets, self.coffsets = {}, {}
+        self._versions = None
+        self.build()
+        STORES.add(self)
+
+    # ------------------------------------------------------------------ layout
+    @staticmethod
+    def _shaped(buf, off, p):
+        """view of buf[off:off+numel] with p's shape; 4-D conv weights are laid out channels-last
+        (O, kh, kw, I) so MIOpen sees NHWC activations AND NHWC filters."""
+        k = p.numel()
+        if p.dim() == 4:
+            O, I, kh, kw = p.shape
+            return buf[off:off + k].view(O, kh, kw, I).permute(0, 3, 1, 2)
+        return buf[off:off + k].view(p.shape)
+
+    def build(self):
+        ps = [self.params[n] for n in self.names]
+        device = ps[0].device
+        total = sum(p.numel() for p in ps)
+        flat = torch.empty(total, dtype=torch.float32, device=device)
+        grad = torch.zeros(total, dtype=torch.float32, device=device)
+        off = 0
+        for n, p in zip(self.names, ps):
+            k = p.numel()
+            if p.device != device:
+                raise RuntimeError(f"ParamStore: {n} on {p.device}, expected {device}")
+            pv, gv = self._shaped(flat, off, p), self._shaped(grad, off, p)
+            pv.copy_(p.detach())
+            if p.grad is not None:
+                gv.copy_(p.grad.detach())
+            p.data = pv
+            p.grad = gv
+            self.offsets[n] = off
+            off += k
+        self.flat, self.grad = flat, grad
+        ctot = sum(self.params[n].numel() for n in self.compute_names)
+        self.compute = torch.empty(ctot, dtype=torch.bfloat16, device=device)
+        off = 0
+        for n in self.compute_names:
+            self.coffsets[n] = off
+            off += self.params[n].numel()
+        self.sync_compute()
+
+    @property
+    def device(self):
+        return self.flat.device
+
+    def numel(self):
+        return self.flat.numel()
+
+    def span(self, names):
+        """(offset, numel) of a run of consecutive names in the flat buffer"""
+        o0 = self.offsets[names[0]]
+        tot = 0
+        for n in names:
+            if self.offsets[n] != o0 + tot:
+                raise RuntimeError(f"ParamStore: {names} are not contiguous")
+            tot += self.params[n].numel()
+        return o0, tot
+
+    def fused(self, names, shape):
+        o, k = self.span(names)
+        return self.flat[o:o + k].view(shape)
+
+    def fused_grad(self, names, shape):
+        o, k = self.span(names)
+        return self.grad[o:o + k].view(shape)
+
+    def fused_compute(self, names, shape):
+        c0 = self.coffsets[names[0]]
+        tot = 0
+        for n in names:
+            if self.coffsets[n] != c0 + tot:
+                raise RuntimeError(f"ParamStore: compute copies of {names} are not contiguous")
+            tot += self.params[n].numel()
+        return self.compute[c0:c0 + tot].view(shape)
+
+    def grad_of(self, name):
+        return self._shaped(self.grad, self.offsets[name], self.params[name])
+
+    # ------------------------------------------------------------------ grads
+    def ensure_grads(self, quick=False):
+        """Re-attach grad views if a caller dropped them (e.g. Module.zero_grad(set_to_none=True)).
+        quick: only look at the first / last tensor (what set_to_none touches: all of them)."""
+        base = self.grad.data_ptr()
+        names = self.names
+        if quick:
+            ends = [names[0], names[-1]]
+            if all(self.params[n].grad is not None and
+                   self.params[n].grad.data_ptr() == base + 4 * self.offsets[n] for n in ends):
+                return
+        for n in names:
+            p = self.params[n]
+            o = self.offsets[n]
+            view = self._shaped(self.grad, o, p)
+            g = p.grad
+            if g is None:
+                view.zero_()
+                p.grad = view
+            elif g.data_ptr() != base + 4 * o:
+                view.copy_(g)
+                p.grad = view
+
+    def zero_grad(self):
+        self.ensure_grads()
+        self.grad.zero_()
+
+    # ------------------------------------------------------------------ bf16 copies
+    def _current_versions(self):
+        return tuple(self.params[n]._version for n in self.compute_names)
+
+    def sync_compute(self):
+        with torch.no_grad():
+            for n in self.compute_names:
+                c = self.coffsets[n]
+                p = self.params[n]
+                self.compute[c:c + p.numel()].copy_(p.detach().reshape(-1))
+        self._versions = self._current_versions()
+
+    def maybe_sync_compute(self):
+        """bf16 copies follow the masters; only an out-of-band write (version bump) needs a resync."""
+        if self._current_versions() != self._versions:
+            self.sync_compute()
+
+    def check_views(self):
+        """True if every parameter still aliases the flat buffer (Module._apply breaks this)."""
+        base = self.flat.data_ptr()
+        return all(self.params[n].data_ptr() == base + 4 * self.offsets[n] and self.params[n].device == self.device
+                   for n in self.names)

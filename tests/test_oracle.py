@@ -1,0 +1,79 @@
+"""CPU: the oracle restatement is pinned against the reference's own outputs (tests/golden)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _inputs(g, cfg):
+    from oracle.gen_golden import make_inputs
+    T = g["text"].shape[1]
+    lens = g["mask"].sum(1).tolist()
+    x, y = make_inputs(cfg, 2, T, lens, int(g["seed"]))
+    assert np.array_equal(x[0].numpy(), g["text"]) and np.array_equal(y.numpy(), g["y"])
+    assert abs(float(x[3].double().sum()) - float(g["img_sum"])) < 1e-6 * abs(float(g["img_sum"])) + 1e-6
+    return x, y
+
+
+@pytest.mark.parametrize("tag", ["small_t16", "full_t508"])
+def test_oracle_matches_reference_golden(tag):
+    from oracle import mmbt_ref as R
+    from oracle.weights import SMALL, FULL, make_state_dict, checksum, key_shapes
+    cfg = SMALL if tag.startswith("small") else FULL
+    g = np.load(os.path.join(GOLD, f"mmbt_{tag}.npz"))
+    keys = json.load(open(os.path.join(GOLD, f"mmbt_{tag}_keys.json")))["state_dict_keys"]
+    assert keys == [k for k, *_ in key_shapes(cfg)]
+    sd = make_state_dict(int(g["wseed"]), cfg)
+    assert abs(checksum(sd) - float(g["weight_checksum"])) <= 1e-9 * float(g["weight_checksum"])
+    x, y = _inputs(g, cfg)
+    txt, seg, mask, img = x
+    with torch.no_grad():
+        feats = R.image_encoder(sd, img, cfg)
+        np.testing.assert_allclose(feats.numpy(), g["feats"], rtol=1e-4, atol=1e-4)
+        # model(*x) passes (text, segment, mask, img) into forward(txt, mask, segment, img)
+        for v in ("full", "img_only", "txt_only"):
+            lo = R.forward(sd, txt, seg, mask, img, cfg, v, feats=feats)
+            np.testing.assert_allclose(lo.numpy(), g[f"logits_{v}"], rtol=1e-4, atol=1e-5)
+        for modal in ("image", "text"):
+            lo = R.forward(sd, txt, seg, mask, img, cfg, "control", indices=g[f"indices_control_{modal}"], feats=feats)
+            np.testing.assert_allclose(lo.numpy(), g[f"logits_control_{modal}"], rtol=1e-4, atol=1e-5)
+        lo, pooled = R.forward(sd, txt, seg, mask, img, cfg, "full", feats=feats, return_pooled=True)
+        np.testing.assert_allclose(pooled.numpy(), g["pooled_full"], rtol=1e-4, atol=1e-5)
+        assert abs(float(R.cross_entropy(lo, y)) - float(g["loss_eval"])) < 1e-5
+
+
+def test_oracle_control_indices_follow_reference_rng():
+    from oracle import mmbt_ref as R
+    g = np.load(os.path.join(GOLD, "mmbt_small_t16.npz"))
+    T = g["text"].shape[1]
+    torch.manual_seed(77)
+    assert np.array_equal(R.control_indices(T + 5, 4).numpy(), g["indices_control_image"])
+    torch.manual_seed(78)
+    assert np.array_equal(R.control_indices(T + 5, T).numpy(), g["indices_control_text"])
+
+
+def test_warmup_linear_schedule():
+    from oracle.bertadam_ref import schedule_factor
+    assert schedule_factor(0, 0.1, 100) == 0.0      # first step has lr 0 (step read before increment)
+    assert abs(schedule_factor(5, 0.1, 100) - 0.5) < 1e-12
+    assert abs(schedule_factor(10, 0.1, 100) - 1.0) < 1e-12
+    assert abs(schedule_factor(55, 0.1, 100) - 0.5) < 1e-12
+    assert schedule_factor(150, 0.1, 100) == 0.0
+    assert schedule_factor(7, 0.1, -1) == 1.0
+
+
+def test_uncertainty_reference_definitions():
+    from oracle import uncertainty_ref as U
+    logits = np.array([[[2.0, 0.0, 0.0]], [[0.0, 0.0, 5.0]]])  # S=2, R=1
+    p = U.probs_mean(logits.transpose(1, 0, 2), member_axes=(0,))
+    y = np.array([0, 1])
+    # NLL at K=T=1 is the reference CrossEntropyLoss (src/mmbt.py:243)
+    ce = torch.nn.functional.cross_entropy(torch.tensor(logits[:, 0]), torch.tensor(y)).item()
+    assert abs(U.nll(p, y) - ce) < 1e-12
+    conf = p.max(1)
+    acc = (p.argmax(1) == y).astype(float)
+    assert abs(U.ece(p, y, 15) - np.mean(np.abs(conf - acc))) < 1e-12  # one sample per bin here
