@@ -63,7 +63,11 @@ typedef struct mmu_epilogue {
   float* colsum;            /* f32 partial column sums of the final C, [2*ceil(M/128), N] per batch */
   int64_t colsum_bstride;
   float drop_p;             /* BIAS_DROP_RES                                            */
-  uint64_t seed;            /* dropout stream: element (m, n) uses counter m*N+n        */
+  uint64_t seed;            /* dropout stream: element (z, m, n) uses counter (z*M+m)*N+n */
+  float* workspace;         /* optional f32 scratch: lets a STORE/f32/no-bias product split K
+                               over workgroups (weight gradients); slabs summed in slice
+                               order, so results stay deterministic                     */
+  int64_t workspace_floats;
 } mmu_epilogue;
 
 int mmu_gemm(const void* A, int64_t lda, int a_kmajor,

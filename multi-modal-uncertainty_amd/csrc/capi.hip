@@ -115,6 +115,24 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
     return fail("mmu_gemm: epilogue needs residual");
   if (p.accumulate && c_dtype != MMU_F32) return fail("mmu_gemm: accumulate needs f32 C");
   if (p.drop_p < 0.f || p.drop_p >= 1.f) return fail("mmu_gemm: drop_p out of range");
+  // split-K for long-K / few-tile products (the weight gradients: K = tokens, M x N = a weight matrix)
+  p.splitk = 1;
+  p.kchunk = K;
+  if (kind == MMU_EPI_STORE && c_dtype == MMU_F32 && !p.bias && !p.colsum && epi && epi->workspace && K >= 4096) {
+    const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n * batch;
+    int64_t want = (640 + tiles - 1) / tiles;
+    if (want > K / 1024) want = K / 1024;
+    if (want > 32) want = 32;
+    const int64_t cap = epi->workspace_floats / (batch * M * N);
+    if (want > cap) want = cap;
+    if (want >= 2) {
+      int64_t chunk = (K + want - 1) / want;
+      chunk = (chunk + 63) / 64 * 64;
+      p.kchunk = chunk;
+      p.splitk = (int)((K + chunk - 1) / chunk);
+      p.ws = epi->workspace;
+    }
+  }
   hipStream_t s = (hipStream_t)stream;
   bool timed;
   std::pair<hipEvent_t, hipEvent_t> ev;
@@ -127,6 +145,7 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
     (void)hipEventRecord(ev.first, s);
   }
   gemm_launch(p, a_kmajor != 0, b_kmajor != 0, c_dtype == MMU_F32, (int)batch, s);
+  if (p.splitk > 1) splitk_reduce_launch(p, (int)batch, s);
   if (timed) {
     (void)hipEventRecord(ev.second, s);
     std::lock_guard<std::mutex> lk(g_t.mu);

@@ -94,9 +94,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   uint4 ra[4], rb[4];
-  const int nk = (int)((p.K + BKT - 1) / BKT);
-  g_load<AK>(ra, A, p.lda, m0, p.M, 0, p.K, t);
-  g_load<BKM>(rb, B, p.ldb, n0, p.N, 0, p.K, t);
+  // split-K: slice blockIdx.y owns k in [kb, ke); kchunk is a multiple of the K tile
+  const int64_t kb = (int64_t)blockIdx.y * p.kchunk;
+  const int64_t ke = kb + p.kchunk < p.K ? kb + p.kchunk : p.K;
+  const int nk = (int)((ke - kb + BKT - 1) / BKT);
+  g_load<AK>(ra, A, p.lda, m0, p.M, kb, ke, t);
+  g_load<BKM>(rb, B, p.ldb, n0, p.N, kb, ke, t);
   s_store<AK>(smem, ra, t);
   s_store<BKM>(smem + BM * BKT * 2, rb, t);
   __syncthreads();
@@ -106,8 +109,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
     const char* sb = sa + BM * BKT * 2;
     const bool more = kt + 1 < nk;
     if (more) {
-      g_load<AK>(ra, A, p.lda, m0, p.M, (int64_t)(kt + 1) * BKT, p.K, t);
-      g_load<BKM>(rb, B, p.ldb, n0, p.N, (int64_t)(kt + 1) * BKT, p.K, t);
+      g_load<AK>(ra, A, p.lda, m0, p.M, kb + (int64_t)(kt + 1) * BKT, ke, t);
+      g_load<BKM>(rb, B, p.ldb, n0, p.N, kb + (int64_t)(kt + 1) * BKT, ke, t);
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -131,6 +134,19 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
   }
 
   // ------------------------------------------------------------------ epilogue
+  if (p.splitk > 1) {  // raw partial product -> this slice's f32 slab; summed by splitk_reduce_kernel
+    float* slab = p.ws + (z * p.splitk + blockIdx.y) * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t n = n0 + 64 * wn + 16 * i + 4 * (l >> 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t m = m0 + 64 * wm + 16 * j + (l & 15);
+        if (m < p.M) *(float4*)(slab + m * p.N + n) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+    }
+    return;
+  }
   const float* bias = p.bias ? p.bias + z * p.bias_bstride : nullptr;
   const bf16* res = p.residual ? (const bf16*)p.residual + z * p.res_bstride : nullptr;
   bf16* aux = p.aux ? (bf16*)p.aux + z * p.aux_bstride : nullptr;
@@ -159,7 +175,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
         for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
       } else if (EPI == MMU_EPI_BIAS_DROP_RES) {
         if (p.drop_p > 0.f) {
-          uint32_t keep = mmu_keep4(p.seed, (uint64_t)(m * p.N + n) >> 2, thr);
+          // counter over the whole batched output: batch item z, row m, column n
+          uint32_t keep = mmu_keep4(p.seed, (uint64_t)((z * p.M + m) * p.N + n) >> 2, thr);
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = ((keep >> r) & 1) ? v[r] * scale : 0.f;
         }
@@ -213,8 +230,36 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
 
 template <bool AK, bool BKM, int EPI, bool F32>
 static void launch_t(const GemmParams& p, int batch, hipStream_t s) {
-  dim3 grid(p.tiles_m * p.tiles_n, 1, batch);
+  dim3 grid(p.tiles_m * p.tiles_n, p.splitk, batch);
   hipLaunchKernelGGL((gemm_kernel<AK, BKM, EPI, F32>), grid, dim3(256), 0, s, p);
+}
+
+// C[z] (+)= sum over the split-K slabs of batch item z (fixed slice order: deterministic)
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ C,
+                                                            int64_t M, int64_t N, int64_t ldc, int64_t sC,
+                                                            int splitk, int accumulate) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;  // float4 index within one batch item
+  const int64_t z = blockIdx.y;
+  if (q * 4 >= M * N) return;
+  const int64_t e = q * 4, m = e / N, n = e - m * N;
+  const float* s = ws + z * splitk * M * N + e;
+  float4 a = *(const float4*)s;
+  for (int k = 1; k < splitk; ++k) {
+    const float4 b = *(const float4*)(s + k * M * N);
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  float* c = C + z * sC + m * ldc + n;
+  if (accumulate) {
+    const float4 o = *(const float4*)c;
+    a.x += o.x; a.y += o.y; a.z += o.z; a.w += o.w;
+  }
+  *(float4*)c = a;
+}
+
+void splitk_reduce_launch(const GemmParams& p, int batch, hipStream_t s) {
+  const int64_t q = (p.M * p.N) / 4;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((q + 255) / 256), batch), dim3(256), 0, s, p.ws,
+                     (float*)p.C, p.M, p.N, p.ldc, p.sC, p.splitk, p.accumulate);
 }
 
 template <int EPI, bool F32>
@@ -239,18 +284,25 @@ void gemm_launch(const GemmParams& p, bool ak, bool bk, bool f32out, int batch, 
 }
 
 // ------------------------------------------------------------------ column sums
-__global__ void colsum_reduce_kernel(const float* __restrict__ part, int64_t parts, int64_t N,
-                                     float* __restrict__ out, int accumulate) {
-  int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// grid (ceil(N/256), ceil(parts/64)): each thread sums 64 partial rows of one column and adds
+// the result into out with one float atomic (out zeroed first when not accumulating)
+constexpr int COLSUM_ROWS = 64;
+__global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restrict__ part, int64_t parts, int64_t N,
+                                                            float* __restrict__ out) {
+  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (n >= N) return;
+  const int64_t r0 = (int64_t)blockIdx.y * COLSUM_ROWS;
+  const int64_t r1 = r0 + COLSUM_ROWS < parts ? r0 + COLSUM_ROWS : parts;
   float s = 0.f;
-  for (int64_t r = 0; r < parts; ++r) s += part[r * N + n];
-  out[n] = accumulate ? out[n] + s : s;
+  for (int64_t r = r0; r < r1; ++r) s += part[r * N + n];
+  atomicAdd(out + n, s);
 }
 
 void colsum_reduce_launch(const float* part, int64_t parts, int64_t N, float* out, int acc, hipStream_t s) {
-  hipLaunchKernelGGL(colsum_reduce_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s,
-                     part, parts, N, out, acc);
+  if (!acc) (void)hipMemsetAsync(out, 0, sizeof(float) * N, s);
+  hipLaunchKernelGGL(colsum_reduce_kernel,
+                     dim3((unsigned)((N + 255) / 256), (unsigned)((parts + COLSUM_ROWS - 1) / COLSUM_ROWS)),
+                     dim3(256), 0, s, part, parts, N, out);
 }
 
 // bf16 [M,N] -> partial[ceil(M/256), N]: each block sums 256 rows for 512 columns (8 per lane-column pass)

@@ -26,8 +26,13 @@ struct GemmParams {
   int64_t colsum_bstride;
   float drop_p;
   uint64_t seed;
+  // split-K (EPI_STORE, f32 C, no bias/colsum): grid.y slices of kchunk, slabs in ws
+  int splitk;
+  int64_t kchunk;
+  float* ws;
 };
 
+void splitk_reduce_launch(const GemmParams& p, int batch, hipStream_t s);
 void gemm_launch(const GemmParams& p, bool a_kmajor, bool b_kmajor, bool f32out, int batch, hipStream_t s);
 void colsum_reduce_launch(const float* part, int64_t parts, int64_t N, float* out, int acc, hipStream_t s);
 void colsum_bf16_launch(const bf16* X, int64_t M, int64_t N, int64_t ld, float* part, float* out, int acc,

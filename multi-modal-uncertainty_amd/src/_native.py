@@ -21,7 +21,7 @@ class Epilogue(ctypes.Structure):
     _fields_ = [("kind", c_i32), ("accumulate", c_i32), ("bias", c_vp), ("bias_bstride", c_i64),
                 ("residual", c_vp), ("ldr", c_i64), ("res_bstride", c_i64), ("aux", c_vp), ("ldx", c_i64),
                 ("aux_bstride", c_i64), ("colsum", c_vp), ("colsum_bstride", c_i64), ("drop_p", c_f32),
-                ("seed", c_u64)]
+                ("seed", c_u64), ("workspace", c_vp), ("workspace_floats", c_i64)]
 
 
 # name -> (restype, argtypes); every entry must be exported by the library (tested on CPU)
@@ -68,6 +68,9 @@ def load():
         if not os.path.exists(LIB_PATH):
             raise NativeError(f"libmmu_hip.so not built at {LIB_PATH}: run `python -c 'import __graft_entry__ as g; "
                               f"g.build()'` (hipcc --offload-arch=gfx950)")
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()  # let torch own HIP runtime / context creation before our code object registers
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)

@@ -1,0 +1,186 @@
+"""MMBT input contract: Food-101 jsonl dataset, vocab, collate.
+
+Same public names / signatures as the reference src/dataset.py MMBT part
+(JsonlDataset :348-405, get_labels_and_frequencies :408-417, collate_fn :420-438,
+Vocab/get_vocab :440-472, get_food101 :474-545).  Differences forced by the image:
+  * torchvision is absent: Resize(256) -> CenterCrop(224) -> ToTensor -> Normalize is
+    restated on PIL + numpy (`food101_transform`);
+  * BertTokenizer.from_pretrained needs the network: the vocab is read from a local
+    file (`<DATA_DIR>/<bert_model>-vocab.txt` or $BERT_VOCAB) via transformers' BertTokenizer.
+``SyntheticFood101`` produces batches of the same contract for benchmarks and tests.
+"""
+import json
+import os
+from collections import Counter
+
+import numpy as np
+import torch
+from torch.utils.data import Dataset
+
+from .utils import numpy_seed
+
+MEAN = (0.46777044, 0.44531429, 0.40661017)
+STD = (0.12221994, 0.12145835, 0.14380469)
+
+
+def food101_transform(img, size=256, crop=224):
+    """Resize shorter side to `size` (bilinear), center-crop `crop`, to [0,1] CHW, normalise."""
+    from PIL import Image
+    w, h = img.size
+    if w <= h:
+        nw, nh = size, int(size * h / w)
+    else:
+        nw, nh = int(size * w / h), size
+    img = img.resize((nw, nh), Image.BILINEAR)
+    left, top = int(round((nw - crop) / 2.0)), int(round((nh - crop) / 2.0))
+    img = img.crop((left, top, left + crop, top + crop))
+    a = np.asarray(img, dtype=np.float32) / 255.0
+    a = (a - np.array(MEAN, dtype=np.float32)) / np.array(STD, dtype=np.float32)
+    return torch.from_numpy(a.transpose(2, 0, 1).copy())
+
+
+class Vocab(object):
+    def __init__(self, emptyInit=False):
+        if emptyInit:
+            self.stoi, self.itos, self.vocab_sz = {}, [], 0
+        else:
+            self.itos = ["[PAD]", "[UNK]", "[CLS]", "[SEP]", "[MASK]"]
+            self.stoi = {w: i for i, w in enumerate(self.itos)}
+            self.vocab_sz = len(self.itos)
+
+    def add(self, words):
+        for w in words:
+            if w not in self.stoi:
+                self.stoi[w] = len(self.itos)
+                self.itos.append(w)
+        self.vocab_sz = len(self.itos)
+
+
+def _vocab_file(bert_model):
+    cands = [os.environ.get("BERT_VOCAB", ""),
+             os.path.join(os.environ.get("DATA_DIR", ""), f"{bert_model}-vocab.txt"),
+             os.path.join(os.environ.get("DATA_DIR", ""), bert_model, "vocab.txt")]
+    for c in cands:
+        if c and os.path.exists(c):
+            return c
+    raise FileNotFoundError(f"no local vocab for {bert_model}: set $BERT_VOCAB or put {bert_model}-vocab.txt in "
+                            f"$DATA_DIR (BertTokenizer.from_pretrained needs the network)")
+
+
+def bert_tokenizer(bert_model):
+    from transformers import BertTokenizer
+    return BertTokenizer(vocab_file=_vocab_file(bert_model), do_lower_case=True)
+
+
+def get_vocab(bert_model):
+    tok = bert_tokenizer(bert_model)
+    vocab = Vocab()
+    vocab.stoi = dict(tok.vocab)
+    vocab.itos = dict(tok.ids_to_tokens)
+    vocab.vocab_sz = len(vocab.itos)
+    return vocab
+
+
+class JsonlDataset(Dataset):
+    """One Food-101 row -> (text ids, segment, image, label); text = wordpieces truncated to
+    max_seq_len - num_image_embeds - 1 after a leading [SEP] that is then dropped
+    (the first [SEP] belongs to the image tokens)."""
+
+    def __init__(self, data_path, tokenizer, transforms, vocab, n_classes, drop_img_percent, max_seq_len,
+                 num_image_embeds, labels):
+        with open(data_path) as f:
+            self.data = [json.loads(line) for line in f]
+        self.data_dir = os.path.dirname(data_path)
+        self.tokenizer, self.vocab, self.n_classes, self.labels = tokenizer, vocab, n_classes, labels
+        self.text_start_token = ["[SEP]"]
+        with numpy_seed(0):
+            for row in self.data:
+                if np.random.random() < drop_img_percent:
+                    row["img"] = None
+        self.max_seq_len = max_seq_len - num_image_embeds
+        self.transforms = transforms
+
+    def __len__(self):
+        return len(self.data)
+
+    def __getitem__(self, index):
+        row = self.data[index]
+        words = self.text_start_token + self.tokenizer(row["text"])[:(self.max_seq_len - 1)]
+        unk = self.vocab.stoi["[UNK]"]
+        ids = torch.LongTensor([self.vocab.stoi.get(w, unk) for w in words])[1:]
+        segment = torch.ones(len(ids))
+        label = torch.LongTensor([self.labels.index(row["label"])])
+        from PIL import Image
+        if row["img"]:
+            image = Image.open(os.path.join(self.data_dir, row["img"])).convert("RGB")
+        else:
+            image = Image.fromarray(128 * np.ones((256, 256, 3), dtype=np.uint8))
+        return ids, segment, self.transforms(image), label
+
+
+def get_labels_and_frequencies(path):
+    with open(path) as f:
+        labels = [json.loads(line)["label"] for line in f]
+    freqs = Counter()
+    if labels and isinstance(labels[0], list):
+        for row in labels:
+            freqs.update(row)
+    else:
+        freqs.update(labels)
+    return list(freqs.keys()), freqs
+
+
+def collate_fn(batch):
+    """Pad to the longest text in the batch -> ((text, segment, mask, img), tgt)."""
+    lens = [len(r[0]) for r in batch]
+    B, T = len(batch), max(lens)
+    text = torch.zeros(B, T, dtype=torch.long)
+    segment = torch.zeros(B, T, dtype=torch.long)
+    mask = torch.zeros(B, T, dtype=torch.long)
+    for i, (r, n) in enumerate(zip(batch, lens)):
+        text[i, :n] = r[0]
+        segment[i, :n] = r[1]
+        mask[i, :n] = 1
+    img = torch.stack([r[2] for r in batch])
+    tgt = torch.cat([r[3] for r in batch]).long()
+    return (text, segment, mask, img), tgt
+
+
+def get_food101(bert_model="bert-base-uncased", datapath=None, drop_img_percent=0.0, max_seq_len=512,
+                num_image_embeds=3, batch_size=128, n_workers=20):
+    datapath = datapath or os.environ["DATA_DIR"]
+    tokenizer = bert_tokenizer(bert_model).tokenize
+    labels, _ = get_labels_and_frequencies(os.path.join(datapath, "train.jsonl"))
+    vocab = get_vocab(bert_model)
+    n_classes = len(labels)
+
+    def make(split):
+        return JsonlDataset(os.path.join(datapath, f"{split}.jsonl"), tokenizer, food101_transform, vocab, n_classes,
+                            drop_img_percent, max_seq_len, num_image_embeds, labels)
+
+    def loader(ds, shuffle):
+        return torch.utils.data.DataLoader(ds, batch_size=batch_size, shuffle=shuffle, num_workers=n_workers,
+                                           collate_fn=collate_fn, pin_memory=torch.cuda.is_available())
+
+    return loader(make("train"), True), loader(make("dev"), False), loader(make("test"), False), n_classes, vocab
+
+
+class SyntheticFood101(Dataset):
+    """Seeded stand-in with the JsonlDataset item contract (texts of random length up to
+    max_text, image already normalised) -- no dataset is available offline."""
+
+    def __init__(self, n, max_text=508, n_classes=101, vocab_size=30522, min_text=None, seed=0):
+        self.n, self.max_text, self.n_classes, self.vocab_size = n, max_text, n_classes, vocab_size
+        self.min_text = max_text if min_text is None else min_text
+        self.seed = seed
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        g = torch.Generator().manual_seed(self.seed * 1000003 + i)
+        T = int(torch.randint(self.min_text, self.max_text + 1, (1,), generator=g))
+        ids = torch.randint(1000, self.vocab_size, (T,), generator=g)
+        img = torch.randn(3, 224, 224, generator=g)
+        y = torch.randint(0, self.n_classes, (1,), generator=g)
+        return ids, torch.ones(T), img, y

@@ -42,7 +42,19 @@ def epilogue(kind=EPI_STORE, bias=None, residual=None, aux=None, colsum=None, dr
     e.aux, e.ldx, e.aux_bstride = _ptr(aux), ldx or (aux.shape[-1] if aux is not None else 0), aux_bstride
     e.colsum, e.colsum_bstride = _ptr(colsum), colsum_bstride
     e.drop_p, e.seed = float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF
+    e.workspace, e.workspace_floats = None, 0
     return e
+
+
+SPLITK_WS_FLOATS = 16 << 20  # 64 MiB per device, reused stream-ordered by every split-K product
+_ws = {}
+
+
+def _splitk_workspace(dev):
+    t = _ws.get(dev)
+    if t is None:
+        t = _ws[dev] = torch.empty(SPLITK_WS_FLOATS, dtype=torch.float32, device=dev)
+    return t
 
 
 def gemm(A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, M, N_, K, epi=None, batch=1, sA=0, sB=0, sC=0):
@@ -53,6 +65,12 @@ def gemm(A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, M, N_, K, epi=None, batch=1
     cdt = N.MMU_F32 if C.dtype == torch.float32 else N.MMU_BF16
     if C.dtype not in (torch.float32, torch.bfloat16):
         raise N.NativeError("gemm C must be f32 or bf16")
+    if cdt == N.MMU_F32 and (epi is None or (epi.kind == EPI_STORE and not epi.bias and not epi.colsum)):
+        if epi is None:
+            epi = epilogue(EPI_STORE)
+        if not epi.workspace:
+            ws = _splitk_workspace(C.device)
+            epi.workspace, epi.workspace_floats = ws.data_ptr(), ws.numel()
     N.call("mmu_gemm", _ptr(A), lda, int(a_kmajor), _ptr(B), ldb, int(b_kmajor), _ptr(C), ldc, cdt, M, N_, K,
            batch, sA, sB, sC, ctypes.byref(epi) if epi is not None else None, _stream(C))
     return C

@@ -108,8 +108,8 @@ class BertAdam(torch.optim.Optimizer):
             s = self.state.get(p, {})
             o, k = st.offsets[n], p.numel()
             if "next_m" in s:
-                m[o:o + k].copy_(s["next_m"].reshape(-1))
-                v[o:o + k].copy_(s["next_v"].reshape(-1))
+                st._shaped(m, o, p).copy_(s["next_m"])
+                st._shaped(v, o, p).copy_(s["next_v"])
                 host_steps[i] = int(s["step"])
         steps = torch.tensor(host_steps, dtype=torch.int32).to(dev)
         self._fused = dict(store=st, names=names, m=m, v=v, steps=steps, group_of=group_of, active=None,
@@ -117,8 +117,8 @@ class BertAdam(torch.optim.Optimizer):
         for i, n in enumerate(names):
             p = st.params[n]
             o, k = st.offsets[n], p.numel()
-            self.state[p] = {"step": host_steps[i], "next_m": m[o:o + k].view(p.shape),
-                             "next_v": v[o:o + k].view(p.shape)}
+            # same element layout as the parameter view (conv weights are channels-last in the flat buffer)
+            self.state[p] = {"step": host_steps[i], "next_m": st._shaped(m, o, p), "next_v": st._shaped(v, o, p)}
         self._host_steps_valid = True
 
     def _table(self):

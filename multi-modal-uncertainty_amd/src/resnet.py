@@ -9,20 +9,35 @@ On MI355X the trunk runs through MIOpen in bf16, channels-last (ImageEncoder).
 import torch.nn as nn
 
 
+class BatchNorm2d(nn.BatchNorm2d):
+    """BatchNorm2d whose inference form is a per-channel affine (y = x * s + t with
+    s = w / sqrt(var + eps), t = b - mean * s) computed in the activation dtype.
+    Training keeps MIOpen's batch-statistics kernel.  (On this ROCm 7.2 stack MIOpen's
+    bf16 NHWC inference batch-norm crashes in host code; the affine form is also one
+    elementwise pass.)"""
+
+    def forward(self, x):
+        if self.training or not self.track_running_stats:
+            return super().forward(x)
+        s = self.weight * (self.running_var + self.eps).rsqrt()
+        t = self.bias - self.running_mean * s
+        return x * s.view(1, -1, 1, 1).to(x.dtype) + t.view(1, -1, 1, 1).to(x.dtype)
+
+
 class Bottleneck(nn.Module):
     def __init__(self, cin, width, stride):
         super().__init__()
         cout = width * 4
         self.conv1 = nn.Conv2d(cin, width, 1, bias=False)
-        self.bn1 = nn.BatchNorm2d(width)
+        self.bn1 = BatchNorm2d(width)
         self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
-        self.bn2 = nn.BatchNorm2d(width)
+        self.bn2 = BatchNorm2d(width)
         self.conv3 = nn.Conv2d(width, cout, 1, bias=False)
-        self.bn3 = nn.BatchNorm2d(cout)
+        self.bn3 = BatchNorm2d(cout)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = None
         if stride != 1 or cin != cout:
-            self.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, stride=stride, bias=False), nn.BatchNorm2d(cout))
+            self.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, stride=stride, bias=False), BatchNorm2d(cout))
 
     def forward(self, x):
         skip = x if self.downsample is None else self.downsample(x)
@@ -33,7 +48,7 @@ class Bottleneck(nn.Module):
 
 def resnet152_trunk(blocks=(3, 8, 36, 3)):
     """Sequential(conv1, bn1, relu, maxpool, layer1..layer4) -> [B,2048,H/32,W/32]."""
-    mods = [nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False), nn.BatchNorm2d(64), nn.ReLU(inplace=True),
+    mods = [nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False), BatchNorm2d(64), nn.ReLU(inplace=True),
             nn.MaxPool2d(3, 2, 1)]
     cin = 64
     for i, (width, n) in enumerate(zip((64, 128, 256, 512), blocks)):

@@ -68,6 +68,21 @@ def test_gemm_k_tail_weight_grad(dev):
     torch.testing.assert_close(C, ref, rtol=1e-4, atol=2e-3)
 
 
+@pytest.mark.parametrize("accumulate", [True, False])
+def test_gemm_splitk_weight_grad(dev, accumulate):
+    """long-K / few-tile product takes the split-K path (slabs + ordered reduce): same result, deterministic."""
+    k = K()
+    Ktok, M, N = 20000, 256, 128
+    dY, X = rnd(Ktok, M, dev=dev, seed=31), rnd(Ktok, N, dev=dev, seed=32)
+    C = torch.full((M, N), 0.5, dtype=torch.float32, device=dev)
+    k.gemm(dY, M, False, X, N, False, C, N, M, N, Ktok, epi=k.epilogue(k.EPI_STORE, accumulate=accumulate))
+    ref = dY.float().t() @ X.float() + (0.5 if accumulate else 0.0)
+    torch.testing.assert_close(C, ref, rtol=1e-4, atol=1e-2)
+    C2 = torch.full((M, N), 0.5, dtype=torch.float32, device=dev)
+    k.gemm(dY, M, False, X, N, False, C2, N, M, N, Ktok, epi=k.epilogue(k.EPI_STORE, accumulate=accumulate))
+    assert torch.equal(C, C2)
+
+
 def test_gemm_gelu_dgelu_colsum(dev):
     k = K()
     M, N, Kd = 300, 256, 128
