@@ -60,7 +60,7 @@ typedef struct mmu_epilogue {
   int64_t ldr, res_bstride;
   void* aux;                /* bf16 [M, ldx]: GELU pre-activation (written or read)     */
   int64_t ldx, aux_bstride;
-  float* colsum;            /* f32 partial column sums of the final C, [2*ceil(M/128), N] per batch */
+  float* colsum;            /* f32 [N] per batch: += column sums of the final C (bias grads) */
   int64_t colsum_bstride;
   float drop_p;             /* BIAS_DROP_RES                                            */
   uint64_t seed;            /* dropout stream: element (z, m, n) uses counter (z*M+m)*N+n */
@@ -80,8 +80,8 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor,
 /* Sum `parts` rows of a [parts, N] f32 partial table into out[N] (+= if accumulate). */
 int mmu_colsum_reduce(const float* partial, int64_t parts, int64_t N, float* out,
                       int accumulate, mmu_stream_t stream);
-/* Column sums of a bf16 [M, N] matrix into out[N] f32 (+= if accumulate), via
- * `partial` workspace of [ceil(M/256), N] f32 (bias grad of the fused QKV projection). */
+/* Column sums of a bf16 [M, N] matrix into out[N] f32 (+= if accumulate): the bias grad
+ * of the fused QKV projection.  `partial` is unused (kept for ABI stability; may be NULL). */
 int mmu_colsum_bf16(const void* X, int64_t M, int64_t N, int64_t ldx, float* partial,
                     float* out, int accumulate, mmu_stream_t stream);
 

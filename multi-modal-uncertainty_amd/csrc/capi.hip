@@ -95,8 +95,12 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
   p.A = (const bf16*)A; p.B = (const bf16*)B; p.C = C;
   p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
   p.sA = strideA; p.sB = strideB; p.sC = strideC;
-  p.tiles_m = (int)((M + 127) / 128);
-  p.tiles_n = (int)(N / 128);
+  // big (256x256, LDS-DMA) tiling needs >= 256 rows/cols and 32-bit buffer offsets per operand
+  const int64_t a_span = 2 * (a_kmajor ? M * lda : K * lda), b_span = 2 * (b_kmajor ? N * ldb : K * ldb);
+  const bool big = M >= 256 && N >= 256 && a_span < (1ll << 32) - 4096 && b_span < (1ll << 32) - 4096;
+  const int tile = big ? 256 : 128;
+  p.tiles_m = (int)((M + tile - 1) / tile);
+  p.tiles_n = (int)((N + tile - 1) / tile);
   int kind = MMU_EPI_STORE;
   if (epi) {
     kind = epi->kind;
@@ -144,7 +148,7 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
     ev = take_events();
     (void)hipEventRecord(ev.first, s);
   }
-  gemm_launch(p, a_kmajor != 0, b_kmajor != 0, c_dtype == MMU_F32, (int)batch, s);
+  gemm_launch(p, a_kmajor != 0, b_kmajor != 0, c_dtype == MMU_F32, big, (int)batch, s);
   if (p.splitk > 1) splitk_reduce_launch(p, (int)batch, s);
   if (timed) {
     (void)hipEventRecord(ev.second, s);
@@ -164,7 +168,7 @@ int mmu_colsum_reduce(const float* partial, int64_t parts, int64_t N, float* out
 
 int mmu_colsum_bf16(const void* X, int64_t M, int64_t N, int64_t ldx, float* partial, float* out, int accumulate,
                     mmu_stream_t stream) {
-  if (!X || !partial || !out || M <= 0 || N <= 0 || N % 8 || ldx % 8) return fail("mmu_colsum_bf16: bad args");
+  if (!X || !out || M <= 0 || N <= 0 || N % 8 || ldx % 8) return fail("mmu_colsum_bf16: bad args");
   colsum_bf16_launch((const bf16*)X, M, N, ldx, partial, out, accumulate, (hipStream_t)stream);
   return check_launch("mmu_colsum_bf16");
 }

@@ -105,10 +105,10 @@ def layer_backward(lw, saved, dY, keymask, B, L, p_attn, p_hid, seeds, wgrad):
         _reduce(pbias, lw.g_b2)
         K.gemm(dY2, HID, False, Hh, FFN, False, lw.g_w2, FFN, HID, FFN, M, epi=acc)
     dZ = torch.empty(M, FFN, dtype=bf16, device=dev)
-    part1 = torch.empty(K.colsum_partial_rows(M), FFN, dtype=torch.float32, device=dev) if wgrad else None
-    K.gemm(dY2, HID, True, lw.w216, FFN, False, dZ, FFN, M, FFN, HID, epi=K.epilogue(K.EPI_DGELU, aux=Z, colsum=part1))
+    # dgelu epilogue also accumulates the intermediate-bias gradient (column sums of dZ) in place
+    K.gemm(dY2, HID, True, lw.w216, FFN, False, dZ, FFN, M, FFN, HID,
+           epi=K.epilogue(K.EPI_DGELU, aux=Z, colsum=lw.g_b1 if wgrad else None))
     if wgrad:
-        _reduce(part1, lw.g_b1)
         K.gemm(dZ, FFN, False, A, HID, False, lw.g_w1, HID, FFN, HID, M, epi=acc)
     dA = torch.empty(M, HID, dtype=bf16, device=dev)
     K.gemm(dZ, FFN, True, lw.w116, HID, False, dA, HID, M, HID, FFN, epi=K.epilogue(K.EPI_ADD_RES, residual=dS2))

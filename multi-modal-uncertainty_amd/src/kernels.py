@@ -76,23 +76,16 @@ def gemm(A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, M, N_, K, epi=None, batch=1
     return C
 
 
-def colsum_partial_rows(M):
-    """rows of the partial column-sum table a GEMM epilogue writes for M output rows"""
-    return 2 * ((M + 127) // 128)
-
-
 def colsum_reduce(partial, out, accumulate=False):
     _dev_check(partial, out)
     N.call("mmu_colsum_reduce", _ptr(partial), partial.shape[0], partial.shape[1], _ptr(out), int(accumulate),
            _stream(out))
 
 
-def colsum_bf16(X, out, partial=None, accumulate=False):
+def colsum_bf16(X, out, accumulate=False):
     _dev_check(X, out)
     M, N_ = X.shape
-    if partial is None:
-        partial = torch.empty(((M + 255) // 256, N_), dtype=torch.float32, device=X.device)
-    N.call("mmu_colsum_bf16", _ptr(X), M, N_, X.stride(0), _ptr(partial), _ptr(out), int(accumulate), _stream(X))
+    N.call("mmu_colsum_bf16", _ptr(X), M, N_, X.stride(0), None, _ptr(out), int(accumulate), _stream(X))
 
 
 def attention_fwd(qkv, keymask, O, lse, batch, L, heads=12, drop_p=0.0, seed=0):

@@ -6,19 +6,26 @@ Child order and parameter names follow torchvision's resnet152 so that
 use torchvision's default init (He-normal fan_out convs, BN gamma 1 / beta 0).
 On MI355X the trunk runs through MIOpen in bf16, channels-last (ImageEncoder).
 """
+import torch
 import torch.nn as nn
 
 
 class BatchNorm2d(nn.BatchNorm2d):
-    """BatchNorm2d whose inference form is a per-channel affine (y = x * s + t with
-    s = w / sqrt(var + eps), t = b - mean * s) computed in the activation dtype.
-    Training keeps MIOpen's batch-statistics kernel.  (On this ROCm 7.2 stack MIOpen's
-    bf16 NHWC inference batch-norm crashes in host code; the affine form is also one
-    elementwise pass.)"""
+    """BatchNorm2d with two MI355X-specific forms (state_dict / semantics unchanged):
+    * inference: a per-channel affine y = x * s + t (s = w / sqrt(var + eps),
+      t = b - mean * s) in the activation dtype -- one elementwise pass;
+    * training: MIOpen's batch-statistics kernels for real batches, PyTorch's native
+      NHWC kernels below MIOPEN_MIN_BATCH images.
+    On this ROCm 7.2 stack MIOpen's bf16 NHWC batch-norm crashes in host code for tiny
+    batches (B=2 in training; inference), while the native kernels are ~2x slower at
+    B=256 (DESIGN.md, "ResNet trunk")."""
+
+    MIOPEN_MIN_BATCH = 8
 
     def forward(self, x):
         if self.training or not self.track_running_stats:
-            return super().forward(x)
+            with torch.backends.cudnn.flags(enabled=x.shape[0] >= self.MIOPEN_MIN_BATCH):
+                return super().forward(x)
         s = self.weight * (self.running_var + self.eps).rsqrt()
         t = self.bias - self.running_mean * s
         return x * s.view(1, -1, 1, 1).to(x.dtype) + t.view(1, -1, 1, 1).to(x.dtype)

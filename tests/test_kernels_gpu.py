@@ -98,14 +98,43 @@ def test_gemm_gelu_dgelu_colsum(dev):
     G = rnd(M, Kd, dev=dev, seed=9)
     W = rnd(Kd, N, dev=dev, seed=10, scale=0.2)  # stored [K][N] -> MN-major B
     out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-    part = torch.empty(k.colsum_partial_rows(M), N, dtype=torch.float32, device=dev)
-    k.gemm(G, Kd, True, W, N, False, out, N, M, N, Kd, epi=k.epilogue(k.EPI_DGELU, aux=Z, colsum=part))
+    cs = torch.full((N,), 1.0, device=dev)  # the epilogue ADDS its column sums (bias-grad accumulation)
+    k.gemm(G, Kd, True, W, N, False, out, N, M, N, Kd, epi=k.epilogue(k.EPI_DGELU, aux=Z, colsum=cs))
     zz = Z.float().requires_grad_(True)
     g = torch.autograd.grad(torch.nn.functional.gelu(zz), zz, G.float() @ W.float())[0]
     close(out, g)
-    cs = torch.empty(N, device=dev)
-    k.colsum_reduce(part, cs)
-    torch.testing.assert_close(cs, g.sum(0), rtol=2e-2, atol=2e-2 * g.abs().sum(0).max().item() / 50)
+    torch.testing.assert_close(cs, g.sum(0) + 1.0, rtol=2e-2, atol=2e-2 * g.abs().sum(0).max().item() / 50)
+
+
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, False), (False, True)])
+@pytest.mark.parametrize("M,N,Kd", [(512, 256, 128), (700, 768, 192), (1024, 384, 4096)])
+def test_gemm_big_tiles(dev, ak, bk, M, N, Kd):
+    """256x256 LDS-DMA tiling (M, N >= 256): all layouts, ragged M/N tails, deep K."""
+    k = K()
+    if not ak and M % 128:
+        pytest.skip("M-major A needs M % 128 == 0")
+    A = rnd(M, Kd, dev=dev, seed=41) if ak else rnd(Kd, M, dev=dev, seed=41)
+    B = rnd(N, Kd, dev=dev, seed=42) if bk else rnd(Kd, N, dev=dev, seed=42)
+    C = torch.full((M, N), 3.0, dtype=torch.float32, device=dev)
+    k.gemm(A, A.shape[1], ak, B, B.shape[1], bk, C, N, M, N, Kd, epi=k.epilogue(k.EPI_STORE, accumulate=True))
+    ref = op(A, ak, M, Kd) @ op(B, bk, N, Kd).t() + 3.0
+    torch.testing.assert_close(C, ref, rtol=1e-4, atol=5e-3)
+
+
+def test_gemm_big_tiles_epilogues(dev):
+    k = K()
+    M, N, Kd = 777, 768, 256
+    A, B = rnd(M, Kd, dev=dev, seed=51), rnd(N, Kd, dev=dev, seed=52, scale=0.1)
+    bias = torch.randn(N, device=dev) * 0.1
+    R = rnd(M, N, dev=dev, seed=53)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    k.gemm(A, Kd, True, B, Kd, True, out, N, M, N, Kd, epi=k.epilogue(k.EPI_BIAS_DROP_RES, bias=bias, residual=R))
+    close(out, R.float() + A.float() @ B.float().t() + bias)
+    Z = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    k.gemm(A, Kd, True, B, Kd, True, out, N, M, N, Kd, epi=k.epilogue(k.EPI_BIAS_GELU, bias=bias, aux=Z))
+    z = A.float() @ B.float().t() + bias
+    close(Z, z)
+    close(out, torch.nn.functional.gelu(z))
 
 
 def test_gemm_bias_dropout_residual(dev):
