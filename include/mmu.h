@@ -92,17 +92,21 @@ int mmu_colsum_bf16(const void* X, int64_t M, int64_t N, int64_t ldx, float* par
  * softmax / dropout / context (inside the encoder call src/mmbt.py:124-126).
  *   O   [rows, ld_o] bf16 (col h*64)   LSE [batch*heads, L] f32 (natural log-sum-exp
  *   of the scaled+masked scores).  keymask [batch, L] f32 additive.
+ *   dropmask (may be NULL): [batch*heads, L, ceil(L/64)] u64 keep bits of the
+ *   attention-probs dropout (bit k of word j = key 64j+k kept), written when
+ *   drop_p > 0 for the backward to read.
  */
 int mmu_attention_fwd(const void* QKV, int64_t ld_qkv, const float* keymask,
                       void* O, int64_t ld_o, float* LSE,
                       int64_t batch, int64_t L, int64_t heads,
-                      float drop_p, uint64_t seed, mmu_stream_t stream);
-/* dQKV [rows, ld_dqkv] bf16 from dO; `delta` workspace [batch*heads, L] f32. */
+                      float drop_p, uint64_t seed, uint64_t* dropmask, mmu_stream_t stream);
+/* dQKV [rows, ld_dqkv] bf16 from dO; `delta` workspace [batch*heads, L] f32;
+ * dropmask = the forward's (required when drop_p > 0). */
 int mmu_attention_bwd(const void* QKV, int64_t ld_qkv, const float* keymask,
                       const void* O, int64_t ld_o, const void* dO, int64_t ld_do,
                       const float* LSE, float* delta, void* dQKV, int64_t ld_dqkv,
                       int64_t batch, int64_t L, int64_t heads,
-                      float drop_p, uint64_t seed, mmu_stream_t stream);
+                      float drop_p, uint64_t seed, const uint64_t* dropmask, mmu_stream_t stream);
 
 /* ------------------------------------------------------------------ LayerNorm
  * y = LN(x) * w + b over the last dim (768), eps; x, y bf16 [rows, H]; saves

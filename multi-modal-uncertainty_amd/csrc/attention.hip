@@ -18,7 +18,8 @@
 //
 // Dropout: element (q, key) of head-row bh draws 16 bits from
 // lowbias32(((q*Lp + key) >> 1) ^ seed_bh), low/high half by key parity; dropped
-// when < round(p*65536).  fwd, dQ and dKdV regenerate identical masks.
+// when < round(p*65536).  The forward hashes and stores the keep bits as one u64
+// per (bh, query, 64-key tile) in `dropmask`; dQ and dKdV read those bits.
 #include "mmu_common.h"
 #include "mmu_internal.h"
 
@@ -39,10 +40,8 @@ static __device__ __forceinline__ uint32_t seed_for(uint64_t seed, int bh) {
 static __device__ __forceinline__ uint32_t drop_pair(uint32_t sbh, uint32_t q, uint32_t key, uint32_t Lp) {
   return lowbias32(((q * Lp + key) >> 1) ^ sbh);
 }
-static __device__ __forceinline__ bool keep_elem(uint32_t sbh, uint32_t q, uint32_t key, uint32_t Lp, uint32_t thr) {
-  uint32_t h = drop_pair(sbh, q, key & ~1u, Lp);
-  return ((h >> ((key & 1) * 16)) & 0xFFFFu) >= thr;
-}
+
+static __device__ __forceinline__ uint32_t drop_thr(float p) { return (uint32_t)(p * 65536.0f + 0.5f); }
 
 static __device__ __forceinline__ int fsw(int r) { return (((r >> 1) & 1) << 2) | ((r >> 3) & 3); }
 static __device__ __forceinline__ int tile_off(int row, int chunk) { return row * 128 + ((chunk ^ fsw(row)) << 4); }
@@ -118,7 +117,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
   const bf16* Vb = base + 2 * HD;
   const float* km = p.keymask + (int64_t)b * L;
   const uint32_t sbh = seed_for(p.seed, bh), Lp = (uint32_t)((L + 1) & ~1);
-  const uint32_t thr = (uint32_t)(p.drop_p * 65536.0f + 0.5f);
+  const uint32_t thr = drop_thr(p.drop_p);
 
   bf16x8 qf[4];
 #pragma unroll
@@ -190,17 +189,26 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
       if (thr) {
+        uint64_t kbits = 0;  // keep bits of this lane's 32 keys of the tile (bit = key - j*KV)
 #pragma unroll
         for (int st = 0; st < 2; ++st)
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            const uint32_t key = j * KV + 32 * st + 8 * g + 4 * h;
+            const int kl = 32 * st + 8 * g + 4 * h;
+            const uint32_t key = j * KV + kl;
             uint32_t h0 = drop_pair(sbh, q, key, Lp), h1 = drop_pair(sbh, q, key + 2, Lp);
-            if ((h0 & 0xFFFFu) < thr) sc[st][4 * g + 0] = 0.f;
-            if ((h0 >> 16) < thr) sc[st][4 * g + 1] = 0.f;
-            if ((h1 & 0xFFFFu) < thr) sc[st][4 * g + 2] = 0.f;
-            if ((h1 >> 16) < thr) sc[st][4 * g + 3] = 0.f;
+            const uint32_t k4 = ((h0 & 0xFFFFu) >= thr ? 1u : 0u) | ((h0 >> 16) >= thr ? 2u : 0u) |
+                                ((h1 & 0xFFFFu) >= thr ? 4u : 0u) | ((h1 >> 16) >= thr ? 8u : 0u);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (!((k4 >> e) & 1)) sc[st][4 * g + e] = 0.f;
+            kbits |= (uint64_t)k4 << kl;
           }
+        if (p.dropmask) {  // the backward kernels read these bits instead of re-hashing
+          const uint64_t other = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(kbits >> 32), 32, 64) << 32) |
+                                 (uint32_t)__shfl_xor((int)(uint32_t)kbits, 32, 64);
+          if (h == 0 && q < L) p.dropmask[((int64_t)bh * L + q) * nkv + j] = kbits | other;
+        }
       }
 #pragma unroll
       for (int st = 0; st < 2; ++st)
@@ -268,9 +276,8 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnParams p) {
   const bf16* Kb = base + HD;
   const bf16* Vb = base + 2 * HD;
   const float* km = p.keymask + (int64_t)b * L;
-  const uint32_t sbh = seed_for(p.seed, bh), Lp = (uint32_t)((L + 1) & ~1);
-  const uint32_t thr = (uint32_t)(p.drop_p * 65536.0f + 0.5f);
-  const float zs = p.drop_p > 0.f ? 1.0f / (1.0f - p.drop_p) : 1.0f;
+  const bool drop = drop_thr(p.drop_p) != 0;  // same test as the forward's
+  const float zs = drop ? 1.0f / (1.0f - p.drop_p) : 1.0f;
 
   bf16x8 qf[4], df[4];
   const bf16* dob = p.dout + ((int64_t)b * L + q) * p.ld_do + hd * 64;
@@ -289,6 +296,11 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnParams p) {
 
   TileLoader<KV, 256> lk, lv;
   const int nkv = (L + KV - 1) / KV;
+  // keep bits of this query row (written by the forward), pre-shifted by 4h so the bit
+  // of accumulator register r of sub-tile st sits at the constant 32st + (r&3) + 8(r>>2)
+  const uint64_t* kwp = p.dropmask + ((int64_t)bh * L + q) * nkv;
+  const bool kwl = drop && qv;
+  uint64_t kw = kwl ? kwp[0] : ~0ull;
   lk.load(Kb, p.ld_qkv, 0, L, t);
   lv.load(Vb, p.ld_qkv, 0, L, t);
   lk.store(smem, t);
@@ -302,12 +314,15 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnParams p) {
     const float* mk = maskL + stg * KV;
     const bool more = j + 1 < nkv;
     float mnext = 0.f;
+    uint64_t kwn = ~0ull;
     if (more) {
       lk.load(Kb, p.ld_qkv, (j + 1) * KV, L, t);
       lv.load(Vb, p.ld_qkv, (j + 1) * KV, L, t);
       if (t < KV) { int key = (j + 1) * KV + t; mnext = key < L ? km[key] * LOG2E : NEG_INF; }
+      if (kwl) kwn = kwp[j + 1];
     }
     if (wave_live) {
+      const uint64_t kwh = kw >> (4 * h);
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
         f32x16 sc, dp;
@@ -320,16 +335,12 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnParams p) {
         }
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const uint32_t key = j * KV + 32 * st + 8 * g + 4 * h;
-          uint32_t h0 = 0xFFFFFFFFu, h1 = 0xFFFFFFFFu;
-          if (thr) { h0 = drop_pair(sbh, q, key, Lp); h1 = drop_pair(sbh, q, key + 2, Lp); }
-          const uint32_t bits[4] = {h0 & 0xFFFFu, h0 >> 16, h1 & 0xFFFFu, h1 >> 16};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int r = 4 * g + e;
-            const int kl = 32 * st + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int kc = 32 * st + (r & 3) + 8 * (r >> 2), kl = kc + 4 * h;
             float pr = exp2f(sc[r] * LOG2E + mk[kl] - lse2);
-            float dpv = bits[e] >= thr ? dp[r] * zs : 0.f;
+            float dpv = ((kwh >> kc) & 1) ? dp[r] * zs : 0.f;
             sc[r] = pr * (dpv - dlt);  // dS^T
           }
         }
@@ -348,6 +359,7 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnParams p) {
       lv.store(dK + TILE, t);
       if (t < KV) maskL[(stg ^ 1) * KV + t] = mnext;
     }
+    kw = kwn;
     __syncthreads();
   }
   if (!qv) return;
@@ -363,10 +375,11 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnParams p) {
 }
 
 // dK, dV: grid (ceil(L/64), batch*heads), 128 threads; wave owns 32 keys; loops over 32-query tiles
-__global__ __launch_bounds__(128) void attn_dkdv_kernel(AttnParams p) {
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void attn_dkdv_kernel(AttnParams p) {
   constexpr int QT = 32, TILE = QT * 128;
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE + 2 * 2 * QT * 4];
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE + 2 * 2 * QT * 4 + 2 * QT * 8];
   float* rowL = (float*)(smem + 4 * TILE);  // [stage][2][QT]: lse2, delta
+  uint64_t* rowK = (uint64_t*)(rowL + 4 * QT);  // [stage][QT]: keep bits of this block's 64 keys
   const int t = threadIdx.x, l = t & 63, w = t >> 6, h = l >> 5;
   const int bh = blockIdx.y, b = bh / p.heads, hd = bh - b * p.heads;
   const int L = p.L, HD = p.heads * 64;
@@ -374,9 +387,9 @@ __global__ __launch_bounds__(128) void attn_dkdv_kernel(AttnParams p) {
   const bool wave_live = k0w < L, kv = key < L;
   const bf16* base = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64;
   const bf16* dob = p.dout + (int64_t)b * L * p.ld_do + hd * 64;
-  const uint32_t sbh = seed_for(p.seed, bh), Lp = (uint32_t)((L + 1) & ~1);
-  const uint32_t thr = (uint32_t)(p.drop_p * 65536.0f + 0.5f);
-  const float zs = p.drop_p > 0.f ? 1.0f / (1.0f - p.drop_p) : 1.0f;
+  const bool drop = drop_thr(p.drop_p) != 0;  // same test as the forward's
+  const float zs = drop ? 1.0f / (1.0f - p.drop_p) : 1.0f;
+  const int nkv = (L + 63) / 64;
   const float mkey = kv ? p.keymask[(int64_t)b * L + key] * LOG2E : NEG_INF;
 
   bf16x8 kf[4], vf[4];
@@ -393,18 +406,20 @@ __global__ __launch_bounds__(128) void attn_dkdv_kernel(AttnParams p) {
 
   TileLoader<QT, 128> lq, ld;
   const int nq = (L + QT - 1) / QT;
-  auto load_rows = [&](int i0, float& a, float& c) {
+  auto load_rows = [&](int i0, float& a, float& c, uint64_t& k) {
     int qq = i0 + (t & 31);
     a = qq < L ? p.lse[(int64_t)bh * L + qq] * LOG2E : __builtin_huge_valf();
     c = qq < L ? p.delta[(int64_t)bh * L + qq] : 0.f;
+    k = (drop && qq < L) ? p.dropmask[((int64_t)bh * L + qq) * nkv + blockIdx.x] : ~0ull;
   };
   float ra = 0.f, rc = 0.f;
+  uint64_t rk = 0;
   lq.load(base, p.ld_qkv, 0, L, t);
   ld.load(dob, p.ld_do, 0, L, t);
-  load_rows(0, ra, rc);
+  load_rows(0, ra, rc, rk);
   lq.store(smem, t, 0.125f);
   ld.store(smem + TILE, t);
-  if (t < QT) { rowL[t] = ra; rowL[QT + t] = rc; }
+  if (t < QT) { rowL[t] = ra; rowL[QT + t] = rc; rowK[t] = rk; }
   __syncthreads();
   for (int i = 0; i < nq; ++i) {
     const int stg = i & 1;
@@ -412,11 +427,12 @@ __global__ __launch_bounds__(128) void attn_dkdv_kernel(AttnParams p) {
     const char* Ds = Qs + TILE;
     const float* lse2 = rowL + stg * 2 * QT;
     const float* dlt = lse2 + QT;
+    const uint32_t* kbit = (const uint32_t*)(rowK + stg * QT);  // [QT][2] halves: this wave's keys = half w
     const bool more = i + 1 < nq;
     if (more) {
       lq.load(base, p.ld_qkv, (i + 1) * QT, L, t);
       ld.load(dob, p.ld_do, (i + 1) * QT, L, t);
-      load_rows((i + 1) * QT, ra, rc);
+      load_rows((i + 1) * QT, ra, rc, rk);
     }
     if (wave_live) {
       f32x16 sc, dp;
@@ -431,10 +447,8 @@ __global__ __launch_bounds__(128) void attn_dkdv_kernel(AttnParams p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int ql = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const uint32_t qq = (uint32_t)(i * QT + ql);
         float pr = exp2f(sc[r] * LOG2E + mkey - lse2[ql]);
-        bool keep = thr ? keep_elem(sbh, qq, (uint32_t)key, Lp, thr) : true;
-        float z = keep ? zs : 0.f;
+        float z = ((kbit[2 * ql + w] >> (l & 31)) & 1u) ? zs : 0.f;
         pz[r] = pr * z;
         sc[r] = pr * (dp[r] * z - dlt[ql]);  // dS
       }
@@ -452,7 +466,11 @@ __global__ __launch_bounds__(128) void attn_dkdv_kernel(AttnParams p) {
       char* dQ = smem + (stg ^ 1) * 2 * TILE;
       lq.store(dQ, t, 0.125f);
       ld.store(dQ + TILE, t);
-      if (t < QT) { rowL[(stg ^ 1) * 2 * QT + t] = ra; rowL[(stg ^ 1) * 2 * QT + QT + t] = rc; }
+      if (t < QT) {
+        rowL[(stg ^ 1) * 2 * QT + t] = ra;
+        rowL[(stg ^ 1) * 2 * QT + QT + t] = rc;
+        rowK[(stg ^ 1) * QT + t] = rk;
+      }
     }
     __syncthreads();
   }

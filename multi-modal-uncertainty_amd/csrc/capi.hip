@@ -182,7 +182,8 @@ static int attn_common(int64_t ld_qkv, int64_t batch, int64_t L, int64_t heads, 
 }
 
 int mmu_attention_fwd(const void* QKV, int64_t ld_qkv, const float* keymask, void* O, int64_t ld_o, float* LSE,
-                      int64_t batch, int64_t L, int64_t heads, float drop_p, uint64_t seed, mmu_stream_t stream) {
+                      int64_t batch, int64_t L, int64_t heads, float drop_p, uint64_t seed, uint64_t* dropmask,
+                      mmu_stream_t stream) {
   if (!QKV || !keymask || !O || !LSE) return fail("mmu_attention_fwd: null pointer");
   if (attn_common(ld_qkv, batch, L, heads, drop_p)) return 1;
   if (ld_o < heads * 64 || ld_o % 4) return fail("mmu_attention_fwd: bad ld_o");
@@ -190,14 +191,18 @@ int mmu_attention_fwd(const void* QKV, int64_t ld_qkv, const float* keymask, voi
   AttnParams p{};
   p.qkv = (const bf16*)QKV; p.ld_qkv = ld_qkv; p.keymask = keymask; p.out = (bf16*)O; p.ld_out = ld_o;
   p.lse = LSE; p.batch = (int)batch; p.L = (int)L; p.heads = (int)heads; p.drop_p = drop_p; p.seed = seed;
+  p.dropmask = dropmask;
   attention_fwd_launch(p, (hipStream_t)stream);
   return check_launch("mmu_attention_fwd");
 }
 
 int mmu_attention_bwd(const void* QKV, int64_t ld_qkv, const float* keymask, const void* O, int64_t ld_o,
                       const void* dO, int64_t ld_do, const float* LSE, float* delta, void* dQKV, int64_t ld_dqkv,
-                      int64_t batch, int64_t L, int64_t heads, float drop_p, uint64_t seed, mmu_stream_t stream) {
+                      int64_t batch, int64_t L, int64_t heads, float drop_p, uint64_t seed,
+                      const uint64_t* dropmask, mmu_stream_t stream) {
   if (!QKV || !keymask || !O || !dO || !LSE || !delta || !dQKV) return fail("mmu_attention_bwd: null pointer");
+  if ((uint32_t)(drop_p * 65536.0f + 0.5f) != 0 && !dropmask)
+    return fail("mmu_attention_bwd: dropout needs the forward's dropmask");
   if (attn_common(ld_qkv, batch, L, heads, drop_p)) return 1;
   if (ld_dqkv < 3 * heads * 64 || ld_do % 8 || ld_o % 8 || ld_dqkv % 4) return fail("mmu_attention_bwd: bad ld");
   if (batch * heads > 65535) return fail("mmu_attention_bwd: batch*heads > 65535");
@@ -205,6 +210,7 @@ int mmu_attention_bwd(const void* QKV, int64_t ld_qkv, const float* keymask, con
   p.qkv = (const bf16*)QKV; p.ld_qkv = ld_qkv; p.keymask = keymask; p.o = (const bf16*)O; p.ld_o = ld_o;
   p.dout = (const bf16*)dO; p.ld_do = ld_do; p.lse = (float*)LSE; p.delta = delta; p.out = (bf16*)dQKV;
   p.ld_out = ld_dqkv; p.batch = (int)batch; p.L = (int)L; p.heads = (int)heads; p.drop_p = drop_p; p.seed = seed;
+  p.dropmask = (uint64_t*)dropmask;
   attention_bwd_launch(p, (hipStream_t)stream);
   return check_launch("mmu_attention_bwd");
 }

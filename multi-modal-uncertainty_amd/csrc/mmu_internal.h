@@ -50,6 +50,7 @@ struct AttnParams {
   float* delta;
   bf16* out;   // O (fwd) or dQKV (bwd)
   int64_t ld_out;
+  uint64_t* dropmask;  // [batch*heads][L][ceil(L/64)] keep bits: written by fwd, read by bwd
   int batch, L, heads;
   float drop_p;
   uint64_t seed;

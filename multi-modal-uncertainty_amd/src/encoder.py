@@ -60,7 +60,8 @@ def layer_forward(lw, X, keymask, B, L, p_attn, p_hid, seeds, save):
     K.gemm(X, HID, True, lw.wqkv16, HID, True, qkv, 3 * HID, M, 3 * HID, HID, epi=K.epilogue(K.EPI_STORE, bias=lw.bqkv))
     O = torch.empty(M, HID, dtype=bf16, device=dev)
     lse = torch.empty(B * HEADS, L, dtype=torch.float32, device=dev)
-    K.attention_fwd(qkv, keymask, O, lse, B, L, HEADS, p_attn, seeds[0])
+    dmask = K.dropmask_empty(B, L, HEADS, dev) if (save and p_attn > 0) else None
+    K.attention_fwd(qkv, keymask, O, lse, B, L, HEADS, p_attn, seeds[0], dmask)
     S1 = torch.empty(M, HID, dtype=bf16, device=dev)
     K.gemm(O, HID, True, lw.wo16, HID, True, S1, HID, M, HID, HID,
            epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw.bo, residual=X, drop_p=p_hid, seed=seeds[1]))
@@ -78,7 +79,7 @@ def layer_forward(lw, X, keymask, B, L, p_attn, p_hid, seeds, save):
     mean2 = torch.empty(M, dtype=torch.float32, device=dev)
     rstd2 = torch.empty(M, dtype=torch.float32, device=dev)
     K.layernorm_fwd(S2, lw.ln2w, lw.ln2b, Y, mean2, rstd2)
-    saved = (X, qkv, O, lse, S1, mean1, rstd1, A, Z, Hh, S2, mean2, rstd2) if save else None
+    saved = (X, qkv, O, lse, dmask, S1, mean1, rstd1, A, Z, Hh, S2, mean2, rstd2) if save else None
     return Y, saved
 
 
@@ -87,7 +88,7 @@ def _reduce(part, out):
 
 
 def layer_backward(lw, saved, dY, keymask, B, L, p_attn, p_hid, seeds, wgrad):
-    X, qkv, O, lse, S1, mean1, rstd1, A, Z, Hh, S2, mean2, rstd2 = saved
+    X, qkv, O, lse, dmask, S1, mean1, rstd1, A, Z, Hh, S2, mean2, rstd2 = saved
     M = B * L
     dev = dY.device
     P = K.ln_parts(M)
@@ -126,7 +127,7 @@ def layer_backward(lw, saved, dY, keymask, B, L, p_attn, p_hid, seeds, wgrad):
     # ---- attention + fused QKV
     dqkv = torch.empty(M, 3 * HID, dtype=bf16, device=dev)
     delta = torch.empty(B * HEADS, L, dtype=torch.float32, device=dev)
-    K.attention_bwd(qkv, keymask, O, dO, lse, delta, dqkv, B, L, HEADS, p_attn, seeds[0])
+    K.attention_bwd(qkv, keymask, O, dO, lse, delta, dqkv, B, L, HEADS, p_attn, seeds[0], dmask)
     if wgrad:
         K.colsum_bf16(dqkv, lw.g_bqkv, accumulate=True)
         K.gemm(dqkv, 3 * HID, False, X, HID, False, lw.g_wqkv, HID, 3 * HID, HID, M, epi=acc)

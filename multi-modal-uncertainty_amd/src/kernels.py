@@ -88,18 +88,41 @@ def colsum_bf16(X, out, accumulate=False):
     N.call("mmu_colsum_bf16", _ptr(X), M, N_, X.stride(0), None, _ptr(out), int(accumulate), _stream(X))
 
 
-def attention_fwd(qkv, keymask, O, lse, batch, L, heads=12, drop_p=0.0, seed=0):
+def dropmask_empty(batch, L, heads=12, device=None):
+    """Keep-bit buffer of the attention-probs dropout: [batch*heads, L, ceil(L/64)] words
+    (int64 storage of the kernel's u64; bit k of word j = key 64j+k kept)."""
+    return torch.empty(batch * heads, L, (L + 63) // 64, dtype=torch.int64, device=device)
+
+
+def dropmask_dense(mask, L):
+    """[BH, L, W] keep words -> [BH, L, L] float 0/1 (test/debug helper)."""
+    bits = torch.arange(64, device=mask.device, dtype=torch.int64)
+    d = (mask.unsqueeze(-1) >> bits) & 1
+    return d.flatten(-2)[..., :L].float()
+
+
+def attention_fwd(qkv, keymask, O, lse, batch, L, heads=12, drop_p=0.0, seed=0, dropmask=None):
     _dev_check(qkv, keymask, O, lse)
     _want(qkv, torch.bfloat16, "attention qkv")
+    if dropmask is not None:
+        _dev_check(dropmask)
+        if dropmask.numel() < batch * heads * L * ((L + 63) // 64) or not dropmask.is_contiguous():
+            raise ValueError("attention_fwd: dropmask too small / not contiguous")
     N.call("mmu_attention_fwd", _ptr(qkv), qkv.stride(0), _ptr(keymask), _ptr(O), O.stride(0), _ptr(lse), batch, L,
-           heads, float(drop_p), int(seed), _stream(qkv))
+           heads, float(drop_p), int(seed), _ptr(dropmask) if dropmask is not None else None, _stream(qkv))
 
 
-def attention_bwd(qkv, keymask, O, dO, lse, delta, dqkv, batch, L, heads=12, drop_p=0.0, seed=0):
+def attention_bwd(qkv, keymask, O, dO, lse, delta, dqkv, batch, L, heads=12, drop_p=0.0, seed=0, dropmask=None):
+    """`dropmask` = the buffer the forward filled (required when drop_p > 0); `seed` is
+    kept for signature symmetry with the forward."""
     _dev_check(qkv, keymask, O, dO, lse, delta, dqkv)
+    if dropmask is not None:
+        _dev_check(dropmask)
+        if dropmask.numel() < batch * heads * L * ((L + 63) // 64) or not dropmask.is_contiguous():
+            raise ValueError("attention_bwd: dropmask too small / not contiguous")
     N.call("mmu_attention_bwd", _ptr(qkv), qkv.stride(0), _ptr(keymask), _ptr(O), O.stride(0), _ptr(dO), dO.stride(0),
            _ptr(lse), _ptr(delta), _ptr(dqkv), dqkv.stride(0), batch, L, heads, float(drop_p), int(seed),
-           _stream(qkv))
+           _ptr(dropmask) if dropmask is not None else None, _stream(qkv))
 
 
 def layernorm_fwd(X, w, b, Y, mean, rstd, eps=1e-12, group_rows=0, param_stride=0):

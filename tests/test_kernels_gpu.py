@@ -241,20 +241,51 @@ def test_attention_dropout_consistent(dev):
     probe = probe.view(B * L, 2304)
     O = torch.empty(B * L, 768, dtype=torch.bfloat16, device=dev)
     lse = torch.empty(B * 12, L, device=dev)
-    k.attention_fwd(probe, km, O, lse, B, L, drop_p=p, seed=seed)
+    dm = k.dropmask_empty(B, L, 12, dev)
+    k.attention_fwd(probe, km, O, lse, B, L, drop_p=p, seed=seed, dropmask=dm)
     Pd = O.float().view(B, L, 12, 64).permute(0, 2, 1, 3)[..., :L]  # [B,h,q,key] = P*mask/(1-p)
     mask = (Pd > 0).float()
     rate = 1 - mask.mean().item()
     assert abs(rate - p) < 0.02, rate
+    # the emitted keep bits are exactly the mask the forward applied
+    assert torch.equal(k.dropmask_dense(dm, L).view(B, 12, L, L), mask)
     # (b) forward on the real V with the recovered mask
-    k.attention_fwd(qkv, km, O, lse, B, L, drop_p=p, seed=seed)
+    k.attention_fwd(qkv, km, O, lse, B, L, drop_p=p, seed=seed, dropmask=dm)
     o_ref, _ = attn_ref(qkv, km, B, L, dropmask=mask, p=p)
     close(O, o_ref, atol_frac=2e-2)
     # (c) backward
     dO = rnd(B * L, 768, dev=dev, seed=7)
     dqkv = torch.zeros(B * L, 2304, dtype=torch.bfloat16, device=dev)
     delta = torch.empty(B * 12, L, device=dev)
-    k.attention_bwd(qkv, km, O, dO, lse, delta, dqkv, B, L, drop_p=p, seed=seed)
+    k.attention_bwd(qkv, km, O, dO, lse, delta, dqkv, B, L, drop_p=p, seed=seed, dropmask=dm)
+    x = qkv.float().requires_grad_(True)
+    o2, _ = attn_ref(x, km, B, L, dropmask=mask, p=p)
+    (g,) = torch.autograd.grad(o2, x, dO.float())
+    for part in range(3):
+        close(dqkv[:, 768 * part:768 * (part + 1)], g[:, 768 * part:768 * (part + 1)], atol_frac=3e-2)
+    with pytest.raises(Exception):  # dropout backward without the forward's bits is refused
+        k.attention_bwd(qkv, km, O, dO, lse, delta, dqkv, B, L, drop_p=p, seed=seed)
+
+
+@pytest.mark.parametrize("B,L", [(2, 200), (1, 321)])
+def test_attention_dropout_multiword(dev, B, L):
+    """L > 64: several keep words per query row; fwd and bwd against autograd with the
+    mask decoded from the emitted bits, plus the drop rate."""
+    k = K()
+    p, seed = 0.1, 1234
+    qkv, km = make_attn_inputs(dev, B, L, pad=True, seed=11, scale=1.0)
+    O = torch.empty(B * L, 768, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(B * 12, L, device=dev)
+    dm = k.dropmask_empty(B, L, 12, dev)
+    k.attention_fwd(qkv, km, O, lse, B, L, drop_p=p, seed=seed, dropmask=dm)
+    mask = k.dropmask_dense(dm, L).view(B, 12, L, L)
+    assert abs((1 - mask.mean().item()) - p) < 0.01
+    o_ref, _ = attn_ref(qkv, km, B, L, dropmask=mask, p=p)
+    close(O, o_ref, atol_frac=2e-2)
+    dO = rnd(B * L, 768, dev=dev, seed=8)
+    dqkv = torch.zeros(B * L, 2304, dtype=torch.bfloat16, device=dev)
+    delta = torch.empty(B * 12, L, device=dev)
+    k.attention_bwd(qkv, km, O, dO, lse, delta, dqkv, B, L, drop_p=p, seed=seed, dropmask=dm)
     x = qkv.float().requires_grad_(True)
     o2, _ = attn_ref(x, km, B, L, dropmask=mask, p=p)
     (g,) = torch.autograd.grad(o2, x, dO.float())
