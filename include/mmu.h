@@ -46,9 +46,9 @@ const char* mmu_last_error(void);
  */
 enum {
   MMU_EPI_STORE = 0,        /* C = acc (+bias[n]) (+C if accumulate)                     */
-  MMU_EPI_BIAS_GELU = 1,    /* aux = bf16(acc+bias); C = gelu_erf(acc+bias)              */
+  MMU_EPI_BIAS_GELU = 1,    /* z = acc+bias; C = gelu_erf(z); aux (optional) = gelu'(z)  */
   MMU_EPI_BIAS_DROP_RES = 2,/* C = residual + dropout(acc+bias)                          */
-  MMU_EPI_DGELU = 3,        /* C = acc * gelu'(aux)                                      */
+  MMU_EPI_DGELU = 3,        /* C = acc * aux   (aux = the forward's gelu'(z))            */
   MMU_EPI_ADD_RES = 4       /* C = acc + residual                                        */
 };
 typedef struct mmu_epilogue {
@@ -58,7 +58,7 @@ typedef struct mmu_epilogue {
   int64_t bias_bstride;
   const void* residual;     /* bf16 [M, ldr]                                            */
   int64_t ldr, res_bstride;
-  void* aux;                /* bf16 [M, ldx]: GELU pre-activation (written or read)     */
+  void* aux;                /* bf16 [M, ldx]: GELU derivative (written or read)         */
   int64_t ldx, aux_bstride;
   float* colsum;            /* f32 [N] per batch: += column sums of the final C (bias grads) */
   int64_t colsum_bstride;

@@ -96,7 +96,10 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
   p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
   p.sA = strideA; p.sB = strideB; p.sC = strideC;
   // big (256x256, LDS-DMA) tiling needs >= 256 rows/cols and 32-bit buffer offsets per operand
-  const int64_t a_span = 2 * (a_kmajor ? M * lda : K * lda), b_span = 2 * (b_kmajor ? N * ldb : K * ldb);
+  // (spans include the rows a 256-tile / 64-deep K-tile may address past the end, so the
+  // 32-bit buffer offsets of those out-of-range reads never wrap back into the operand)
+  const int64_t a_span = 2 * (a_kmajor ? (M + 256) * lda : (K + 64) * lda);
+  const int64_t b_span = 2 * (b_kmajor ? (N + 256) * ldb : (K + 64) * ldb);
   const bool big = M >= 256 && N >= 256 && a_span < (1ll << 32) - 4096 && b_span < (1ll << 32) - 4096;
   const int tile = big ? 256 : 128;
   p.tiles_m = (int)((M + tile - 1) / tile);
@@ -114,7 +117,7 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
   p.kind = kind;
   if (kind < 0 || kind > MMU_EPI_ADD_RES) return fail("mmu_gemm: bad epilogue kind %d", kind);
   if (kind != MMU_EPI_STORE && c_dtype != MMU_BF16) return fail("mmu_gemm: fused epilogues write bf16");
-  if ((kind == MMU_EPI_BIAS_GELU || kind == MMU_EPI_DGELU) && !p.aux) return fail("mmu_gemm: epilogue needs aux");
+  if (kind == MMU_EPI_DGELU && !p.aux) return fail("mmu_gemm: DGELU epilogue needs aux");
   if ((kind == MMU_EPI_BIAS_DROP_RES || kind == MMU_EPI_ADD_RES) && !p.residual)
     return fail("mmu_gemm: epilogue needs residual");
   if (p.accumulate && c_dtype != MMU_F32) return fail("mmu_gemm: accumulate needs f32 C");

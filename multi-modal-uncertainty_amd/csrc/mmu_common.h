@@ -19,32 +19,51 @@ static __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 // ---------------------------------------------------------------- counter-based RNG
 // SplitMix64 finaliser of (seed + ctr * golden): stateless, so forward and backward
 // regenerate the same dropout mask from (seed, element counter).
-static __device__ __forceinline__ uint64_t mmu_mix64(uint64_t seed, uint64_t ctr) {
-  uint64_t z = seed + ctr * 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
+static __device__ __forceinline__ uint32_t mmu_lowbias32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
 }
-// keep-mask for 4 consecutive elements [4*q, 4*q+4) of a stream: 16 random bits each.
+// 32-bit stream key of a 64-bit dropout seed (wave-uniform: folded into scalar code)
+static __device__ __forceinline__ uint32_t mmu_seed32(uint64_t seed) {
+  return mmu_lowbias32((uint32_t)seed ^ mmu_lowbias32((uint32_t)(seed >> 32) ^ 0x68bc21ebu));
+}
+// keep-mask for 4 consecutive elements [4*q, 4*q+4) of a stream: 16 random bits each,
+// from two 32-bit hashes of (2q, 2q+1) ^ key (4 integer multiplies per quad).
 // An element is dropped when its 16-bit draw is < thr16 (= round(p * 65536)).
 static __device__ __forceinline__ uint32_t mmu_keep4(uint64_t seed, uint64_t quad, uint32_t thr16) {
-  uint64_t z = mmu_mix64(seed, quad);
-  uint32_t m = 0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) m |= (((uint32_t)(z >> (16 * i)) & 0xFFFFu) >= thr16 ? 1u : 0u) << i;
-  return m;
+  const uint32_t x = (((uint32_t)quad << 1) ^ ((uint32_t)(quad >> 31) * 0x9E3779B8u)) ^ mmu_seed32(seed);
+  const uint32_t h0 = mmu_lowbias32(x), h1 = mmu_lowbias32(x ^ 1u);
+  return ((h0 & 0xFFFFu) >= thr16 ? 1u : 0u) | ((h0 >> 16) >= thr16 ? 2u : 0u) |
+         ((h1 & 0xFFFFu) >= thr16 ? 4u : 0u) | ((h1 >> 16) >= thr16 ? 8u : 0u);
 }
 static __device__ __forceinline__ bool mmu_keep1(uint64_t seed, uint64_t idx, uint32_t thr16) {
-  uint64_t z = mmu_mix64(seed, idx >> 2);
-  return ((uint32_t)(z >> (16 * (idx & 3))) & 0xFFFFu) >= thr16;
+  const uint64_t quad = idx >> 2;
+  const uint32_t x = (((uint32_t)quad << 1) ^ ((uint32_t)(quad >> 31) * 0x9E3779B8u)) ^ mmu_seed32(seed);
+  const uint32_t h = mmu_lowbias32(x ^ (uint32_t)((idx >> 1) & 1));
+  return ((h >> (16 * (idx & 1))) & 0xFFFFu) >= thr16;
 }
 
 // ---------------------------------------------------------------- math
-static __device__ __forceinline__ float gelu_erf(float z) {
-  return 0.5f * z * (1.0f + erff(z * 0.70710678118654752f));
+// GELU (erf form, as pytorch_pretrained_bert's gelu) and its derivative from ONE
+// branch-free evaluation: erf(x) = 1 - t*P(t)*exp(-x^2), t = 1/(1 + 0.3275911 x), x >= 0
+// (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7), so Phi(z) and phi(z) share the exp.
+static __device__ __forceinline__ void gelu_pair(float z, float& g, float& dg) {
+  const float x = fabsf(z) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, x, 1.0f));
+  float P = fmaf(1.061405429f, t, -1.453152027f);
+  P = fmaf(P, t, 1.421413741f);
+  P = fmaf(P, t, -0.284496736f);
+  P = fmaf(P, t, 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f(z * z * -0.72134752044448170f);  // exp(-z^2/2) = exp(-x^2)
+  const float h = 0.5f * (t * P) * e;                                      // = 1 - Phi(|z|)
+  const float phi = z >= 0.f ? 1.0f - h : h;                               // Phi(z)
+  g = z * phi;
+  dg = fmaf(z * 0.39894228040143268f, e, phi);                             // Phi(z) + z phi(z)
 }
-static __device__ __forceinline__ float gelu_erf_grad(float z) {
-  return 0.5f * (1.0f + erff(z * 0.70710678118654752f)) + z * 0.39894228040143268f * __expf(-0.5f * z * z);
+static __device__ __forceinline__ float gelu_erf(float z) {
+  float g, dg;
+  gelu_pair(z, g, dg);
+  return g;
 }
 
 static __device__ __forceinline__ float wave_sum(float v) {

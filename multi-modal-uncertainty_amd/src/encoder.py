@@ -7,7 +7,7 @@ Forward per layer (M = B*L token rows, bf16 activations, f32 accumulation):
   O, lse = attention(qkv, keymask)            mmu_attention_fwd (dropout on P)
   S1 = X + dropout(O Wo^T + bo)               mmu_gemm  EPI_BIAS_DROP_RES
   A  = LN1(S1)                                mmu_layernorm_fwd
-  H  = gelu(Z), Z = A W1^T + b1               mmu_gemm  EPI_BIAS_GELU (Z kept)
+  H  = gelu(A W1^T + b1)                      mmu_gemm  EPI_BIAS_GELU (saves Z = gelu'(.), bf16)
   S2 = A + dropout(H W2^T + b2)               mmu_gemm  EPI_BIAS_DROP_RES
   Y  = LN2(S2)                                mmu_layernorm_fwd
 Backward mirrors it; weight gradients are written straight into the flat f32
@@ -69,7 +69,7 @@ def layer_forward(lw, X, keymask, B, L, p_attn, p_hid, seeds, save):
     mean1 = torch.empty(M, dtype=torch.float32, device=dev)
     rstd1 = torch.empty(M, dtype=torch.float32, device=dev)
     K.layernorm_fwd(S1, lw.ln1w, lw.ln1b, A, mean1, rstd1)
-    Z = torch.empty(M, FFN, dtype=bf16, device=dev)
+    Z = torch.empty(M, FFN, dtype=bf16, device=dev) if save else None  # gelu'(A W1^T + b1), for the backward
     Hh = torch.empty(M, FFN, dtype=bf16, device=dev)
     K.gemm(A, HID, True, lw.w116, HID, True, Hh, FFN, M, FFN, HID, epi=K.epilogue(K.EPI_BIAS_GELU, bias=lw.b1, aux=Z))
     S2 = torch.empty(M, HID, dtype=bf16, device=dev)

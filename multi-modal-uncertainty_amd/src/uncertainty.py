@@ -62,10 +62,9 @@ class EnsembleMMBT:
                                           res_bstride=M * HID, drop_p=p_hid, seed=seeds[1]))
         A = torch.empty_like(O)
         K.layernorm_fwd(S1, lw["ln1w"], lw["ln1b"], A, None, None, LN_EPS, group_rows=M, param_stride=HID)
-        Z = torch.empty(Km * M, FFN, dtype=bf16, device=dev)
-        Hh = torch.empty_like(Z)
+        Hh = torch.empty(Km * M, FFN, dtype=bf16, device=dev)
         K.gemm(A, HID, True, lw["w116"], HID, True, Hh, FFN, M, FFN, HID, batch=Km, sA=M * HID, sB=FFN * HID,
-               sC=M * FFN, epi=K.epilogue(K.EPI_BIAS_GELU, bias=lw["b1"], bias_bstride=FFN, aux=Z, aux_bstride=M * FFN))
+               sC=M * FFN, epi=K.epilogue(K.EPI_BIAS_GELU, bias=lw["b1"], bias_bstride=FFN))
         S2 = torch.empty_like(O)
         K.gemm(Hh, FFN, True, lw["w216"], FFN, True, S2, HID, M, HID, FFN, batch=Km, sA=M * FFN, sB=HID * FFN,
                sC=M * HID, epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw["b2"], bias_bstride=HID, residual=A,

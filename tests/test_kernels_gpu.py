@@ -91,17 +91,18 @@ def test_gemm_gelu_dgelu_colsum(dev):
     Z = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
     Hh = torch.empty_like(Z)
     k.gemm(A, Kd, True, B, Kd, True, Hh, N, M, N, Kd, epi=k.epilogue(k.EPI_BIAS_GELU, bias=bias, aux=Z))
-    z = A.float() @ B.float().t() + bias
-    close(Z, z)
-    close(Hh, torch.nn.functional.gelu(z))
-    # dgelu with column sums
+    z = (A.float() @ B.float().t() + bias).requires_grad_(True)
+    gz = torch.nn.functional.gelu(z)  # erf form
+    (dgz,) = torch.autograd.grad(gz.sum(), z)
+    close(Hh, gz.detach())
+    close(Z, dgz)  # aux = gelu'(z)
+    # dgelu with column sums: C = acc * aux
     G = rnd(M, Kd, dev=dev, seed=9)
     W = rnd(Kd, N, dev=dev, seed=10, scale=0.2)  # stored [K][N] -> MN-major B
     out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
     cs = torch.full((N,), 1.0, device=dev)  # the epilogue ADDS its column sums (bias-grad accumulation)
     k.gemm(G, Kd, True, W, N, False, out, N, M, N, Kd, epi=k.epilogue(k.EPI_DGELU, aux=Z, colsum=cs))
-    zz = Z.float().requires_grad_(True)
-    g = torch.autograd.grad(torch.nn.functional.gelu(zz), zz, G.float() @ W.float())[0]
+    g = (G.float() @ W.float()) * dgz
     close(out, g)
     torch.testing.assert_close(cs, g.sum(0) + 1.0, rtol=2e-2, atol=2e-2 * g.abs().sum(0).max().item() / 50)
 
@@ -132,9 +133,13 @@ def test_gemm_big_tiles_epilogues(dev):
     close(out, R.float() + A.float() @ B.float().t() + bias)
     Z = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
     k.gemm(A, Kd, True, B, Kd, True, out, N, M, N, Kd, epi=k.epilogue(k.EPI_BIAS_GELU, bias=bias, aux=Z))
-    z = A.float() @ B.float().t() + bias
-    close(Z, z)
-    close(out, torch.nn.functional.gelu(z))
+    z = (A.float() @ B.float().t() + bias).requires_grad_(True)
+    gz = torch.nn.functional.gelu(z)
+    close(out, gz.detach())
+    close(Z, torch.autograd.grad(gz.sum(), z)[0])
+    out2 = torch.empty_like(out)  # aux is optional (inference)
+    k.gemm(A, Kd, True, B, Kd, True, out2, N, M, N, Kd, epi=k.epilogue(k.EPI_BIAS_GELU, bias=bias))
+    assert torch.equal(out, out2)
 
 
 def test_gemm_bias_dropout_residual(dev):

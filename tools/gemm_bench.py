@@ -1,0 +1,107 @@
+"""Per-shape throughput of the BERT-layer GEMMs (mmu_gemm) at the bench workload
+(M = 256 x 513 token rows), with hipBLASLt (torch.matmul) on the same shapes as a
+yardstick.  Random operands (zero-filled data inflates MFMA clocks).
+
+  python tools/gemm_bench.py [--rows 131328] [--iters 10]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "multi-modal-uncertainty_amd"))
+from src import kernels as K  # noqa: E402
+
+HID, FFN = 768, 3072
+
+
+def timed(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    best = float("inf")
+    for _ in range(iters):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        best = min(best, a.elapsed_time(b))
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=256 * 513)
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    M, dev, bf = a.rows, "cuda", torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(0)
+
+    def rnd(*s):
+        return (torch.rand(*s, generator=g, device=dev) * 2 - 1).to(bf)
+
+    X, A, O = rnd(M, HID), rnd(M, HID), rnd(M, HID)
+    Hh = rnd(M, FFN)
+    dY, dqkv, dZ = rnd(M, HID), rnd(M, 3 * HID), rnd(M, FFN)
+    Wqkv, Wo, W1, W2 = rnd(3 * HID, HID), rnd(HID, HID), rnd(FFN, HID), rnd(HID, FFN)
+    bqkv, bo, b1 = (torch.randn(n, device=dev) for n in (3 * HID, HID, FFN))
+    out768, out2304, out3072 = (torch.empty(M, n, dtype=bf, device=dev) for n in (HID, 3 * HID, FFN))
+    Zs = rnd(M, FFN)
+    gW = torch.zeros(FFN, HID, device=dev)
+    cs = torch.zeros(FFN, device=dev)
+    cases = [
+        ("fwd qkv  X.Wqkv^T+b", M, 3 * HID, HID,
+         lambda: K.gemm(X, HID, True, Wqkv, HID, True, out2304, 3 * HID, M, 3 * HID, HID,
+                        epi=K.epilogue(K.EPI_STORE, bias=bqkv)),
+         lambda: torch.matmul(X, Wqkv.t())),
+        ("fwd o    drop_res", M, HID, HID,
+         lambda: K.gemm(O, HID, True, Wo, HID, True, out768, HID, M, HID, HID,
+                        epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=bo, residual=X, drop_p=0.1, seed=1)),
+         lambda: torch.matmul(O, Wo.t())),
+        ("fwd ffn1 gelu", M, FFN, HID,
+         lambda: K.gemm(A, HID, True, W1, HID, True, out3072, FFN, M, FFN, HID,
+                        epi=K.epilogue(K.EPI_BIAS_GELU, bias=b1, aux=Zs)),
+         lambda: torch.matmul(A, W1.t())),
+        ("fwd ffn2 drop_res", M, HID, FFN,
+         lambda: K.gemm(Hh, FFN, True, W2, FFN, True, out768, HID, M, HID, FFN,
+                        epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=bo, residual=A, drop_p=0.1, seed=2)),
+         lambda: torch.matmul(Hh, W2.t())),
+        ("bwd dZ   dgelu+colsum", M, FFN, HID,
+         lambda: K.gemm(dY, HID, True, W2, FFN, False, out3072, FFN, M, FFN, HID,
+                        epi=K.epilogue(K.EPI_DGELU, aux=Zs, colsum=cs)),
+         lambda: torch.matmul(dY, W2)),
+        ("bwd dA   add_res", M, HID, FFN,
+         lambda: K.gemm(dZ, FFN, True, W1, HID, False, out768, HID, M, HID, FFN,
+                        epi=K.epilogue(K.EPI_ADD_RES, residual=dY)),
+         lambda: torch.matmul(dZ, W1)),
+        ("bwd dX   qkv add_res", M, HID, 3 * HID,
+         lambda: K.gemm(dqkv, 3 * HID, True, Wqkv, HID, False, out768, HID, M, HID, 3 * HID,
+                        epi=K.epilogue(K.EPI_ADD_RES, residual=dY)),
+         lambda: torch.matmul(dqkv, Wqkv)),
+        ("bwd dO   store", M, HID, HID,
+         lambda: K.gemm(dY, HID, True, Wo, HID, False, out768, HID, M, HID, HID),
+         lambda: torch.matmul(dY, Wo)),
+        ("wgrad W1 dZ^T.A f32acc", FFN, HID, M,
+         lambda: K.gemm(dZ, FFN, False, A, HID, False, gW, HID, FFN, HID, M,
+                        epi=K.epilogue(K.EPI_STORE, accumulate=True)),
+         lambda: torch.matmul(dZ.t(), A)),
+    ]
+    print(f"{'gemm':26s} {'M':>7s} {'N':>5s} {'K':>7s} {'pipe ms':>8s} {'TF/s':>7s} {'2stg ms':>8s} {'TF/s':>7s}"
+          f" {'blasLt ms':>9s} {'TF/s':>7s}")
+    for name, m, n, k, f_mmu, f_ref in cases:
+        fl = 2.0 * m * n * k
+        t0, t1 = float("inf"), float("inf")
+        for _ in range(3):  # interleaved A/B rounds in one process
+            os.environ["MMU_GEMM_PIPE"] = "1"
+            t0 = min(t0, timed(f_mmu, a.iters))
+            os.environ["MMU_GEMM_PIPE"] = "0"
+            t1 = min(t1, timed(f_mmu, a.iters))
+        os.environ["MMU_GEMM_PIPE"] = "1"
+        t2 = timed(f_ref, a.iters)
+        print(f"{name:26s} {m:7d} {n:5d} {k:7d} {t0:8.3f} {fl / t0 / 1e9:7.1f} {t1:8.3f} {fl / t1 / 1e9:7.1f}"
+              f" {t2:9.3f} {fl / t2 / 1e9:7.1f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
