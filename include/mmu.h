@@ -166,6 +166,31 @@ int mmu_row_pool_fwd(const void* fmap, int64_t B, int64_t Hh, int64_t Ww, int64_
 int mmu_row_pool_bwd(const float* dout, int64_t B, int64_t Hh, int64_t Ww, int64_t C, int64_t n,
                      void* dfmap, mmu_stream_t stream);
 
+/* ------------------------------------------------------------------ BatchNorm (image trunk)
+ * BatchNorm2d [+ residual add] [+ ReLU] of the ResNet-152 trunk (torchvision
+ * Bottleneck bn1/bn2/bn3 + downsample, src/mmbt.py:19-21) on channels-last bf16
+ * activations X [rows = N*H*W, C] (C % 8 == 0, C <= 2048):
+ *   Y = act(X * scale + shift [+ skip]),  act = ReLU when relu != 0.
+ * training: batch statistics (biased variance), running_mean / running_var updated
+ *   with momentum (unbiased variance), *num_batches_tracked += 1 (each may be NULL),
+ *   save_mean / save_invstd [C] f32 written for the backward.
+ * eval: running statistics.  weight / bias may be NULL (affine = False).
+ * ws: device scratch of >= mmu_batchnorm_ws_bytes(C) bytes (per-block partial sums +
+ * per-channel coefficients, ~8 MiB), 16-B aligned.
+ */
+int64_t mmu_batchnorm_ws_bytes(int64_t C);
+int mmu_batchnorm_fwd(const void* X, const void* skip, void* Y, int64_t rows, int64_t C,
+                      const float* weight, const float* bias, float* running_mean, float* running_var,
+                      int64_t* num_batches_tracked, int training, float momentum, float eps, int relu,
+                      float* save_mean, float* save_invstd, void* ws, int64_t ws_bytes, mmu_stream_t stream);
+/* Training-mode backward.  g = dY * [Y > 0] when relu (Y = the forward's output), else dY;
+ * dX [rows, C] bf16; dSkip (may be NULL) = g, the gradient of the residual input;
+ * dweight / dbias (may be NULL) f32 [C] are ACCUMULATED (+=). */
+int mmu_batchnorm_bwd(const void* dY, const void* Y, const void* X, int64_t rows, int64_t C,
+                      const float* weight, const float* save_mean, const float* save_invstd, int relu,
+                      void* dX, void* dSkip, float* dweight, float* dbias, void* ws, int64_t ws_bytes,
+                      mmu_stream_t stream);
+
 /* ------------------------------------------------------------------ BertAdam
  * Fused multi-tensor BertAdam (pytorch_pretrained_bert 0.6.x, constructed at
  * train.py:142-147; stepped at src/framework.py:303): per-tensor clip

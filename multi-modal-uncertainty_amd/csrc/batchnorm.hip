@@ -1,0 +1,344 @@
+// BatchNorm2d (+ residual add) (+ ReLU) over channels-last bf16 activations (gfx950).
+//
+// The ResNet-152 image trunk (src/mmbt.py:19-21, torchvision Bottleneck) runs every
+// conv output through BatchNorm2d, most of them followed by ReLU and one per block by
+// the residual add + ReLU.  These kernels do that in as few passes over HBM as the math
+// allows, on the NHWC image [rows = N*H*W][C] the MIOpen convs produce:
+//   forward  (train): stats pass (read X)            -> per-block f32 sum / sum of squares
+//                     finalize (per channel, f64)    -> scale, shift, running stats, mean/invstd
+//                     apply pass (read X [+skip])    -> Y = act(X*scale + shift [+ skip])
+//   forward  (eval):  finalize from running stats    -> apply pass
+//   backward:         reduce pass (read dY, Y, X)    -> per-block sum(g), sum(g*(x-mean)), g = dY*[Y>0]
+//                     finalize                       -> dgamma, dbeta (accumulated), dx coefficients
+//                     apply pass (read dY, Y, X)     -> dX = k1*g + k2*x + k0  [, dSkip = g]
+// Semantics of torch.nn.BatchNorm2d in training mode: biased variance normalises, the
+// running variance is updated with the unbiased one, momentum-weighted.
+//
+// Work split: a block owns a chunk of CH <= 512 channels (grid.y) and a range of rows
+// (grid.x) sized to ~64 K elements; a thread owns 8 consecutive channels (16-B bf16
+// accesses, a row chunk is read as CH*2 contiguous bytes) of every rpi-th row.  Per-thread
+// f32 partials are reduced over the block in LDS and stored as one (sum, sum2) pair per
+// channel and block -- no atomics: ~1-3 K blocks x 2C float atomics on the same addresses
+// serialise in the L2 atomic units (measured 4-10x slower than the apply pass).  The
+// finalize sums the block partials per channel in f64 (8 slices per channel + LDS).
+#include "mmu_common.h"
+#include "mmu_internal.h"
+
+namespace mmu {
+
+constexpr int BN_THREADS = 256;
+constexpr int64_t BN_ELEMS_PER_BLOCK = 64 * 1024;
+constexpr int64_t BN_MAX_PART_ELEMS = 1 << 20;  // (block, channel) partial pairs: 8 MiB of scratch
+
+struct BnGeom {
+  int tpr, rpi, cg, rs, c0;  // threads per row, rows per iteration, channel group, row slot, first channel
+  int64_t r0, r1;            // the block's row range
+};
+static __device__ __forceinline__ BnGeom bn_geom(int CH, int64_t rows, int64_t rows_per_blk) {
+  BnGeom g;
+  g.tpr = CH >> 3;
+  g.rpi = BN_THREADS / g.tpr;
+  g.cg = threadIdx.x % g.tpr;
+  g.rs = threadIdx.x / g.tpr;
+  g.c0 = blockIdx.y * CH + 8 * g.cg;
+  g.r0 = (int64_t)blockIdx.x * rows_per_blk;
+  g.r1 = g.r0 + rows_per_blk < rows ? g.r0 + rows_per_blk : rows;
+  return g;
+}
+
+// per-thread (a[8], b[8]) partials -> block sums per channel -> part[blockIdx.x][c] = {a, b}
+static __device__ __forceinline__ void bn_block_reduce(const BnGeom& g, int C, const float (&a)[8],
+                                                       const float (&b)[8], float2* __restrict__ part) {
+  __shared__ float red[2][BN_THREADS * 8];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][t * 8 + e] = a[e]; red[1][t * 8 + e] = b[e]; }
+  __syncthreads();
+  if (t < g.tpr) {
+    float sa[8], sb[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sa[e] = 0.f; sb[e] = 0.f; }
+    for (int r = 0; r < g.rpi; ++r) {
+      const int o = (r * g.tpr + t) * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { sa[e] += red[0][o + e]; sb[e] += red[1][o + e]; }
+    }
+    float2* dst = part + (int64_t)blockIdx.x * C + g.c0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dst[e] = make_float2(sa[e], sb[e]);
+  }
+}
+
+// sum the nparts block partials of 16 channels per block: 8 slices x 32 (channel, component)
+// columns, f64, then LDS; returns true (and the two totals) in the thread that owns channel c
+static __device__ __forceinline__ bool bn_sum_parts(const float2* __restrict__ part, int nparts, int C, int& c,
+                                                    double& s1, double& s2) {
+  __shared__ double red[8][32];
+  const int t = threadIdx.x, col = t & 31, sl = t >> 5;
+  c = blockIdx.x * 16 + (col >> 1);
+  const int comp = col & 1;
+  double acc = 0.0;
+  if (c < C) {
+    const float* p = (const float*)part + 2 * (int64_t)c + comp;
+#pragma unroll 4
+    for (int k = sl; k < nparts; k += 8) acc += (double)p[(int64_t)k * 2 * C];
+  }
+  red[sl][col] = acc;
+  __syncthreads();
+  if (sl != 0 || comp != 0 || c >= C) return false;
+  s1 = 0.0;
+  s2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s1 += red[k][col]; s2 += red[k][col + 1]; }
+  return true;
+}
+
+__global__ __launch_bounds__(BN_THREADS) void bn_stats_kernel(const bf16* __restrict__ X, int64_t rows, int C, int CH,
+                                                               int64_t rows_per_blk, float2* __restrict__ part) {
+  const BnGeom g = bn_geom(CH, rows, rows_per_blk);
+  float s[8], q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s[e] = 0.f; q[e] = 0.f; }
+  if (g.rs < g.rpi) {
+#pragma unroll 4
+    for (int64_t r = g.r0 + g.rs; r < g.r1; r += g.rpi) {
+      const bf16x8 v = *(const bf16x8*)(X + r * C + g.c0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float f = bf2f(v[e]);
+        s[e] += f;
+        q[e] = fmaf(f, f, q[e]);
+      }
+    }
+  }
+  bn_block_reduce(g, C, s, q, part);
+}
+
+// per channel: coef = {scale, shift}; batch (partials) or running statistics
+__global__ __launch_bounds__(BN_THREADS) void bn_fwd_finalize_kernel(
+    const float2* __restrict__ part, int nparts, int64_t rows, int C, const float* w, const float* b, float* rmean,
+    float* rvar, int training, float momentum, float eps, float* smean, float* sinvstd, int64_t* nbt,
+    float* __restrict__ coef) {
+  int c;
+  double s1 = 0.0, s2 = 0.0;
+  if (training) {
+    if (!bn_sum_parts(part, nparts, C, c, s1, s2)) return;
+  } else {
+    const int t = threadIdx.x;
+    if (t >= 16) return;
+    c = blockIdx.x * 16 + t;
+    if (c >= C) return;
+  }
+  double mean, var;
+  if (training) {
+    mean = s1 / (double)rows;
+    var = s2 / (double)rows - mean * mean;
+    if (var < 0.0) var = 0.0;
+  } else {
+    mean = rmean[c];
+    var = rvar[c];
+  }
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float ww = w ? w[c] : 1.0f, bb = b ? b[c] : 0.0f;
+  const float scale = ww * invstd;
+  coef[c] = scale;
+  coef[C + c] = bb - (float)mean * scale;
+  if (training) {
+    if (smean) { smean[c] = (float)mean; sinvstd[c] = invstd; }
+    if (rmean) {
+      rmean[c] = (1.0f - momentum) * rmean[c] + momentum * (float)mean;
+      rvar[c] = (1.0f - momentum) * rvar[c] + momentum * (float)(var * (double)rows / (double)(rows - 1));
+    }
+    if (nbt && c == 0) *nbt += 1;
+  }
+}
+
+template <bool SKIP, bool RELU>
+__global__ __launch_bounds__(BN_THREADS) void bn_apply_kernel(const bf16* __restrict__ X, const bf16* __restrict__ S,
+                                                               bf16* __restrict__ Y, int64_t rows, int C, int CH,
+                                                               int64_t rows_per_blk, const float* __restrict__ coef) {
+  const BnGeom g = bn_geom(CH, rows, rows_per_blk);
+  if (g.rs >= g.rpi) return;
+  float sc[8], sh[8];
+  {
+    const float4 a0 = *(const float4*)(coef + g.c0), a1 = *(const float4*)(coef + g.c0 + 4);
+    const float4 b0 = *(const float4*)(coef + C + g.c0), b1 = *(const float4*)(coef + C + g.c0 + 4);
+    sc[0] = a0.x; sc[1] = a0.y; sc[2] = a0.z; sc[3] = a0.w; sc[4] = a1.x; sc[5] = a1.y; sc[6] = a1.z; sc[7] = a1.w;
+    sh[0] = b0.x; sh[1] = b0.y; sh[2] = b0.z; sh[3] = b0.w; sh[4] = b1.x; sh[5] = b1.y; sh[6] = b1.z; sh[7] = b1.w;
+  }
+#pragma unroll 4
+  for (int64_t r = g.r0 + g.rs; r < g.r1; r += g.rpi) {
+    const int64_t o = r * C + g.c0;
+    const bf16x8 x = *(const bf16x8*)(X + o);
+    bf16x8 sk;
+    if (SKIP) sk = *(const bf16x8*)(S + o);
+    bf16x8 y;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = fmaf(bf2f(x[e]), sc[e], sh[e]);
+      if (SKIP) v += bf2f(sk[e]);
+      if (RELU) v = fmaxf(v, 0.f);
+      y[e] = f2bf(v);
+    }
+    *(bf16x8*)(Y + o) = y;
+  }
+}
+
+// backward reduce: part = {sum g, sum g*(x-mean)},  g = dY * [Y > 0] (RELU)
+template <bool RELU>
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_reduce_kernel(const bf16* __restrict__ dY,
+                                                                    const bf16* __restrict__ Y,
+                                                                    const bf16* __restrict__ X, int64_t rows, int C,
+                                                                    int CH, int64_t rows_per_blk,
+                                                                    const float* __restrict__ smean,
+                                                                    float2* __restrict__ part) {
+  const BnGeom g = bn_geom(CH, rows, rows_per_blk);
+  float s[8], q[8], mu[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s[e] = 0.f; q[e] = 0.f; }
+  if (g.rs < g.rpi) {
+    const float4 m0 = *(const float4*)(smean + g.c0), m1 = *(const float4*)(smean + g.c0 + 4);
+    mu[0] = m0.x; mu[1] = m0.y; mu[2] = m0.z; mu[3] = m0.w; mu[4] = m1.x; mu[5] = m1.y; mu[6] = m1.z; mu[7] = m1.w;
+#pragma unroll 4
+    for (int64_t r = g.r0 + g.rs; r < g.r1; r += g.rpi) {
+      const int64_t o = r * C + g.c0;
+      const bf16x8 dy = *(const bf16x8*)(dY + o), x = *(const bf16x8*)(X + o);
+      bf16x8 y;
+      if (RELU) y = *(const bf16x8*)(Y + o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float gv = bf2f(dy[e]);
+        if (RELU && !(bf2f(y[e]) > 0.f)) gv = 0.f;
+        s[e] += gv;
+        q[e] = fmaf(gv, bf2f(x[e]) - mu[e], q[e]);
+      }
+    }
+  }
+  bn_block_reduce(g, C, s, q, part);
+}
+
+// coef = {k1, k2, k0}: dx = k1*g + k2*x + k0 ; dweight += dgamma, dbias += dbeta
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_finalize_kernel(const float2* __restrict__ part, int nparts,
+                                                                      int64_t rows, int C, const float* w,
+                                                                      const float* smean, const float* sinvstd,
+                                                                      float* dw, float* db, float* __restrict__ coef) {
+  int c;
+  double dbeta, sgx;
+  if (!bn_sum_parts(part, nparts, C, c, dbeta, sgx)) return;
+  const double invstd = sinvstd[c], mean = smean[c];
+  const double dgamma = sgx * invstd;
+  const double a = (w ? (double)w[c] : 1.0) * invstd;
+  const double n = (double)rows;
+  const double k2 = -a * invstd * dgamma / n;
+  coef[c] = (float)a;
+  coef[C + c] = (float)k2;
+  coef[2 * C + c] = (float)(-a * dbeta / n - k2 * mean);
+  if (dw) dw[c] += (float)dgamma;
+  if (db) db[c] += (float)dbeta;
+}
+
+template <bool RELU, bool DSKIP>
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_kernel(const bf16* __restrict__ dY,
+                                                                   const bf16* __restrict__ Y,
+                                                                   const bf16* __restrict__ X, int64_t rows, int C,
+                                                                   int CH, int64_t rows_per_blk,
+                                                                   const float* __restrict__ coef,
+                                                                   bf16* __restrict__ dX, bf16* __restrict__ dS) {
+  const BnGeom g = bn_geom(CH, rows, rows_per_blk);
+  if (g.rs >= g.rpi) return;
+  float k1[8], k2[8], k0[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    k1[e] = coef[g.c0 + e];
+    k2[e] = coef[C + g.c0 + e];
+    k0[e] = coef[2 * C + g.c0 + e];
+  }
+#pragma unroll 4
+  for (int64_t r = g.r0 + g.rs; r < g.r1; r += g.rpi) {
+    const int64_t o = r * C + g.c0;
+    const bf16x8 dy = *(const bf16x8*)(dY + o), x = *(const bf16x8*)(X + o);
+    bf16x8 y;
+    if (RELU) y = *(const bf16x8*)(Y + o);
+    bf16x8 dx, gs;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float gv = bf2f(dy[e]);
+      if (RELU && !(bf2f(y[e]) > 0.f)) gv = 0.f;
+      dx[e] = f2bf(fmaf(k1[e], gv, fmaf(k2[e], bf2f(x[e]), k0[e])));
+      gs[e] = f2bf(gv);
+    }
+    *(bf16x8*)(dX + o) = dx;
+    if (DSKIP) *(bf16x8*)(dS + o) = gs;
+  }
+}
+
+// ------------------------------------------------------------------------------ launchers
+struct BnGrid {
+  int CH;
+  int64_t rpb;
+  dim3 grid;
+};
+// channel chunk: the largest of 512, 256, ..., 8 dividing C; rows per block ~64 K elements,
+// a multiple of the rows per iteration, and few enough row blocks that blocks x C partial
+// pairs fit BN_MAX_PART_ELEMS
+static BnGrid bn_grid(int64_t rows, int C) {
+  BnGrid g;
+  g.CH = 512;
+  while (C % g.CH) g.CH >>= 1;
+  const int rpi = BN_THREADS / (g.CH / 8);
+  int64_t rpb = BN_ELEMS_PER_BLOCK / g.CH;
+  rpb = (rpb + rpi - 1) / rpi * rpi;
+  const int64_t max_parts = BN_MAX_PART_ELEMS / C;
+  if ((rows + rpb - 1) / rpb > max_parts) rpb = ((rows + max_parts - 1) / max_parts + rpi - 1) / rpi * rpi;
+  g.rpb = rpb;
+  g.grid = dim3((unsigned)((rows + rpb - 1) / rpb), (unsigned)(C / g.CH));
+  return g;
+}
+
+int64_t batchnorm_ws_bytes(int64_t C) { return BN_MAX_PART_ELEMS * 8 + ((3 * C + 3) & ~3) * 4; }
+
+void batchnorm_fwd_launch(const BnFwdParams& q, hipStream_t s) {
+  const BnGrid G = bn_grid(q.rows, q.C);
+  const int nparts = (int)G.grid.x;
+  float* coef = (float*)q.ws;
+  float2* part = (float2*)(coef + ((3 * q.C + 3) & ~3));
+  if (q.training)
+    hipLaunchKernelGGL(bn_stats_kernel, G.grid, dim3(BN_THREADS), 0, s, q.X, q.rows, q.C, G.CH, G.rpb, part);
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((q.C + 15) / 16), dim3(BN_THREADS), 0, s, part, nparts, q.rows, q.C,
+                     q.w, q.b, q.rmean, q.rvar, q.training, q.momentum, q.eps, q.smean, q.sinvstd, q.nbt, coef);
+  const bool sk = q.skip != nullptr;
+#define BN_APPLY(SK, RL)                                                                                    \
+  hipLaunchKernelGGL((bn_apply_kernel<SK, RL>), G.grid, dim3(BN_THREADS), 0, s, q.X, q.skip, q.Y, q.rows, q.C, \
+                     G.CH, G.rpb, coef)
+  if (sk && q.relu) BN_APPLY(true, true);
+  else if (sk) BN_APPLY(true, false);
+  else if (q.relu) BN_APPLY(false, true);
+  else BN_APPLY(false, false);
+#undef BN_APPLY
+}
+
+void batchnorm_bwd_launch(const BnBwdParams& q, hipStream_t s) {
+  const BnGrid G = bn_grid(q.rows, q.C);
+  const int nparts = (int)G.grid.x;
+  float* coef = (float*)q.ws;
+  float2* part = (float2*)(coef + ((3 * q.C + 3) & ~3));
+  if (q.relu)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true>), G.grid, dim3(BN_THREADS), 0, s, q.dY, q.Y, q.X, q.rows, q.C, G.CH,
+                       G.rpb, q.smean, part);
+  else
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false>), G.grid, dim3(BN_THREADS), 0, s, q.dY, q.Y, q.X, q.rows, q.C,
+                       G.CH, G.rpb, q.smean, part);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((q.C + 15) / 16), dim3(BN_THREADS), 0, s, part, nparts, q.rows, q.C,
+                     q.w, q.smean, q.sinvstd, q.dw, q.db, coef);
+  const bool ds = q.dS != nullptr;
+#define BN_BAPPLY(RL, DS)                                                                                     \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<RL, DS>), G.grid, dim3(BN_THREADS), 0, s, q.dY, q.Y, q.X, q.rows, q.C, \
+                     G.CH, G.rpb, coef, q.dX, q.dS)
+  if (q.relu && ds) BN_BAPPLY(true, true);
+  else if (q.relu) BN_BAPPLY(true, false);
+  else if (ds) BN_BAPPLY(false, true);
+  else BN_BAPPLY(false, false);
+#undef BN_BAPPLY
+}
+
+}  // namespace mmu

@@ -294,6 +294,50 @@ int mmu_row_pool_bwd(const float* dout, int64_t B, int64_t Hh, int64_t Ww, int64
   return check_launch("mmu_row_pool_bwd");
 }
 
+int64_t mmu_batchnorm_ws_bytes(int64_t C) { return batchnorm_ws_bytes(C); }
+
+static int bn_common(int64_t rows, int64_t C, void* ws, int64_t ws_bytes, const char* who) {
+  if (rows <= 0 || C <= 0 || C % 8 || C > 2048) return fail("%s: C=%ld must be a multiple of 8, <= 2048", who, C);
+  if (!ws || ws_bytes < batchnorm_ws_bytes(C) || ((uintptr_t)ws & 15))
+    return fail("%s: ws must be >= mmu_batchnorm_ws_bytes(C) bytes, 16-B aligned", who);
+  return 0;
+}
+
+int mmu_batchnorm_fwd(const void* X, const void* skip, void* Y, int64_t rows, int64_t C, const float* weight,
+                      const float* bias, float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                      int training, float momentum, float eps, int relu, float* save_mean, float* save_invstd,
+                      void* ws, int64_t ws_bytes, mmu_stream_t stream) {
+  if (!X || !Y) return fail("mmu_batchnorm_fwd: null pointer");
+  if (bn_common(rows, C, ws, ws_bytes, "mmu_batchnorm_fwd")) return 1;
+  if ((running_mean == nullptr) != (running_var == nullptr))
+    return fail("mmu_batchnorm_fwd: running_mean / running_var must both be given or NULL");
+  if ((save_mean == nullptr) != (save_invstd == nullptr))
+    return fail("mmu_batchnorm_fwd: save_mean / save_invstd must both be given or NULL");
+  if (training && rows < 2) return fail("mmu_batchnorm_fwd: training needs more than 1 value per channel");
+  if (!training && !running_mean) return fail("mmu_batchnorm_fwd: eval needs running statistics");
+  BnFwdParams q{};
+  q.X = (const bf16*)X; q.skip = (const bf16*)skip; q.Y = (bf16*)Y; q.rows = rows; q.C = (int)C;
+  q.w = weight; q.b = bias; q.rmean = running_mean; q.rvar = running_var; q.nbt = num_batches_tracked;
+  q.training = training; q.relu = relu; q.momentum = momentum; q.eps = eps;
+  q.smean = save_mean; q.sinvstd = save_invstd; q.ws = ws;
+  batchnorm_fwd_launch(q, (hipStream_t)stream);
+  return check_launch("mmu_batchnorm_fwd");
+}
+
+int mmu_batchnorm_bwd(const void* dY, const void* Y, const void* X, int64_t rows, int64_t C, const float* weight,
+                      const float* save_mean, const float* save_invstd, int relu, void* dX, void* dSkip,
+                      float* dweight, float* dbias, void* ws, int64_t ws_bytes, mmu_stream_t stream) {
+  if (!dY || !X || !dX || !save_mean || !save_invstd) return fail("mmu_batchnorm_bwd: null pointer");
+  if (relu && !Y) return fail("mmu_batchnorm_bwd: relu needs the forward output Y");
+  if (bn_common(rows, C, ws, ws_bytes, "mmu_batchnorm_bwd")) return 1;
+  BnBwdParams q{};
+  q.dY = (const bf16*)dY; q.Y = (const bf16*)Y; q.X = (const bf16*)X; q.rows = rows; q.C = (int)C; q.w = weight;
+  q.smean = save_mean; q.sinvstd = save_invstd; q.relu = relu; q.dX = (bf16*)dX; q.dS = (bf16*)dSkip;
+  q.dw = dweight; q.db = dbias; q.ws = ws;
+  batchnorm_bwd_launch(q, (hipStream_t)stream);
+  return check_launch("mmu_batchnorm_bwd");
+}
+
 int mmu_bertadam_step(float* params, const float* grads, float* m, float* v, void* bf16_copy, const int64_t* table,
                       int32_t* steps, int64_t n_tensors, int64_t n_chunks, float lr_decay, float lr_nodecay, float wd,
                       float warmup, float t_total, float b1, float b2, float eps, float max_grad_norm, float* ws,

@@ -102,6 +102,33 @@ struct AdamParams {
 };
 int bertadam_launch(const AdamParams& p, hipStream_t s, const char** err);
 
+struct BnFwdParams {
+  const bf16 *X, *skip;
+  bf16* Y;
+  int64_t rows;
+  int C;
+  const float *w, *b;
+  float *rmean, *rvar;
+  int training, relu;
+  float momentum, eps;
+  float *smean, *sinvstd;
+  int64_t* nbt;
+  void* ws;
+};
+void batchnorm_fwd_launch(const BnFwdParams& q, hipStream_t s);
+struct BnBwdParams {
+  const bf16 *dY, *Y, *X;
+  int64_t rows;
+  int C;
+  const float *w, *smean, *sinvstd;
+  int relu;
+  bf16 *dX, *dS;
+  float *dw, *db;
+  void* ws;
+};
+void batchnorm_bwd_launch(const BnBwdParams& q, hipStream_t s);
+int64_t batchnorm_ws_bytes(int64_t C);
+
 void uncertainty_launch(const float* logits, const int64_t* y, int64_t S, int64_t R, int64_t C, float* p_bar,
                         float* nll, float* conf, float* correct, hipStream_t s);
 void ece_bins_launch(const float* conf, const float* correct, int64_t S, int64_t n_bins, float* out, hipStream_t s);

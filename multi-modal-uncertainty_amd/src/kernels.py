@@ -180,6 +180,41 @@ def row_pool_bwd(dout, n, dfmap_nhwc):
     N.call("mmu_row_pool_bwd", _ptr(dout), B, Hh, Ww, C, n, _ptr(dfmap_nhwc), _stream(dout))
 
 
+_bn_ws = {}
+
+
+def _bn_workspace(dev):
+    """per-device scratch for mmu_batchnorm_*, reused stream-ordered by every call"""
+    t = _bn_ws.get(dev)
+    if t is None:
+        nbytes = N.load().mmu_batchnorm_ws_bytes(2048)
+        t = _bn_ws[dev] = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
+    return t
+
+
+def batchnorm_fwd(X, Y, weight, bias, running_mean, running_var, training, momentum, eps, relu=False, skip=None,
+                  num_batches_tracked=None, save_mean=None, save_invstd=None):
+    """X, Y, skip: channels-last bf16 [N, C, H, W] (contiguous as [N*H*W, C])."""
+    _dev_check(X, Y)
+    _want(X, torch.bfloat16, "batchnorm X")
+    C = X.shape[1]
+    rows = X.numel() // C
+    ws = _bn_workspace(X.device)
+    N.call("mmu_batchnorm_fwd", _ptr(X), _ptr(skip), _ptr(Y), rows, C, _ptr(weight), _ptr(bias), _ptr(running_mean),
+           _ptr(running_var), _ptr(num_batches_tracked), int(bool(training)), float(momentum), float(eps),
+           int(bool(relu)), _ptr(save_mean), _ptr(save_invstd), _ptr(ws), ws.numel() * 4, _stream(X))
+
+
+def batchnorm_bwd(dY, Y, X, weight, save_mean, save_invstd, relu, dX, dSkip=None, dweight=None, dbias=None):
+    _dev_check(dY, X, dX)
+    C = X.shape[1]
+    rows = X.numel() // C
+    ws = _bn_workspace(X.device)
+    N.call("mmu_batchnorm_bwd", _ptr(dY), _ptr(Y), _ptr(X), rows, C, _ptr(weight), _ptr(save_mean),
+           _ptr(save_invstd), int(bool(relu)), _ptr(dX), _ptr(dSkip), _ptr(dweight), _ptr(dbias), _ptr(ws),
+           ws.numel() * 4, _stream(X))
+
+
 def bertadam_step(params, grads, m, v, bf16_copy, table, steps, n_tensors, n_chunks, lr_decay, lr_nodecay, wd,
                   warmup, t_total, b1, b2, eps, max_grad_norm, ws):
     _dev_check(params, grads, m, v, table, steps, ws)

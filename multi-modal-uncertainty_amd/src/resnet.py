@@ -4,31 +4,96 @@ Child order and parameter names follow torchvision's resnet152 so that
 ``ImageEncoder.model = Sequential(children[:-2])`` yields the reference keys
 ``enc.img_encoder.model.{0..7}.*``.  No pretrained weights exist offline: weights
 use torchvision's default init (He-normal fan_out convs, BN gamma 1 / beta 0).
-On MI355X the trunk runs through MIOpen in bf16, channels-last (ImageEncoder).
+On MI355X the trunk's convs run through MIOpen in bf16, channels-last (ImageEncoder), and
+every BatchNorm2d [+ residual] [+ ReLU] through mmu_batchnorm_fwd/bwd.
 """
 import torch
 import torch.nn as nn
 
+from . import kernels as K
+
+
+class _BatchNormAct(torch.autograd.Function):
+    """Training-mode BatchNorm2d [+ residual] [+ ReLU] on channels-last bf16 via
+    mmu_batchnorm_fwd / mmu_batchnorm_bwd (batch statistics, running stats updated)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, skip, bn, relu):
+        ctx.bias_ref = bias
+        Y = torch.empty_like(x)
+        C = x.shape[1]
+        smean = torch.empty(C, dtype=torch.float32, device=x.device)
+        sinv = torch.empty_like(smean)
+        K.batchnorm_fwd(x, Y, weight, bias, bn.running_mean, bn.running_var, True, bn.momentum, bn.eps, relu=relu,
+                        skip=skip, num_batches_tracked=bn.num_batches_tracked, save_mean=smean, save_invstd=sinv)
+        ctx.save_for_backward(x, Y, weight, smean, sinv)
+        ctx.relu, ctx.has_skip = relu, skip is not None
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        x, Y, weight, smean, sinv = ctx.saved_tensors
+        dY = dY.contiguous(memory_format=torch.channels_last)
+        dX = torch.empty_like(x)
+        dS = torch.empty_like(x) if ctx.has_skip and ctx.needs_input_grad[3] else None
+        want_w, want_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        # straight into the flat gradient store when it exists (no AccumulateGrad pass)
+        dw = (weight.grad if weight.grad is not None else torch.zeros_like(weight)) if want_w else None
+        db = None
+        if want_b:
+            bias = ctx.bias_ref
+            db = bias.grad if bias.grad is not None else torch.zeros_like(bias)
+        K.batchnorm_bwd(dY, Y if ctx.relu else None, x, weight, smean, sinv, ctx.relu, dX, dS, dw, db)
+        rw = dw if (want_w and weight.grad is None) else None
+        rb = db if (want_b and ctx.bias_ref.grad is None) else None
+        return dX, rw, rb, dS, None, None
+
 
 class BatchNorm2d(nn.BatchNorm2d):
-    """BatchNorm2d with two MI355X-specific forms (state_dict / semantics unchanged):
-    * inference: a per-channel affine y = x * s + t (s = w / sqrt(var + eps),
-      t = b - mean * s) in the activation dtype -- one elementwise pass;
-    * training: MIOpen's batch-statistics kernels for real batches, PyTorch's native
-      NHWC kernels below MIOPEN_MIN_BATCH images.
-    On this ROCm 7.2 stack MIOpen's bf16 NHWC batch-norm crashes in host code for tiny
-    batches (B=2 in training; inference), while the native kernels are ~2x slower at
-    B=256 (DESIGN.md, "ResNet trunk")."""
+    """BatchNorm2d with the activation fused in (state_dict / semantics of torch's).
+    ``forward(x, skip=None, relu=None)`` computes act(BN(x) [+ skip]); ``relu`` defaults
+    to the module's ``fused_relu`` (set for the stem BN, whose ReLU module is then a
+    FusedReLU no-op).  bf16 channels-last inputs on the GPU run the HIP kernels
+    (training: batch statistics; eval: running statistics, one elementwise pass);
+    anything else (fp32 parity runs) uses PyTorch's batch_norm."""
 
+    fused_relu = False
     MIOPEN_MIN_BATCH = 8
 
-    def forward(self, x):
+    def forward(self, x, skip=None, relu=None):
+        relu = self.fused_relu if relu is None else relu
+        hip = (x.is_cuda and x.dtype == torch.bfloat16 and (skip is None or skip.dtype == torch.bfloat16)
+               and x.shape[1] % 8 == 0)
+        if hip:
+            x = x.contiguous(memory_format=torch.channels_last)
+            if skip is not None:
+                skip = skip.contiguous(memory_format=torch.channels_last)
+            if self.training and self.track_running_stats:
+                return _BatchNormAct.apply(x, self.weight, self.bias, skip, self, relu)
+            if not self.training:
+                Y = torch.empty_like(x)
+                K.batchnorm_fwd(x, Y, self.weight, self.bias, self.running_mean, self.running_var, False,
+                                self.momentum, self.eps, relu=relu, skip=skip)
+                return Y
         if self.training or not self.track_running_stats:
+            # MIOpen's NHWC batch-norm crashes in host code for tiny batches on this stack
             with torch.backends.cudnn.flags(enabled=x.shape[0] >= self.MIOPEN_MIN_BATCH):
-                return super().forward(x)
-        s = self.weight * (self.running_var + self.eps).rsqrt()
-        t = self.bias - self.running_mean * s
-        return x * s.view(1, -1, 1, 1).to(x.dtype) + t.view(1, -1, 1, 1).to(x.dtype)
+                y = super().forward(x)
+        else:  # inference as one per-channel affine pass
+            s = self.weight * (self.running_var + self.eps).rsqrt()
+            t = self.bias - self.running_mean * s
+            y = x * s.view(1, -1, 1, 1).to(x.dtype) + t.view(1, -1, 1, 1).to(x.dtype)
+        if skip is not None:
+            y = y + skip
+        return torch.relu(y) if relu else y
+
+
+class FusedReLU(nn.ReLU):
+    """The stem's ReLU slot (torchvision child index 2): the preceding BatchNorm2d
+    already applied it, so this is the identity."""
+
+    def forward(self, x):
+        return x
 
 
 class Bottleneck(nn.Module):
@@ -48,14 +113,16 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         skip = x if self.downsample is None else self.downsample(x)
-        y = self.relu(self.bn1(self.conv1(x)))
-        y = self.relu(self.bn2(self.conv2(y)))
-        return self.relu(self.bn3(self.conv3(y)) + skip)
+        y = self.bn1(self.conv1(x), relu=True)
+        y = self.bn2(self.conv2(y), relu=True)
+        return self.bn3(self.conv3(y), skip=skip, relu=True)
 
 
 def resnet152_trunk(blocks=(3, 8, 36, 3)):
     """Sequential(conv1, bn1, relu, maxpool, layer1..layer4) -> [B,2048,H/32,W/32]."""
-    mods = [nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False), BatchNorm2d(64), nn.ReLU(inplace=True),
+    stem_bn = BatchNorm2d(64)
+    stem_bn.fused_relu = True
+    mods = [nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False), stem_bn, FusedReLU(inplace=True),
             nn.MaxPool2d(3, 2, 1)]
     cin = 64
     for i, (width, n) in enumerate(zip((64, 128, 256, 512), blocks)):

@@ -415,3 +415,95 @@ def test_uncertainty_nll_ece(dev):
     bb = bins.view(15, 3).cpu().double().numpy()
     ece = float((np.abs(bb[:, 2] - bb[:, 1]) / S).sum())
     assert abs(ece - U.ece(pr, y.numpy())) < 1e-4
+
+
+# ------------------------------------------------------------------ BatchNorm (+ residual) (+ ReLU)
+def _bn_ref(x, w, b, skip, relu, eps=1e-5):
+    """f32 torch reference of training-mode BN [+ skip] [+ ReLU] on the same bf16 inputs"""
+    y = torch.nn.functional.batch_norm(x, None, None, w, b, training=True, eps=eps)
+    if skip is not None:
+        y = y + skip
+    return torch.relu(y) if relu else y
+
+
+@pytest.mark.parametrize("N,C,H,W,skip,relu", [(4, 64, 9, 7, False, True), (3, 256, 5, 5, True, True),
+                                               (2, 2048, 3, 3, False, False), (5, 96, 4, 3, True, False)])
+def test_batchnorm_train_fwd_bwd(dev, N, C, H, W, skip, relu):
+    k = K()
+    g = torch.Generator(device=dev).manual_seed(C + H)
+    cl = torch.channels_last
+    x = (torch.randn(N, C, H, W, generator=g, device=dev) * 2 + 0.7).to(torch.bfloat16).contiguous(memory_format=cl)
+    s = (torch.randn(N, C, H, W, generator=g, device=dev)).to(torch.bfloat16).contiguous(memory_format=cl) if skip else None
+    w = torch.rand(C, generator=g, device=dev) + 0.5
+    b = torch.randn(C, generator=g, device=dev) * 0.1
+    rm, rv = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
+    rm0, rv0 = rm.clone(), rv.clone()
+    nbt = torch.zeros((), dtype=torch.int64, device=dev)
+    Y = torch.empty_like(x)
+    sm, si = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    k.batchnorm_fwd(x, Y, w, b, rm, rv, True, 0.1, 1e-5, relu=relu, skip=s, num_batches_tracked=nbt,
+                    save_mean=sm, save_invstd=si)
+    xf = x.float().requires_grad_(True)
+    wf, bf_ = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    sf = s.float().requires_grad_(True) if skip else None
+    ref = _bn_ref(xf, wf, bf_, sf, relu)
+    close(Y, ref.detach(), atol_frac=1e-2)
+    n = N * H * W
+    mu = x.float().mean((0, 2, 3))
+    var = x.float().var((0, 2, 3), unbiased=False)
+    torch.testing.assert_close(sm, mu, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(si, (var + 1e-5).rsqrt(), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rm, 0.9 * rm0 + 0.1 * mu, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rv, 0.9 * rv0 + 0.1 * var * n / (n - 1), rtol=1e-5, atol=1e-6)
+    assert int(nbt) == 1
+    # backward: the mask comes from the kernel's own output, the reference uses its own
+    dY = torch.randn(N, C, H, W, generator=g, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    dX = torch.empty_like(x)
+    dS = torch.empty_like(x) if skip else None
+    dw = torch.full((C,), 0.25, device=dev)  # accumulated into
+    db = torch.full((C,), -0.5, device=dev)
+    k.batchnorm_bwd(dY, Y if relu else None, x, w, sm, si, relu, dX, dS, dw, db)
+    grads = torch.autograd.grad(ref, [xf, wf, bf_] + ([sf] if skip else []), dY.float())
+    close(dX, grads[0], atol_frac=2e-2)
+    torch.testing.assert_close(dw - 0.25, grads[1], rtol=2e-2, atol=2e-2 * grads[1].abs().max().item() + 1e-3)
+    torch.testing.assert_close(db + 0.5, grads[2], rtol=2e-2, atol=2e-2 * grads[2].abs().max().item() + 1e-3)
+    if skip:
+        close(dS, grads[3], atol_frac=1e-2)
+
+
+def test_batchnorm_eval_and_module(dev):
+    """the module path (train, then eval from the updated running statistics) against
+    torch.nn.BatchNorm2d in f32 on the same bf16 inputs, with the fused residual + ReLU"""
+    from src.resnet import BatchNorm2d
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(3)
+    C = 128
+    bn = BatchNorm2d(C).to(dev)
+    ref = torch.nn.BatchNorm2d(C).to(dev)
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C, generator=g, device=dev) + 0.5)
+        bn.bias.copy_(torch.randn(C, generator=g, device=dev))
+        ref.load_state_dict(bn.state_dict())
+    x = (torch.randn(6, C, 7, 7, generator=g, device=dev) * 3 - 1).to(torch.bfloat16).contiguous(memory_format=cl)
+    sk = torch.randn(6, C, 7, 7, generator=g, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    for _ in range(2):  # two training steps: running stats and num_batches_tracked follow torch
+        y = bn(x, skip=sk, relu=True)
+        yr = torch.relu(ref(x.float()) + sk.float())
+        close(y, yr.detach(), atol_frac=1e-2)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(bn.running_var, ref.running_var, rtol=1e-4, atol=1e-5)
+    assert int(bn.num_batches_tracked) == int(ref.num_batches_tracked) == 2
+    bn.eval()
+    ref.eval()
+    close(bn(x, relu=False), ref(x.float()).detach(), atol_frac=1e-2)
+    # autograd through the module: weight / bias grads land in .grad
+    bn.train()
+    ref.train()
+    xr = x.float().requires_grad_(True)
+    xb = x.clone().requires_grad_(True)
+    y = bn(xb, relu=True)
+    y.float().pow(2).sum().backward()
+    torch.relu(ref(xr)).pow(2).sum().backward()
+    close(xb.grad, xr.grad, atol_frac=3e-2)
+    torch.testing.assert_close(bn.weight.grad, ref.weight.grad, rtol=3e-2, atol=3e-2 * ref.weight.grad.abs().max().item())
+    torch.testing.assert_close(bn.bias.grad, ref.bias.grad, rtol=3e-2, atol=3e-2 * ref.bias.grad.abs().max().item())

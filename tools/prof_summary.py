@@ -17,6 +17,7 @@ CATS = [
     ("mmu LayerNorm", r"mmu::ln_|ln_fwd_kernel|ln_bwd_kernel"),
     ("mmu embed / pool", r"mmu::embed|mmu::row_pool|embed_fwd_kernel|embed_bwd"),
     ("mmu BertAdam", r"mmu::adam"),
+    ("mmu BatchNorm (ResNet)", r"mmu::bn_|bn_(stats|apply|bwd)"),
     ("mmu colsum", r"mmu::colsum"),
     ("ResNet conv (MIOpen / CK)", r"conv|igemm|gtcx|ck::tensor_operation"),
     ("ResNet batch-norm (MIOpen)", r"BatchNorm"),
