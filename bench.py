@@ -106,6 +106,8 @@ def main():
     from src import kernels as K
     from src.dp import GradBucketer, broadcast_parameters
 
+    # MIOpen solver search for the ResNet convs (first warm-up step pays it) when asked
+    torch.backends.cudnn.benchmark = os.environ.get("MMU_MIOPEN_FIND", "0") == "1"
     torch.manual_seed(1234)
     margs = make_args()
     model = MultimodalBertClf(margs).to(dev)

@@ -103,7 +103,7 @@ struct TileLoader {
 
 // =============================================================================== forward
 // grid (ceil(L/128), batch*heads), 256 threads; wave w owns queries [blk*128 + 32w, +32)
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_fwd_kernel(AttnParams p) {
   constexpr int KV = 64, TILE = KV * 128;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE + 2 * KV * 4];
   float* maskL = (float*)(smem + 4 * TILE);
@@ -173,13 +173,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
         }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mnew = fmaxf(m_run, mx);
-      const float alpha = m_run == NEG_INF ? 0.f : exp2f(m_run - mnew);
+      const float alpha = m_run == NEG_INF ? 0.f : __builtin_amdgcn_exp2f(m_run - mnew);
       float rs = 0.f;
 #pragma unroll
       for (int st = 0; st < 2; ++st)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float e = exp2f(sc[st][r] - mnew);
+          float e = __builtin_amdgcn_exp2f(sc[st][r] - mnew);
           sc[st][r] = e;
           rs += e;
         }
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AttnParams p) {
 }
 
 // dQ: grid (ceil(L/128), batch*heads), 256 threads, wave owns 32 queries; loops over 64-key tiles
-__global__ __launch_bounds__(256) void attn_dq_kernel(AttnParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_dq_kernel(AttnParams p) {
   constexpr int KV = 64, TILE = KV * 128;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE + 2 * KV * 4];
   float* maskL = (float*)(smem + 4 * TILE);
@@ -288,8 +288,11 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnParams p) {
     uint4 v = qv ? *(const uint4*)(dob + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
     df[ks] = *(bf16x8*)&v;
   }
-  const float lse2 = qv ? p.lse[(int64_t)bh * L + q] * LOG2E : __builtin_huge_valf();
+  // row constants as the accumulators' initial values: S - lse and dP - delta/zs, so that
+  // p = exp2(log2e (S - lse) + mask) and dS = p (keep ? (dP - delta/zs) zs : -delta)
+  const float nlse = qv ? -p.lse[(int64_t)bh * L + q] : -__builtin_huge_valf();
   const float dlt = qv ? p.delta[(int64_t)bh * L + q] : 0.f;
+  const float ndz = -dlt / zs;
   f32x16 dq[2];
 #pragma unroll
   for (int i = 0; i < 16; ++i) { dq[0][i] = 0.f; dq[1][i] = 0.f; }
@@ -325,9 +328,10 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnParams p) {
       const uint64_t kwh = kw >> (4 * h);
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
+        const uint32_t kw32 = (uint32_t)(kwh >> (32 * st));
         f32x16 sc, dp;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) { sc[i] = 0.f; dp[i] = 0.f; }
+        for (int i = 0; i < 16; ++i) { sc[i] = nlse; dp[i] = ndz; }
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ks, 32 * st, ks, l), qf[ks], sc, 0, 0, 0);
@@ -338,10 +342,10 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnParams p) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int r = 4 * g + e;
-            const int kc = 32 * st + (r & 3) + 8 * (r >> 2), kl = kc + 4 * h;
-            float pr = exp2f(sc[r] * LOG2E + mk[kl] - lse2);
-            float dpv = ((kwh >> kc) & 1) ? dp[r] * zs : 0.f;
-            sc[r] = pr * (dpv - dlt);  // dS^T
+            const int kc = (r & 3) + 8 * (r >> 2), kl = 32 * st + kc + 4 * h;
+            const float pr = __builtin_amdgcn_exp2f(fmaf(sc[r], LOG2E, mk[kl]));
+            const float v = (kw32 & (1u << kc)) ? dp[r] * zs : -dlt;
+            sc[r] = pr * v;  // dS^T
           }
         }
 #pragma unroll
@@ -378,7 +382,7 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnParams p) {
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void attn_dkdv_kernel(AttnParams p) {
   constexpr int QT = 32, TILE = QT * 128;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE + 2 * 2 * QT * 4 + 2 * QT * 8];
-  float* rowL = (float*)(smem + 4 * TILE);  // [stage][2][QT]: lse2, delta
+  float* rowL = (float*)(smem + 4 * TILE);  // [stage][2][QT]: -lse, delta
   uint64_t* rowK = (uint64_t*)(rowL + 4 * QT);  // [stage][QT]: keep bits of this block's 64 keys
   const int t = threadIdx.x, l = t & 63, w = t >> 6, h = l >> 5;
   const int bh = blockIdx.y, b = bh / p.heads, hd = bh - b * p.heads;
@@ -408,7 +412,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
   const int nq = (L + QT - 1) / QT;
   auto load_rows = [&](int i0, float& a, float& c, uint64_t& k) {
     int qq = i0 + (t & 31);
-    a = qq < L ? p.lse[(int64_t)bh * L + qq] * LOG2E : __builtin_huge_valf();
+    a = qq < L ? -p.lse[(int64_t)bh * L + qq] : -__builtin_huge_valf();
     c = qq < L ? p.delta[(int64_t)bh * L + qq] : 0.f;
     k = (drop && qq < L) ? p.dropmask[((int64_t)bh * L + qq) * nkv + blockIdx.x] : ~0ull;
   };
@@ -425,8 +429,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
     const int stg = i & 1;
     const char* Qs = smem + stg * 2 * TILE;
     const char* Ds = Qs + TILE;
-    const float* lse2 = rowL + stg * 2 * QT;
-    const float* dlt = lse2 + QT;
+    const float* nlse = rowL + stg * 2 * QT;
+    const float* dlt = nlse + QT;
     const uint32_t* kbit = (const uint32_t*)(rowK + stg * QT);  // [QT][2] halves: this wave's keys = half w
     const bool more = i + 1 < nq;
     if (more) {
@@ -435,9 +439,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
       load_rows((i + 1) * QT, ra, rc, rk);
     }
     if (wave_live) {
-      f32x16 sc, dp;
+      f32x16 sc, dp;  // S starts at -lse of its query row (row constant as initial accumulator)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { sc[r] = 0.f; dp[r] = 0.f; }
+      for (int r = 0; r < 16; ++r) { sc[r] = nlse[(r & 3) + 8 * (r >> 2) + 4 * h]; dp[r] = 0.f; }
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Qs, 0, ks, l), kf[ks], sc, 0, 0, 0);
@@ -447,7 +451,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int ql = (r & 3) + 8 * (r >> 2) + 4 * h;
-        float pr = exp2f(sc[r] * LOG2E + mkey - lse2[ql]);
+        float pr = __builtin_amdgcn_exp2f(fmaf(sc[r], LOG2E, mkey));
         float z = ((kbit[2 * ql + w] >> (l & 31)) & 1u) ? zs : 0.f;
         pz[r] = pr * z;
         sc[r] = pr * (dp[r] * z - dlt[ql]);  // dS

@@ -7,6 +7,7 @@
 #include <string>
 #include <vector>
 #include "mmu_internal.h"
+#include <cstdlib>
 
 using namespace mmu;
 
@@ -100,7 +101,9 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
   // 32-bit buffer offsets of those out-of-range reads never wrap back into the operand)
   const int64_t a_span = 2 * (a_kmajor ? (M + 256) * lda : (K + 64) * lda);
   const int64_t b_span = 2 * (b_kmajor ? (N + 256) * ldb : (K + 64) * ldb);
-  const bool big = M >= 256 && N >= 256 && a_span < (1ll << 32) - 4096 && b_span < (1ll << 32) - 4096;
+  const char* force_small = getenv("MMU_GEMM_SMALL");  // A/B experiments: 1 = always the 128x128 kernel
+  const bool big = M >= 256 && N >= 256 && a_span < (1ll << 32) - 4096 && b_span < (1ll << 32) - 4096 &&
+                   !(force_small && force_small[0] == '1');
   const int tile = big ? 256 : 128;
   p.tiles_m = (int)((M + tile - 1) / tile);
   p.tiles_n = (int)((N + tile - 1) / tile);

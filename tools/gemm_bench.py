@@ -34,6 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=256 * 513)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--var", default="MMU_GEMM_PIPE", help="env switch of the variant compared (=1) to default (=0)")
     a = ap.parse_args()
     M, dev, bf = a.rows, "cuda", torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
@@ -87,17 +88,17 @@ def main():
                         epi=K.epilogue(K.EPI_STORE, accumulate=True)),
          lambda: torch.matmul(dZ.t(), A)),
     ]
-    print(f"{'gemm':26s} {'M':>7s} {'N':>5s} {'K':>7s} {'pipe ms':>8s} {'TF/s':>7s} {'2stg ms':>8s} {'TF/s':>7s}"
+    print(f"{'gemm':26s} {'M':>7s} {'N':>5s} {'K':>7s} {'var ms':>8s} {'TF/s':>7s} {'dflt ms':>8s} {'TF/s':>7s}"
           f" {'blasLt ms':>9s} {'TF/s':>7s}")
     for name, m, n, k, f_mmu, f_ref in cases:
         fl = 2.0 * m * n * k
         t0, t1 = float("inf"), float("inf")
-        for _ in range(3):  # interleaved A/B rounds in one process
-            os.environ["MMU_GEMM_PIPE"] = "1"
+        for _ in range(3):  # interleaved A/B rounds in one process: variant (env) vs default
+            os.environ[a.var] = "1"
             t0 = min(t0, timed(f_mmu, a.iters))
-            os.environ["MMU_GEMM_PIPE"] = "0"
+            os.environ[a.var] = "0"
             t1 = min(t1, timed(f_mmu, a.iters))
-        os.environ["MMU_GEMM_PIPE"] = "1"
+        os.environ[a.var] = "0"
         t2 = timed(f_ref, a.iters)
         print(f"{name:26s} {m:7d} {n:5d} {k:7d} {t0:8.3f} {fl / t0 / 1e9:7.1f} {t1:8.3f} {fl / t1 / 1e9:7.1f}"
               f" {t2:9.3f} {fl / t2 / 1e9:7.1f}", flush=True)
