@@ -14,6 +14,8 @@ Backward mirrors it; weight gradients are written straight into the flat f32
 gradient buffer (src/params.py) and skipped when the layer is frozen
 (src/framework.py:284-285 toggles requires_grad).
 """
+import os
+
 import torch
 
 from . import kernels as K
@@ -87,41 +89,77 @@ def _reduce(part, out):
     K.colsum_reduce(part, out, accumulate=True)
 
 
+SIDE_STREAM = os.environ.get("MMU_SIDE_STREAM", "0") == "1"
+
+
+class _Side:
+    """Runs the weight-gradient work of a layer's backward (split-K dW products, LN /
+    bias column-sum reductions) on a side stream, each piece ordered after the main-stream
+    kernel that produced its inputs by an event, so it overlaps the data-gradient chain
+    (and fills the tail rounds of its GEMMs).  Tensors touched on the side stream are
+    record_stream'ed so the caching allocator does not recycle them early.
+    Opt-in (MMU_SIDE_STREAM=1): measured 210 -> 207 ms per step, but co-running kernels
+    stretch each other's event-timed durations, which the per-kernel roofline of bench.py
+    reads as a slower GEMM."""
+
+    def __init__(self, dev, on):
+        on = on and SIDE_STREAM
+        self.on = on
+        self.main = torch.cuda.current_stream(dev)
+        self.side = K.side_stream(dev) if on else None
+
+    def run(self, fn, *tensors):
+        if not self.on:
+            return fn()
+        ev = torch.cuda.Event()
+        ev.record(self.main)
+        self.side.wait_event(ev)
+        for t in tensors:
+            t.record_stream(self.side)
+        with torch.cuda.stream(self.side):
+            fn()
+
+
 def layer_backward(lw, saved, dY, keymask, B, L, p_attn, p_hid, seeds, wgrad):
     X, qkv, O, lse, dmask, S1, mean1, rstd1, A, Z, Hh, S2, mean2, rstd2 = saved
     M = B * L
     dev = dY.device
     P = K.ln_parts(M)
-    pw = pb = pbias = None
-    if wgrad:
-        pw, pb, pbias = (torch.empty(P, HID, dtype=torch.float32, device=dev) for _ in range(3))
+    side = _Side(dev, wgrad)
+    pw = pb = pbias = pw1 = pb1 = pbias1 = None
+    if wgrad:  # two sets: the side stream reduces one while the main stream fills the other
+        pw, pb, pbias, pw1, pb1, pbias1 = (torch.empty(P, HID, dtype=torch.float32, device=dev) for _ in range(6))
     acc = K.epilogue(K.EPI_STORE, accumulate=True)
     # ---- output LayerNorm + dropout + W2
     dS2 = torch.empty(M, HID, dtype=bf16, device=dev)
     dY2 = torch.empty(M, HID, dtype=bf16, device=dev)
     K.layernorm_bwd(dY, S2, mean2, rstd2, lw.ln2w, dS2, dY2, p_hid, seeds[2], pw, pb, pbias)
     if wgrad:
-        _reduce(pw, lw.g_ln2w)
-        _reduce(pb, lw.g_ln2b)
-        _reduce(pbias, lw.g_b2)
-        K.gemm(dY2, HID, False, Hh, FFN, False, lw.g_w2, FFN, HID, FFN, M, epi=acc)
+        def w2():
+            _reduce(pw, lw.g_ln2w)
+            _reduce(pb, lw.g_ln2b)
+            _reduce(pbias, lw.g_b2)
+            K.gemm(dY2, HID, False, Hh, FFN, False, lw.g_w2, FFN, HID, FFN, M, epi=acc)
+        side.run(w2, pw, pb, pbias, dY2, Hh)
     dZ = torch.empty(M, FFN, dtype=bf16, device=dev)
     # dgelu epilogue also accumulates the intermediate-bias gradient (column sums of dZ) in place
     K.gemm(dY2, HID, True, lw.w216, FFN, False, dZ, FFN, M, FFN, HID,
            epi=K.epilogue(K.EPI_DGELU, aux=Z, colsum=lw.g_b1 if wgrad else None))
     if wgrad:
-        K.gemm(dZ, FFN, False, A, HID, False, lw.g_w1, HID, FFN, HID, M, epi=acc)
+        side.run(lambda: K.gemm(dZ, FFN, False, A, HID, False, lw.g_w1, HID, FFN, HID, M, epi=acc), dZ, A)
     dA = torch.empty(M, HID, dtype=bf16, device=dev)
     K.gemm(dZ, FFN, True, lw.w116, HID, False, dA, HID, M, HID, FFN, epi=K.epilogue(K.EPI_ADD_RES, residual=dS2))
     # ---- attention-output LayerNorm + dropout + Wo
     dS1 = torch.empty(M, HID, dtype=bf16, device=dev)
     dAo = torch.empty(M, HID, dtype=bf16, device=dev)
-    K.layernorm_bwd(dA, S1, mean1, rstd1, lw.ln1w, dS1, dAo, p_hid, seeds[1], pw, pb, pbias)
+    K.layernorm_bwd(dA, S1, mean1, rstd1, lw.ln1w, dS1, dAo, p_hid, seeds[1], pw1, pb1, pbias1)
     if wgrad:
-        _reduce(pw, lw.g_ln1w)
-        _reduce(pb, lw.g_ln1b)
-        _reduce(pbias, lw.g_bo)
-        K.gemm(dAo, HID, False, O, HID, False, lw.g_wo, HID, HID, HID, M, epi=acc)
+        def wo():
+            _reduce(pw1, lw.g_ln1w)
+            _reduce(pb1, lw.g_ln1b)
+            _reduce(pbias1, lw.g_bo)
+            K.gemm(dAo, HID, False, O, HID, False, lw.g_wo, HID, HID, HID, M, epi=acc)
+        side.run(wo, pw1, pb1, pbias1, dAo, O)
     dO = torch.empty(M, HID, dtype=bf16, device=dev)
     K.gemm(dAo, HID, True, lw.wo16, HID, False, dO, HID, M, HID, HID)
     # ---- attention + fused QKV
@@ -129,12 +167,14 @@ def layer_backward(lw, saved, dY, keymask, B, L, p_attn, p_hid, seeds, wgrad):
     delta = torch.empty(B * HEADS, L, dtype=torch.float32, device=dev)
     K.attention_bwd(qkv, keymask, O, dO, lse, delta, dqkv, B, L, HEADS, p_attn, seeds[0], dmask)
     if wgrad:
-        K.colsum_bf16(dqkv, lw.g_bqkv, accumulate=True)
-        K.gemm(dqkv, 3 * HID, False, X, HID, False, lw.g_wqkv, HID, 3 * HID, HID, M, epi=acc)
+        def wqkv():
+            K.colsum_bf16(dqkv, lw.g_bqkv, accumulate=True)
+            K.gemm(dqkv, 3 * HID, False, X, HID, False, lw.g_wqkv, HID, 3 * HID, HID, M, epi=acc)
+        side.run(wqkv, dqkv, X)
     dX = torch.empty(M, HID, dtype=bf16, device=dev)
     K.gemm(dqkv, 3 * HID, True, lw.wqkv16, HID, False, dX, HID, M, HID, 3 * HID,
            epi=K.epilogue(K.EPI_ADD_RES, residual=dS1))
-    return dX
+    return dX, side
 
 
 class BertLayerFunction(torch.autograd.Function):
@@ -152,8 +192,32 @@ class BertLayerFunction(torch.autograd.Function):
     def backward(ctx, dY):
         lw, keymask, B, L, p_attn, p_hid, seeds, hook = ctx.meta
         wgrad = lw.trainable()
-        dX = layer_backward(lw, ctx.saved_bufs, dY.contiguous(), keymask, B, L, p_attn, p_hid, seeds, wgrad)
+        dX, side = layer_backward(lw, ctx.saved_bufs, dY.contiguous(), keymask, B, L, p_attn, p_hid, seeds, wgrad)
         ctx.saved_bufs = None
-        if wgrad and hook is not None:
+        if wgrad and side.on:
+            if hook is not None:  # the gradient all-reduce is issued behind the side stream's work
+                with torch.cuda.stream(side.side):
+                    hook(lw)
+            _join_side_at_end(side)
+        elif wgrad and hook is not None:
             hook(lw)
         return dX, None, None, None, None, None, None, None, None, None
+
+
+_pending_join = set()
+
+
+def _join_side_at_end(side):
+    """Once per backward pass: the main stream waits for the weight-gradient stream when
+    the autograd engine finishes, so every consumer of .grad (optimizer, tests) sees them."""
+    key = (side.main.cuda_stream, side.side.cuda_stream)
+    if key in _pending_join:
+        return
+    _pending_join.add(key)
+    main, s = side.main, side.side
+
+    def join():
+        _pending_join.discard(key)
+        main.wait_stream(s)
+
+    torch.autograd.Variable._execution_engine.queue_callback(join)

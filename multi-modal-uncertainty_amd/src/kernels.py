@@ -46,15 +46,27 @@ def epilogue(kind=EPI_STORE, bias=None, residual=None, aux=None, colsum=None, dr
     return e
 
 
-SPLITK_WS_FLOATS = 16 << 20  # 64 MiB per device, reused stream-ordered by every split-K product
+SPLITK_WS_FLOATS = 16 << 20  # 64 MiB per (device, stream), reused stream-ordered by every split-K product
 _ws = {}
+_side = {}
 
 
 def _splitk_workspace(dev):
-    t = _ws.get(dev)
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    t = _ws.get(key)
     if t is None:
-        t = _ws[dev] = torch.empty(SPLITK_WS_FLOATS, dtype=torch.float32, device=dev)
+        t = _ws[key] = torch.empty(SPLITK_WS_FLOATS, dtype=torch.float32, device=dev)
     return t
+
+
+def side_stream(dev):
+    """The per-device stream the weight-gradient products run on, beside the data-gradient
+    chain of the backward (src/encoder.py)."""
+    dev = torch.device(dev)
+    s = _side.get(dev)
+    if s is None:
+        s = _side[dev] = torch.cuda.Stream(device=dev)
+    return s
 
 
 def gemm(A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, M, N_, K, epi=None, batch=1, sA=0, sB=0, sC=0):

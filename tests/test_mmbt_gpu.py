@@ -163,3 +163,28 @@ def test_freeze_skips_weight_grads(dev):
     assert all(p.grad.abs().max().item() == 0 for p in model.enc.img_encoder.parameters())
     assert model.enc.txt_embeddings.word_embeddings.weight.grad.abs().max().item() > 0
     assert model.clf.weight.grad.abs().max().item() > 0
+
+
+def test_side_stream_weight_grads_identical(dev, monkeypatch):
+    """MMU_SIDE_STREAM: the weight-gradient work on the side stream gives the same
+    gradients (same kernels; only the float-atomic column sums may reorder) and every
+    .grad is complete when backward() returns."""
+    from src import encoder as E
+    from src.testing import synthetic_batch
+    # MIOpen's default conv solvers are not bitwise reproducible (~1e-6 in fp32), which bf16
+    # rounding in the encoder amplifies to ~3e-3: pin them for the comparison
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    model, sd, cfg = build("small", dev, bert_hidden_dropout=0.0, bert_attn_dropout=0.0, dropout=0.0)
+    x, y = synthetic_batch(4, 16, vocab=cfg.vocab, seed=6)
+    x = tuple(t.to(dev) for t in x)
+    y = y.to(dev)
+    model.train()
+    grads = []
+    for on in (False, True):
+        monkeypatch.setattr(E, "SIDE_STREAM", on)
+        model.store.zero_grad()
+        torch.manual_seed(11)  # same dropout seeds (embedding / hidden dropout draw from the torch RNG)
+        model.compute_loss(model(*x), y).backward()
+        grads.append(model.store.grad.clone())  # read on the main stream right after backward
+    scale = grads[0].abs().max().item()
+    torch.testing.assert_close(grads[1], grads[0], rtol=1e-4, atol=1e-6 * scale)
