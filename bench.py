@@ -84,6 +84,19 @@ def cpu_baseline(args, L_text):
                       f"warm-up, torch CPU {torch.get_num_threads()} threads"}
 
 
+def gemm_traffic():
+    """Per-launch HBM bytes of the GEMMs from the newest committed PMC summary
+    (profiles/r*_gemm_traffic.json, written by tools/pmc_traffic.py from two rocprofv3
+    --pmc passes of this script: FETCH_SIZE, WRITE_SIZE; gfx950 FETCH correction applied)."""
+    import glob
+    here = os.path.dirname(os.path.abspath(__file__))
+    files = sorted(glob.glob(os.path.join(here, "profiles", "r*_gemm_traffic.json")))
+    if not files:
+        return {"bytes": None, "source": None}
+    d = json.load(open(files[-1]))
+    return {"bytes": round(d["traffic_bytes_per_launch"]), "source": os.path.relpath(files[-1], here)}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -149,12 +162,14 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     gemm_ms, gemm_n, gemm_flops = K.timing_read()
+    alg_bytes, _ = K.timing_alg_bytes()
     K.timing_enable(False)
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
     ms_step = 1000.0 * dt / args.steps
+    traffic = gemm_traffic()
     value = args.global_batch * args.steps / dt
     H = 768
     layer_fwd = L * (24 * H * H + 4 * L * H)
@@ -171,7 +186,9 @@ def main():
                    "trainable_params": sum(p.numel() for p in model.parameters())},
         "roofline": {"bound": "mfma", "kernel": "mmu_gemm (all BERT-layer GEMMs, fwd + bwd)",
                      "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic["bytes"],
+                     "traffic_unit": "bytes/launch (PMC, corrected)", "traffic_source": traffic["source"],
+                     "algorithmic_bytes_per_launch": round(alg_bytes / max(gemm_n, 1)),
                      "launches": gemm_n, "avg_launch_ms": round(gemm_ms / max(gemm_n, 1), 4),
                      "gemm_share_of_step": round(gemm_ms / args.steps / ms_step, 3) if ms_step else None},
         "model_tflops_per_step_per_rank": round(B * model_flop / 1e12, 2),

@@ -85,6 +85,8 @@ def gemm(A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, M, N_, K, epi=None, batch=1
             epi.workspace, epi.workspace_floats = ws.data_ptr(), ws.numel()
     N.call("mmu_gemm", _ptr(A), lda, int(a_kmajor), _ptr(B), ldb, int(b_kmajor), _ptr(C), ldc, cdt, M, N_, K,
            batch, sA, sB, sC, ctypes.byref(epi) if epi is not None else None, _stream(C))
+    if _alg["on"]:
+        _count_alg(M, N_, K, batch, 4 if cdt == N.MMU_F32 else 2, epi)
     return C
 
 
@@ -248,11 +250,35 @@ def ece_bins(conf, correct, n_bins, out):
     N.call("mmu_ece_bins", _ptr(conf), _ptr(correct), conf.numel(), n_bins, _ptr(out), _stream(conf))
 
 
+_alg = {"on": False, "bytes": 0.0, "n": 0}
+
+
 def timing_enable(on=True):
+    """HIP-event timing of every mmu_gemm launch (and a count of its algorithmic bytes)."""
     N.call("mmu_timing_enable", int(on))
+    _alg.update(on=bool(on), bytes=0.0, n=0)
 
 
 def timing_read():
     ms, n, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
     N.call("mmu_timing_read", ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl))
     return ms.value, n.value, fl.value
+
+
+def timing_alg_bytes():
+    """(algorithmic HBM bytes, launches) of the timed GEMMs: operands read once, C written
+    once (read too when accumulating), residual / aux streams of the fused epilogues."""
+    return _alg["bytes"], _alg["n"]
+
+
+def _count_alg(M, N_, K, batch, c_bytes, epi):
+    b = 2.0 * (M * K + N_ * K) + c_bytes * M * N_
+    if epi is not None:
+        if epi.accumulate:
+            b += c_bytes * M * N_
+        if epi.residual:
+            b += 2.0 * M * N_
+        if epi.aux:
+            b += 2.0 * M * N_
+    _alg["bytes"] += b * batch
+    _alg["n"] += 1
