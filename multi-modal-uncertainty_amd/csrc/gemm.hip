@@ -29,6 +29,35 @@ constexpr int BKT = 64;
 
 static __device__ __forceinline__ int sw_mn(int r) { return (r & 7) ^ (((r >> 3) & 1) << 2); }
 
+// ---------------------------------------------------------------- tile order
+// Grouped order: pids walk GROUP_M tile rows column by column, so the ~32 tiles an XCD
+// runs at once (consecutive pids after xcd_remap) form an 8 x 4 block sharing 8 A and 4 B
+// panels instead of ~3 x 12 (row-major at N = 3072), which cut the L2 misses of the wide
+// products (rocprofv3 FETCH_SIZE, profiles/).
+// GROUP_M = p.group_m (host heuristic in capi.hip; 1 = plain row-major order).
+static __device__ __forceinline__ void tile_of(int pid, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
+  const int per_group = group_m * tiles_n;
+  const int g = pid / per_group, first = g * group_m;
+  const int gm = tiles_m - first < group_m ? tiles_m - first : group_m;
+  const int r = pid - g * per_group;
+  tm = first + r % gm;
+  tn = r / gm;
+}
+// The dispatcher deals workgroups to the 8 XCDs round-robin by LINEAR id (x fastest, then
+// y = split-K slice, then z = batch item).  Remap the linear id so each XCD holds a
+// contiguous run of pids, and order pids batch item > slice > tile: blocks of one slice
+// (which share A / B K-ranges) then sit on one XCD's L2.
+static __device__ __forceinline__ void block_tile(const GemmParams& p, int64_t& z, int& slice, int& tm, int& tn) {
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int per_z = ntiles * (int)gridDim.y;
+  const int lin = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+  const int pid = xcd_remap(lin, per_z * (int)gridDim.z);
+  z = pid / per_z;
+  const int r = pid - (int)z * per_z;
+  slice = r / ntiles;
+  tile_of(r - slice * ntiles, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
+}
+
 // ---------------------------------------------------------------- fragment reads
 // lane l holds operand[row0 + (l&15)][k = 32ks + 8(l>>4) + j], j = 0..7
 template <bool KMAJ, int ROWB>  // ROWB: bytes per LDS row of an M/N-major tile (256 or 512)
@@ -110,13 +139,13 @@ static __device__ __forceinline__ void epi_oct(const GemmParams& p, int64_t z, i
 // through the wave-private LDS region ws (16 KiB; the caller has passed a barrier that
 // retires every staging read of it)
 template <int EPI, bool OUT_F32, int NJ>
-static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64_t z, int64_t mw, int64_t nw,
-                                                      f32x4 (&acc)[4][NJ], int l, char* ws) {
+static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64_t z, int slice, int64_t mw,
+                                                      int64_t nw, f32x4 (&acc)[4][NJ], int l, char* ws) {
   if (nw >= p.N) return;  // (N % 128 == 0: a 64-column wave block is all in or all out)
   const int q = l & 7, rr = l >> 3;
   const int64_t n = nw + 8 * q;
   const bool slab = p.splitk > 1;  // raw partial product -> this slice's f32 slab (splitk_reduce_kernel)
-  float* slab_base = slab ? p.ws + (z * p.splitk + blockIdx.y) * p.M * p.N : nullptr;
+  float* slab_base = slab ? p.ws + (z * p.splitk + slice) * p.M * p.N : nullptr;
   const float* bias = (!slab && p.bias && EPI != MMU_EPI_DGELU && EPI != MMU_EPI_ADD_RES)
                           ? p.bias + z * p.bias_bstride : nullptr;
   const bf16* res = p.residual ? (const bf16*)p.residual + z * p.res_bstride : nullptr;
@@ -235,10 +264,9 @@ template <bool AK, bool BKM, int EPI, bool OUT_F32>
 __global__ __launch_bounds__(256) void gemm_small_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * S_STAGE];
   const int t = threadIdx.x, l = t & 63, w = t >> 6, wm = w >> 1, wn = w & 1;
-  const int nwg = p.tiles_m * p.tiles_n;
-  const int pid = xcd_remap(blockIdx.x, nwg);
-  const int tm = pid / p.tiles_n, tn = pid - tm * p.tiles_n;
-  const int64_t z = blockIdx.z;
+  int tm, tn, slice;
+  int64_t z;
+  block_tile(p, z, slice, tm, tn);
   const bf16* __restrict__ A = p.A + z * p.sA;
   const bf16* __restrict__ B = p.B + z * p.sB;
   const int64_t m0 = (int64_t)tm * SBM, n0 = (int64_t)tn * SBN;
@@ -248,7 +276,7 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   uint4 ra[4], rb[4];
-  const int64_t kb = (int64_t)blockIdx.y * p.kchunk;
+  const int64_t kb = (int64_t)slice * p.kchunk;
   const int64_t ke = kb + p.kchunk < p.K ? kb + p.kchunk : p.K;
   const int nk = (int)((ke - kb + BKT - 1) / BKT);
   g_load<AK>(ra, A, p.lda, m0, p.M, kb, ke, t);
@@ -284,7 +312,7 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(GemmParams p) {
     }
     __syncthreads();
   }
-  epilogue_block<EPI, OUT_F32, 4>(p, z, m0 + 64 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
+  epilogue_block<EPI, OUT_F32, 4>(p, z, slice, m0 + 64 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
 }
 
 // ================================================================ big: 256x256, LDS-DMA
@@ -321,10 +349,9 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p) {
   const int t = threadIdx.x, l = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = w >> 2, wn = w & 3;
-  const int nwg = p.tiles_m * p.tiles_n;
-  const int pid = xcd_remap(blockIdx.x, nwg);
-  const int tm = pid / p.tiles_n, tn = pid - tm * p.tiles_n;
-  const int64_t z = blockIdx.z;
+  int tm, tn, slice;
+  int64_t z;
+  block_tile(p, z, slice, tm, tn);
   const int64_t m0 = (int64_t)tm * BBM, n0 = (int64_t)tn * BBN;
   // operand byte ranges: rows (K-major) or k-rows (M/N-major) beyond the operand read as zero
   const int64_t a_bytes = (AK ? p.M * p.lda : p.K * p.lda) * 2;
@@ -341,7 +368,7 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int64_t kb = (int64_t)blockIdx.y * p.kchunk;
+  const int64_t kb = (int64_t)slice * p.kchunk;
   const int64_t ke = kb + p.kchunk < p.K ? kb + p.kchunk : p.K;
   const int nk = (int)((ke - kb + BKT - 1) / BKT);
   dma_tile<AK>(smem, ra, p.lda, m0, kb, w, l);
@@ -373,7 +400,7 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  epilogue_block<EPI, OUT_F32, 8>(p, z, m0 + 128 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
+  epilogue_block<EPI, OUT_F32, 8>(p, z, slice, m0 + 128 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
 }
 
 // ================================================================ pipelined 256x256 (8 phases / 2 K-tiles)
@@ -428,10 +455,9 @@ __global__ __launch_bounds__(512) void gemm_pipe_kernel(GemmParams p) {
   const int t = threadIdx.x, l = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = w >> 2, wn = w & 3;
-  const int nwg = p.tiles_m * p.tiles_n;
-  const int pid = xcd_remap(blockIdx.x, nwg);
-  const int tm = pid / p.tiles_n, tn = pid - tm * p.tiles_n;
-  const int64_t z = blockIdx.z;
+  int tm, tn, slice;
+  int64_t z;
+  block_tile(p, z, slice, tm, tn);
   const int64_t m0 = (int64_t)tm * BBM, n0 = (int64_t)tn * BBN;
   const int64_t a_bytes = (AK ? p.M * p.lda : p.K * p.lda) * 2;
   const int64_t b_bytes = (BKM ? p.N * p.ldb : p.K * p.ldb) * 2;
@@ -446,7 +472,7 @@ __global__ __launch_bounds__(512) void gemm_pipe_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int64_t kb = (int64_t)blockIdx.y * p.kchunk;
+  const int64_t kb = (int64_t)slice * p.kchunk;
   const int64_t ke = kb + p.kchunk < p.K ? kb + p.kchunk : p.K;
   const int nk = (int)((ke - kb + BKT - 1) / BKT);
   dma_half<AK, 64>(smem + 0 * P_HALF, ra, p.lda, m0, 0, kb, w, l);
@@ -527,7 +553,7 @@ __global__ __launch_bounds__(512) void gemm_pipe_kernel(GemmParams p) {
     mma(fb0, 0, 1);
     bar();
   }
-  epilogue_block<EPI, OUT_F32, 8>(p, z, m0 + 128 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
+  epilogue_block<EPI, OUT_F32, 8>(p, z, slice, m0 + 128 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
 }
 
 // ---------------------------------------------------------------- launch

@@ -14,6 +14,7 @@ struct GemmParams {
   void* C;
   int64_t lda, ldb, ldc, M, N, K, sA, sB, sC;
   int tiles_m, tiles_n;
+  int group_m;  // tile-order group height (gemm.hip tile_of)
   // epilogue (flattened mmu_epilogue)
   int kind, accumulate;
   const float* bias;

@@ -34,7 +34,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=256 * 513)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--var", default="MMU_GEMM_PIPE", help="env switch of the variant compared (=1) to default (=0)")
+    ap.add_argument("--var", default="MMU_GEMM_PIPE", help="env switch of the variants compared")
+    ap.add_argument("--vals", default="1,0", help="values of --var, timed interleaved in one process")
     a = ap.parse_args()
     M, dev, bf = a.rows, "cuda", torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
@@ -88,20 +89,20 @@ def main():
                         epi=K.epilogue(K.EPI_STORE, accumulate=True)),
          lambda: torch.matmul(dZ.t(), A)),
     ]
-    print(f"{'gemm':26s} {'M':>7s} {'N':>5s} {'K':>7s} {'var ms':>8s} {'TF/s':>7s} {'dflt ms':>8s} {'TF/s':>7s}"
-          f" {'blasLt ms':>9s} {'TF/s':>7s}")
+    vals = a.vals.split(",")
+    print(f"{'gemm':26s} {'M':>7s} {'N':>5s} {'K':>7s} " + " ".join(f"{a.var[-8:] + '=' + v:>18s}" for v in vals)
+          + f" {'hipBLASLt':>18s}")
     for name, m, n, k, f_mmu, f_ref in cases:
         fl = 2.0 * m * n * k
-        t0, t1 = float("inf"), float("inf")
-        for _ in range(3):  # interleaved A/B rounds in one process: variant (env) vs default
-            os.environ[a.var] = "1"
-            t0 = min(t0, timed(f_mmu, a.iters))
-            os.environ[a.var] = "0"
-            t1 = min(t1, timed(f_mmu, a.iters))
-        os.environ[a.var] = "0"
+        ts = {v: float("inf") for v in vals}
+        for _ in range(3):  # interleaved rounds in one process
+            for v in vals:
+                os.environ[a.var] = v
+                ts[v] = min(ts[v], timed(f_mmu, a.iters))
+        os.environ.pop(a.var, None)
         t2 = timed(f_ref, a.iters)
-        print(f"{name:26s} {m:7d} {n:5d} {k:7d} {t0:8.3f} {fl / t0 / 1e9:7.1f} {t1:8.3f} {fl / t1 / 1e9:7.1f}"
-              f" {t2:9.3f} {fl / t2 / 1e9:7.1f}", flush=True)
+        print(f"{name:26s} {m:7d} {n:5d} {k:7d} " + " ".join(f"{ts[v]:8.3f}ms {fl / ts[v] / 1e9:6.0f}T" for v in vals)
+              + f" {t2:8.3f}ms {fl / t2 / 1e9:6.0f}T", flush=True)
 
 
 if __name__ == "__main__":
