@@ -22,6 +22,7 @@
 // per (bh, query, 64-key tile) in `dropmask`; dQ and dKdV read those bits.
 #include "mmu_common.h"
 #include "mmu_internal.h"
+#include <cstdlib>
 
 namespace mmu {
 
@@ -499,10 +500,177 @@ void attention_fwd_launch(const AttnParams& p, hipStream_t s) {
   hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, s, p);
 }
 
+// ------------------------------------------------------------------ dK/dV, LDS-DMA ring
+// Same math and tiles as attn_dkdv_kernel, but the per-query-tile operands (Q and dO rows,
+// -LSE, delta, keep bits) arrive by buffer_load...lds into a 4-deep LDS ring, issued 3
+// tiles ahead: the register-staged version waits for each tile's HBM/L2 round trip
+// behind one tile of compute.  Lane-linear DMA images: Q / dO chunk swizzle applied to the
+// SOURCE address (same image as TileLoader writes); rows past L read as zero through the
+// per-(batch item) buffer range (zero Q and dO rows contribute nothing).  K is pre-scaled
+// by 1/8 in registers (exact), so dK gets the 1/8 at the end.  One raw s_barrier per tile
+// (no __syncthreads: it would drain the DMA queue).
+constexpr int DK_NS = 4;                                   // ring depth
+constexpr int DK_TILE = 32 * 128;                          // 32 rows x 64 d bf16
+constexpr int DK_ROWS = 32 * 4 + 32 * 4 + 32 * 8;          // -lse (as lse), delta, keep words
+constexpr int DK_STAGE = 2 * DK_TILE + DK_ROWS;            // 8704 B
+
+static __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (MMU_LDS(void)*)lds, 16, off, 0, 0, 0);
+}
+static __device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (MMU_LDS(void)*)lds, 4, off, 0, 0, 0);
+}
+static __device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void attn_dkdv_dma_kernel(AttnParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[DK_NS * DK_STAGE];
+  const int t = threadIdx.x, l = t & 63, h = l >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int bh = blockIdx.y, b = bh / p.heads, hd = bh - b * p.heads;
+  const int L = p.L, HD = p.heads * 64;
+  const int k0w = blockIdx.x * 64 + 32 * w, key = k0w + (l & 31);
+  const bool wave_live = k0w < L, kv = key < L;
+  const bool drop = drop_thr(p.drop_p) != 0;
+  const float zs = drop ? 1.0f / (1.0f - p.drop_p) : 1.0f;
+  const int nkv = (L + 63) / 64;
+  const float mkey = kv ? p.keymask[(int64_t)b * L + key] * LOG2E : NEG_INF;
+  const bf16* base = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64;
+
+  // operand buffers of this (batch item, head): rows beyond L are out of range -> zero
+  const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.qkv + (int64_t)b * L * p.ld_qkv), 0, (int)(L * p.ld_qkv * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rdo = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.dout + (int64_t)b * L * p.ld_do), 0, (int)(L * p.ld_do * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)(p.lse + (int64_t)bh * L), 0,
+                                                                      (int)(L * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)(p.delta + (int64_t)bh * L), 0,
+                                                                      (int)(L * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(drop ? p.dropmask + (int64_t)bh * L * nkv : p.dropmask), 0, drop ? (int)(L * nkv * 8) : 0, 0x00020000);
+
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    uint4 u = kv ? *(const uint4*)(base + (int64_t)key * p.ld_qkv + HD + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
+    uint4 v = kv ? *(const uint4*)(base + (int64_t)key * p.ld_qkv + 2 * HD + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
+    kf[ks] = scale_frag(u, 0.125f);
+    vf[ks] = *(bf16x8*)&v;
+  }
+  f32x16 dk[2], dv[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { dk[0][i] = 0.f; dk[1][i] = 0.f; dv[0][i] = 0.f; dv[1][i] = 0.f; }
+
+  const int nq = (L + 31) / 32;
+  // per tile: wave 0 -> Q pieces 0..3, lse, delta (6 DMAs); wave 1 -> dO pieces 0..3, keep (5)
+  auto issue = [&](int i) {
+    char* st = smem + (i % DK_NS) * DK_STAGE;
+    const int q0 = i * 32;
+    if (w == 0) {
+#pragma unroll
+      for (int pc = 0; pc < 4; ++pc) {
+        const int row = 8 * pc + (l >> 3), c = (l & 7) ^ fsw(row);
+        dma16(rq, st + pc * 1024, (uint32_t)(((q0 + row) * p.ld_qkv + hd * 64 + 8 * c) * 2));
+      }
+      if (l < 8) {
+        dma16(rl, st + 2 * DK_TILE, (uint32_t)((q0 + 4 * l) * 4));
+        dma16(rd, st + 2 * DK_TILE + 128, (uint32_t)((q0 + 4 * l) * 4));
+      }
+    } else {
+#pragma unroll
+      for (int pc = 0; pc < 4; ++pc) {
+        const int row = 8 * pc + (l >> 3), c = (l & 7) ^ fsw(row);
+        dma16(rdo, st + DK_TILE + pc * 1024, (uint32_t)(((q0 + row) * p.ld_do + hd * 64 + 8 * c) * 2));
+      }
+      // keep word of query row q0 + l/2 for this key block: 4 B per lane (low / high half)
+      dma4(rk, st + 2 * DK_TILE + 256, (uint32_t)((((q0 + (l >> 1)) * nkv + blockIdx.x) * 8) + 4 * (l & 1)));
+    }
+  };
+  // vmcnt: this wave's DMAs per tile (6 or 5) times the tiles allowed to stay in flight
+  auto wait_for = [&](int ahead) {
+    if (w == 0) {
+      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  };
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K / V fragment loads
+  for (int i = 0; i < DK_NS - 1 && i < nq; ++i) issue(i);
+  for (int i = 0; i < nq; ++i) {
+    // tiles i+1, i+2 may stay in flight; tile i must have landed for every wave
+    const int ahead = nq - 1 - i < DK_NS - 2 ? nq - 1 - i : DK_NS - 2;
+    wait_for(ahead);
+    raw_barrier();
+    if (i + DK_NS - 1 < nq) issue(i + DK_NS - 1);  // into the stage tile i-1 used (all waves are past it)
+    const char* st = smem + (i % DK_NS) * DK_STAGE;
+    const char* Qs = st;
+    const char* Ds = st + DK_TILE;
+    const float* lse = (const float*)(st + 2 * DK_TILE);
+    const float* dlt = lse + 32;
+    const uint32_t* kbit = (const uint32_t*)(st + 2 * DK_TILE + 256);  // [32 rows][2 halves]
+    if (wave_live) {
+      f32x16 sc, dp;  // S starts at -lse of its query row (row constant as initial accumulator)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { sc[r] = -lse[(r & 3) + 8 * (r >> 2) + 4 * h]; dp[r] = 0.f; }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Qs, 0, ks, l), kf[ks], sc, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ds, 0, ks, l), vf[ks], dp, 0, 0, 0);
+      }
+      f32x16 pz;  // dropped P (for dV)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ql = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float pr = __builtin_amdgcn_exp2f(fmaf(sc[r], LOG2E, mkey));
+        const uint32_t kw = drop ? kbit[2 * ql + w] : ~0u;
+        const float z = ((kw >> (l & 31)) & 1u) ? zs : 0.f;
+        pz[r] = pr * z;
+        sc[r] = pr * (dp[r] * z - dlt[ql]);  // dS
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 pf = acc_frag(pz, s2), sf = acc_frag(sc, s2);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf, tr_frag(Ds, 16 * s2, 32 * dt, l), dv[dt], 0, 0, 0);
+          dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sf, tr_frag(Qs, 16 * s2, 32 * dt, l), dk[dt], 0, 0, 0);
+        }
+      }
+    }
+  }
+  if (!wave_live) return;
+  bf16* outb = p.out + (int64_t)b * L * p.ld_out + hd * 64;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kk = k0w + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (kk < L) {
+        const int64_t off = (int64_t)kk * p.ld_out + 32 * dt + (l & 31);
+        outb[off + HD] = f2bf(dk[dt][r] * 0.125f);
+        outb[off + 2 * HD] = f2bf(dv[dt][r]);
+      }
+    }
+}
+
+static bool attn_dma() {
+  const char* e = getenv("MMU_ATTN_DMA");  // 0 = register-staged kernels (A/B comparisons)
+  return !(e && e[0] == '0');
+}
+
 void attention_bwd_launch(const AttnParams& p, hipStream_t s) {
   hipLaunchKernelGGL(attn_delta_kernel, dim3((p.L + 31) / 32, p.batch * p.heads), dim3(256), 0, s, p);
   hipLaunchKernelGGL(attn_dq_kernel, dim3((p.L + 127) / 128, p.batch * p.heads), dim3(256), 0, s, p);
-  hipLaunchKernelGGL(attn_dkdv_kernel, dim3((p.L + 63) / 64, p.batch * p.heads), dim3(128), 0, s, p);
+  if (attn_dma())
+    hipLaunchKernelGGL(attn_dkdv_dma_kernel, dim3((p.L + 63) / 64, p.batch * p.heads), dim3(128), 0, s, p);
+  else
+    hipLaunchKernelGGL(attn_dkdv_kernel, dim3((p.L + 63) / 64, p.batch * p.heads), dim3(128), 0, s, p);
 }
 
 }  // namespace mmu
