@@ -102,6 +102,18 @@ struct TileLoader {
   }
 };
 
+// ---- LDS-DMA helpers (buffer_load ... lds: lane-linear LDS destination, per-lane source)
+static __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (MMU_LDS(void)*)lds, 16, off, 0, 0, 0);
+}
+static __device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (MMU_LDS(void)*)lds, 4, off, 0, 0, 0);
+}
+static __device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // =============================================================================== forward
 // grid (ceil(L/128), batch*heads), 256 threads; wave w owns queries [blk*128 + 32w, +32)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_fwd_kernel(AttnParams p) {
@@ -230,7 +242,173 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     __syncthreads();
   }
   if (!wave_live || q >= L) return;
-  const float inv = (p.drop_p > 0.f ? 1.0f / (1.0f - p.drop_p) : 1.0f) / l_run;
+  const float inv = (thr ? 1.0f / (1.0f - p.drop_p) : 1.0f) / l_run;
+  bf16* ob = p.out + ((int64_t)b * L + q) * p.ld_out + hd * 64;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 v = {f2bf(o[dt][4 * g] * inv), f2bf(o[dt][4 * g + 1] * inv), f2bf(o[dt][4 * g + 2] * inv),
+                  f2bf(o[dt][4 * g + 3] * inv)};
+      *(bf16x4*)(ob + 32 * dt + 8 * g + 4 * h) = v;
+    }
+  if (h == 0) p.lse[(int64_t)bh * L + q] = m_run * LN2 + logf(l_run);
+}
+
+// ---------------------------------------------------------------- forward, LDS-DMA ring
+// attn_fwd_kernel with K / V tiles and the key-mask row arriving by buffer_load...lds into
+// a 3-deep ring (2 tiles ahead, one raw barrier per tile).  Keys past L read as zero rows
+// and mask 0, so the partial last tile masks them to -inf explicitly.  The keep bits go
+// to a per-wave LDS buffer and are written out once at the end (stores inside the loop
+// would break the counted vmcnt waits).  Needs ceil(L/64) <= FWD_MAX_NKV.
+constexpr int FWD_NS = 2;
+constexpr int FWD_TILE = 64 * 128;
+constexpr int FWD_STAGE = 2 * FWD_TILE + 256;
+constexpr int FWD_MAX_NKV = 9;  // L <= 576 (BERT: 512 text + image tokens); keeps 3 blocks / CU
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void attn_fwd_dma_kernel(AttnParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[FWD_NS * FWD_STAGE + 4 * 32 * FWD_MAX_NKV * 8];
+  uint64_t* kbuf_all = (uint64_t*)(smem + FWD_NS * FWD_STAGE);
+  const int t = threadIdx.x, l = t & 63, h = l >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int bh = blockIdx.y, b = bh / p.heads, hd = bh - b * p.heads;
+  const int L = p.L, HD = p.heads * 64;
+  const int q0w = blockIdx.x * 128 + 32 * w, q = q0w + (l & 31);
+  const bool wave_live = q0w < L;
+  const bf16* base = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64;
+  const uint32_t sbh = seed_for(p.seed, bh), Lp = (uint32_t)((L + 1) & ~1);
+  const uint32_t thr = drop_thr(p.drop_p);
+  const int nkv = (L + 63) / 64;
+  uint64_t* kbuf = kbuf_all + w * 32 * nkv;  // [32 rows][nkv] keep words of this wave
+
+  const __amdgpu_buffer_rsrc_t rkv = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.qkv + (int64_t)b * L * p.ld_qkv), 0, (int)(L * p.ld_qkv * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)(p.keymask + (int64_t)b * L), 0,
+                                                                      (int)(L * 4), 0x00020000);
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    uint4 u = q < L ? *(const uint4*)(base + (int64_t)q * p.ld_qkv + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
+    qf[ks] = scale_frag(u, 0.125f);
+  }
+  f32x16 o[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
+  float m_run = NEG_INF, l_run = 0.f;
+
+  // per tile: waves 0,1 -> K pieces, waves 2,3 -> V pieces (4 each); wave 0 also the mask row
+  auto issue = [&](int j) {
+    char* st = smem + (j % FWD_NS) * FWD_STAGE;
+    const int k0 = j * 64;
+    const int off_col = (w < 2 ? HD : 2 * HD) + hd * 64;
+    char* dst = st + (w < 2 ? 0 : FWD_TILE);
+#pragma unroll
+    for (int pc = 0; pc < 4; ++pc) {
+      const int piece = 4 * (w & 1) + pc;
+      const int row = 8 * piece + (l >> 3), c = (l & 7) ^ fsw(row);
+      dma16(rkv, dst + piece * 1024, (uint32_t)(((k0 + row) * p.ld_qkv + off_col + 8 * c) * 2));
+    }
+    if (w == 0 && l < 16) dma16(rm, st + 2 * FWD_TILE, (uint32_t)((k0 + 4 * l) * 4));
+  };
+  auto wait_for = [&](int ahead) {
+    if (w == 0) {
+      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  };
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int j = 0; j < FWD_NS - 1 && j < nkv; ++j) issue(j);
+  for (int j = 0; j < nkv; ++j) {
+    const int ahead = nkv - 1 - j < FWD_NS - 2 ? nkv - 1 - j : FWD_NS - 2;
+    wait_for(ahead);
+    raw_barrier();
+    if (j + FWD_NS - 1 < nkv) issue(j + FWD_NS - 1);
+    const char* st = smem + (j % FWD_NS) * FWD_STAGE;
+    const char* Ks = st;
+    const char* Vs = st + FWD_TILE;
+    const float* mk = (const float*)(st + 2 * FWD_TILE);
+    const bool partial = (j + 1) * 64 > L;  // keys >= L live only in the last tile
+    if (wave_live) {
+      f32x16 sc[2];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[s2][i] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          sc[s2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ks, 32 * s2, ks, l), qf[ks], sc[s2], 0, 0, 0);
+      }
+      float mx = NEG_INF;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = 32 * s2 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          float s = (sc[s2][r] + mk[key]) * LOG2E;
+          if (partial && j * 64 + key >= L) s = NEG_INF;
+          sc[s2][r] = s;
+          mx = fmaxf(mx, s);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m_run, mx);
+      const float alpha = m_run == NEG_INF ? 0.f : __builtin_amdgcn_exp2f(m_run - mnew);
+      float rs = 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = __builtin_amdgcn_exp2f(sc[s2][r] - mnew);
+          sc[s2][r] = e;
+          rs += e;
+        }
+      rs += __shfl_xor(rs, 32, 64);
+      l_run = l_run * alpha + rs;
+      m_run = mnew;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+      if (thr) {
+        uint64_t kbits = 0;  // keep bits of this lane's 32 keys of the tile (bit = key - 64j)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int kl = 32 * s2 + 8 * g + 4 * h;
+            const uint32_t key = j * 64 + kl;
+            uint32_t h0 = drop_pair(sbh, q, key, Lp), h1 = drop_pair(sbh, q, key + 2, Lp);
+            const uint32_t k4 = ((h0 & 0xFFFFu) >= thr ? 1u : 0u) | ((h0 >> 16) >= thr ? 2u : 0u) |
+                                ((h1 & 0xFFFFu) >= thr ? 4u : 0u) | ((h1 >> 16) >= thr ? 8u : 0u);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (!((k4 >> e) & 1)) sc[s2][4 * g + e] = 0.f;
+            kbits |= (uint64_t)k4 << kl;
+          }
+        const uint64_t other = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(kbits >> 32), 32, 64) << 32) |
+                               (uint32_t)__shfl_xor((int)(uint32_t)kbits, 32, 64);
+        if (h == 0) kbuf[(l & 31) * nkv + j] = kbits | other;
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          bf16x8 pf = acc_frag(sc[s2], u);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt)
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Vs, 32 * s2 + 16 * u, 32 * dt, l), pf, o[dt], 0, 0,
+                                                            0);
+        }
+    }
+  }
+  if (!wave_live) return;
+  if (thr && p.dropmask) {  // this wave's 32 rows x nkv words are contiguous in the dropmask
+    uint64_t* dst = p.dropmask + ((int64_t)bh * L + q0w) * nkv;
+    const int rows = L - q0w < 32 ? L - q0w : 32;
+    for (int i = l; i < rows * nkv; i += 64) dst[i] = kbuf[i];
+  }
+  if (q >= L) return;
+  const float inv = (thr ? 1.0f / (1.0f - p.drop_p) : 1.0f) / l_run;
   bf16* ob = p.out + ((int64_t)b * L + q) * p.ld_out + hd * 64;
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt)
@@ -495,9 +673,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
     }
 }
 
+static bool attn_dma();
 void attention_fwd_launch(const AttnParams& p, hipStream_t s) {
   dim3 grid((p.L + 127) / 128, p.batch * p.heads);
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, s, p);
+  if (attn_dma() && (p.L + 63) / 64 <= FWD_MAX_NKV) hipLaunchKernelGGL(attn_fwd_dma_kernel, grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, s, p);
 }
 
 // ------------------------------------------------------------------ dK/dV, LDS-DMA ring
@@ -514,16 +694,6 @@ constexpr int DK_TILE = 32 * 128;                          // 32 rows x 64 d bf1
 constexpr int DK_ROWS = 32 * 4 + 32 * 4 + 32 * 8;          // -lse (as lse), delta, keep words
 constexpr int DK_STAGE = 2 * DK_TILE + DK_ROWS;            // 8704 B
 
-static __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t off) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (MMU_LDS(void)*)lds, 16, off, 0, 0, 0);
-}
-static __device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t off) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (MMU_LDS(void)*)lds, 4, off, 0, 0, 0);
-}
-static __device__ __forceinline__ void raw_barrier() {
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
 
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void attn_dkdv_dma_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) char smem[DK_NS * DK_STAGE];
@@ -659,6 +829,133 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
     }
 }
 
+// ------------------------------------------------------------------ dQ, LDS-DMA ring
+// attn_dq_kernel with its K / V tiles, key-mask row and (per wave) keep words arriving by
+// buffer_load...lds into a 3-deep ring, issued 2 tiles ahead, one raw barrier per tile.
+// Keys past L read as zero K / V rows and mask 0: their P is finite but multiplies zero K
+// rows (dQ += dS K) and zero V rows (dP), so they add nothing.
+constexpr int DQ_NS = 3;
+constexpr int DQ_TILE = 64 * 128;                         // 64 keys x 64 d bf16
+constexpr int DQ_STAGE = 2 * DQ_TILE + 256 + 4 * 256;     // K, V, mask row, 4 waves x 32 keep words
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_dq_dma_kernel(AttnParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[DQ_NS * DQ_STAGE];
+  const int t = threadIdx.x, l = t & 63, h = l >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int bh = blockIdx.y, b = bh / p.heads, hd = bh - b * p.heads;
+  const int L = p.L, HD = p.heads * 64;
+  const int q0w = blockIdx.x * 128 + 32 * w, q = q0w + (l & 31);
+  const bool wave_live = q0w < L, qv = q < L;
+  const bool drop = drop_thr(p.drop_p) != 0;
+  const float zs = drop ? 1.0f / (1.0f - p.drop_p) : 1.0f;
+  const int nkv = (L + 63) / 64;
+  const bf16* base = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64;
+
+  const __amdgpu_buffer_rsrc_t rkv = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.qkv + (int64_t)b * L * p.ld_qkv), 0, (int)(L * p.ld_qkv * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)(p.keymask + (int64_t)b * L), 0,
+                                                                      (int)(L * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(drop ? p.dropmask + (int64_t)bh * L * nkv : p.dropmask), 0, drop ? (int)(L * nkv * 8) : 0, 0x00020000);
+
+  bf16x8 qf[4], df[4];
+  const bf16* dob = p.dout + ((int64_t)b * L + q) * p.ld_do + hd * 64;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    uint4 u = qv ? *(const uint4*)(base + (int64_t)q * p.ld_qkv + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
+    qf[ks] = scale_frag(u, 0.125f);
+    uint4 v = qv ? *(const uint4*)(dob + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
+    df[ks] = *(bf16x8*)&v;
+  }
+  const float nlse = qv ? -p.lse[(int64_t)bh * L + q] : -__builtin_huge_valf();
+  const float dlt = qv ? p.delta[(int64_t)bh * L + q] : 0.f;
+  const float ndz = -dlt / zs;
+  f32x16 dq[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { dq[0][i] = 0.f; dq[1][i] = 0.f; }
+
+  // per tile: waves 0,1 -> K pieces (4 each), waves 2,3 -> V pieces; wave 0 also the mask row;
+  // every wave the keep words of its 32 query rows (4 B per lane)
+  auto issue = [&](int j) {
+    char* st = smem + (j % DQ_NS) * DQ_STAGE;
+    const int k0 = j * 64;
+    const int off_col = (w < 2 ? HD : 2 * HD) + hd * 64;
+    char* dst = st + (w < 2 ? 0 : DQ_TILE);
+#pragma unroll
+    for (int pc = 0; pc < 4; ++pc) {
+      const int piece = 4 * (w & 1) + pc;
+      const int row = 8 * piece + (l >> 3), c = (l & 7) ^ fsw(row);
+      dma16(rkv, dst + piece * 1024, (uint32_t)(((k0 + row) * p.ld_qkv + off_col + 8 * c) * 2));
+    }
+    if (w == 0 && l < 16) dma16(rm, st + 2 * DQ_TILE, (uint32_t)((k0 + 4 * l) * 4));
+    dma4(rk, st + 2 * DQ_TILE + 256 + w * 256, (uint32_t)((((q0w + (l >> 1)) * nkv + j) * 8) + 4 * (l & 1)));
+  };
+  auto wait_for = [&](int ahead) {
+    if (w == 0) {
+      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  };
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int j = 0; j < DQ_NS - 1 && j < nkv; ++j) issue(j);
+  for (int j = 0; j < nkv; ++j) {
+    const int ahead = nkv - 1 - j < DQ_NS - 2 ? nkv - 1 - j : DQ_NS - 2;
+    wait_for(ahead);
+    raw_barrier();
+    if (j + DQ_NS - 1 < nkv) issue(j + DQ_NS - 1);
+    const char* st = smem + (j % DQ_NS) * DQ_STAGE;
+    const char* Ks = st;
+    const char* Vs = st + DQ_TILE;
+    const float* mk = (const float*)(st + 2 * DQ_TILE);
+    const uint32_t* kwords = (const uint32_t*)(st + 2 * DQ_TILE + 256 + w * 256);  // [32 rows][lo, hi]
+    if (wave_live) {
+      // keep bits of this lane's query row, pre-shifted by 4h (as in attn_dq_kernel)
+      const uint64_t kw = drop ? ((uint64_t)kwords[2 * (l & 31) + 1] << 32 | kwords[2 * (l & 31)]) : ~0ull;
+      const uint64_t kwh = kw >> (4 * h);
+#pragma unroll
+      for (int st2 = 0; st2 < 2; ++st2) {
+        const uint32_t kw32 = (uint32_t)(kwh >> (32 * st2));
+        f32x16 sc, dp;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { sc[i] = nlse; dp[i] = ndz; }
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ks, 32 * st2, ks, l), qf[ks], sc, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Vs, 32 * st2, ks, l), df[ks], dp, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kc = (r & 3) + 8 * (r >> 2), kl = 32 * st2 + kc + 4 * h;
+          const float pr = __builtin_amdgcn_exp2f((sc[r] + mk[kl]) * LOG2E);
+          const float v = (kw32 & (1u << kc)) ? dp[r] * zs : -dlt;
+          sc[r] = pr * v;  // dS^T
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 sf = acc_frag(sc, s2);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt)
+            dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Ks, 32 * st2 + 16 * s2, 32 * dt, l), sf, dq[dt],
+                                                             0, 0, 0);
+        }
+      }
+    }
+  }
+  if (!qv) return;
+  bf16* ob = p.out + ((int64_t)b * L + q) * p.ld_out + hd * 64;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 v = {f2bf(dq[dt][4 * g] * 0.125f), f2bf(dq[dt][4 * g + 1] * 0.125f), f2bf(dq[dt][4 * g + 2] * 0.125f),
+                  f2bf(dq[dt][4 * g + 3] * 0.125f)};
+      *(bf16x4*)(ob + 32 * dt + 8 * g + 4 * h) = v;
+    }
+}
+
 static bool attn_dma() {
   const char* e = getenv("MMU_ATTN_DMA");  // 0 = register-staged kernels (A/B comparisons)
   return !(e && e[0] == '0');
@@ -666,7 +963,10 @@ static bool attn_dma() {
 
 void attention_bwd_launch(const AttnParams& p, hipStream_t s) {
   hipLaunchKernelGGL(attn_delta_kernel, dim3((p.L + 31) / 32, p.batch * p.heads), dim3(256), 0, s, p);
-  hipLaunchKernelGGL(attn_dq_kernel, dim3((p.L + 127) / 128, p.batch * p.heads), dim3(256), 0, s, p);
+  if (attn_dma())
+    hipLaunchKernelGGL(attn_dq_dma_kernel, dim3((p.L + 127) / 128, p.batch * p.heads), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(attn_dq_kernel, dim3((p.L + 127) / 128, p.batch * p.heads), dim3(256), 0, s, p);
   if (attn_dma())
     hipLaunchKernelGGL(attn_dkdv_dma_kernel, dim3((p.L + 63) / 64, p.batch * p.heads), dim3(128), 0, s, p);
   else
