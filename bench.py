@@ -20,6 +20,9 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(REPO, "multi-modal-uncertainty_amd"), REPO]
 
+# MIOpen reads its user db path when its first handle is created (first conv)
+os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                          "multi-modal-uncertainty_amd", "miopen_db"))
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -119,8 +122,10 @@ def main():
     from src import kernels as K
     from src.dp import GradBucketer, broadcast_parameters
 
-    # MIOpen solver search for the ResNet convs (first warm-up step pays it) when asked
-    torch.backends.cudnn.benchmark = os.environ.get("MMU_MIOPEN_FIND", "0") == "1"
+    # MIOpen solver choice for the ResNet convs: "find" mode over the find-db shipped in
+    # multi-modal-uncertainty_amd/miopen_db (per-rank batches 256/128/64/32 pre-searched on
+    # MI355X, so no search runs here); MMU_MIOPEN_FIND=0 = MIOpen's immediate-mode heuristics
+    torch.backends.cudnn.benchmark = os.environ.get("MMU_MIOPEN_FIND", "1") == "1"
     torch.manual_seed(1234)
     margs = make_args()
     model = MultimodalBertClf(margs).to(dev)

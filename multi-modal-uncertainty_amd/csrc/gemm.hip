@@ -556,6 +556,114 @@ __global__ __launch_bounds__(512) void gemm_pipe_kernel(GemmParams p) {
   epilogue_block<EPI, OUT_F32, 8>(p, z, slice, m0 + 128 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
 }
 
+// ================================================================ duo: 256x128, 4 waves, 2 blocks / CU
+// The 256x256 kernels hold one block per CU (128 KiB of LDS), so a tile's epilogue (HBM
+// stores, residual / aux reads, GELU) leaves the CU's matrix cores idle.  This variant
+// halves the block -- 256 x 128 tile, 4 waves of the same 128 x 64 per-wave tile -- and
+// its K step (BK = 32, 3-stage LDS-DMA ring = 72 KiB), so TWO blocks share a CU and one
+// block's epilogue overlaps the other's main loop.
+//  * K-major images: [rows][64 B], 16-B chunk c of row r at c ^ (((r >> 3) & 1) * 3)
+//    (enumerated conflict-free for the 16x16x32 operand's ds_read_b128 lane groups)
+//  * M/N-major images: [32 k][256 | 512 B] with the 32-B block ^ sw_mn(k) of the big kernel
+constexpr int DBK = 32;
+constexpr int D_A = 256 * DBK * 2;  // 16 KiB
+constexpr int D_B = 128 * DBK * 2;  //  8 KiB
+constexpr int D_STAGE = D_A + D_B;
+constexpr int D_NS = 3;
+
+static __device__ __forceinline__ int g64(int r) { return ((r >> 3) & 1) * 3; }
+
+// operand fragments of one 32-deep K step: K-major 64-B rows / M,N-major ROWB-byte k-rows
+static __device__ __forceinline__ bf16x8 d_frag_k(const char* s, int row0, int l) {
+  const int row = row0 + (l & 15), c = l >> 4;
+  return *(const bf16x8*)(s + row * 64 + ((c ^ g64(row)) << 4));
+}
+template <int ROWB>
+static __device__ __forceinline__ bf16x8 d_frag_mn(const char* s, int row0, int l) {
+  return s_frag<false, ROWB>(s, row0, 0, l);
+}
+
+// ROWS x 32 k operand tile into LDS, PIECES 1-KiB DMA pieces per wave (4 waves)
+template <bool KMAJ, int ROWS>
+static __device__ __forceinline__ void d_dma(char* s, __amdgpu_buffer_rsrc_t rsrc, int64_t ld, int64_t r0, int64_t k0,
+                                             int w, int l) {
+  constexpr int PIECES = ROWS * DBK * 2 / 1024 / 4;
+#pragma unroll
+  for (int i = 0; i < PIECES; ++i) {
+    const int piece = w * PIECES + i;
+    uint32_t src;
+    if (KMAJ) {  // 16 rows x 64 B per piece
+      const int row = piece * 16 + (l >> 2), c = (l & 3) ^ g64(row);
+      src = (uint32_t)(((r0 + row) * ld + k0 + 8 * c) * 2);
+    } else {     // 1024 / (2 ROWS) k-rows per piece
+      constexpr int KPP = 1024 / (2 * ROWS), UPR = 2 * ROWS / 16;  // k-rows per piece, 16-B units per k-row
+      const int kr = piece * KPP + l / UPR, j = l % UPR;
+      const int b = (j >> 1) ^ sw_mn(kr);
+      src = (uint32_t)(((k0 + kr) * ld + r0 + 16 * b + 8 * (j & 1)) * 2);
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (MMU_LDS(void)*)(s + piece * 1024), 16, src, 0, 0, 0);
+  }
+}
+
+template <bool AK, bool BKM, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void gemm_duo_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[D_NS * D_STAGE];
+  const int t = threadIdx.x, l = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  int tm, tn, slice;
+  int64_t z;
+  block_tile(p, z, slice, tm, tn);
+  const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * 128;
+  const int64_t a_bytes = (AK ? p.M * p.lda : p.K * p.lda) * 2;
+  const int64_t b_bytes = (BKM ? p.N * p.ldb : p.K * p.ldb) * 2;
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + z * p.sA), 0, (int)(uint32_t)a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.B + z * p.sB), 0, (int)(uint32_t)b_bytes, 0x00020000);
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t kb = (int64_t)slice * p.kchunk;
+  const int64_t ke = kb + p.kchunk < p.K ? kb + p.kchunk : p.K;
+  const int nk = (int)((ke - kb + DBK - 1) / DBK);
+  auto issue = [&](int kt) {
+    char* st = smem + (kt % D_NS) * D_STAGE;
+    const int64_t k0 = kb + (int64_t)kt * DBK;
+    d_dma<AK, 256>(st, ra, p.lda, m0, k0, w, l);
+    d_dma<BKM, 128>(st + D_A, rb, p.ldb, n0, k0, w, l);
+  };
+  // DMAs per wave per stage: A 4 + B 2
+  for (int kt = 0; kt < D_NS - 1 && kt < nk; ++kt) issue(kt);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + D_NS - 1 < nk) issue(kt + D_NS - 1);  // into the stage of kt-1: every wave is past it
+    const char* sa = smem + (kt % D_NS) * D_STAGE;
+    const char* sb = sa + D_A;
+    bf16x8 fb[4], fa[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      fb[i] = BKM ? d_frag_k(sb, 64 * wn + 16 * i, l) : d_frag_mn<256>(sb, 64 * wn + 16 * i, l);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      fa[j] = AK ? d_frag_k(sa, 128 * wm + 16 * j, l) : d_frag_mn<512>(sa, 128 * wm + 16 * j, l);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
+  }
+  __builtin_amdgcn_s_barrier();  // every wave's last fragment reads are done: the ring is epilogue scratch
+  asm volatile("" ::: "memory");
+  epilogue_block<EPI, OUT_F32, 8>(p, z, slice, m0 + 128 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
+}
+
 // ---------------------------------------------------------------- launch
 // MMU_GEMM_PIPE=1 selects the 8-phase kernel (read per launch, for A/B comparisons).  On the
 // BERT shapes it measures within +-3 % of the 2-stage kernel and 10 % slower on the long-K
@@ -565,10 +673,21 @@ static bool use_pipe() {
   return e && e[0] == '1';
 }
 
+// MMU_GEMM_DUO=1 selects the 256x128 two-blocks-per-CU kernel (A/B while it is evaluated)
+static bool use_duo() {
+  const char* e = getenv("MMU_GEMM_DUO");
+  return e && e[0] == '1';
+}
+
 template <bool AK, bool BKM, int EPI, bool F32>
 static void launch_t(const GemmParams& p, bool big, int batch, hipStream_t s) {
   dim3 grid(p.tiles_m * p.tiles_n, p.splitk, batch);
-  if (big && use_pipe()) hipLaunchKernelGGL((gemm_pipe_kernel<AK, BKM, EPI, F32>), grid, dim3(512), 0, s, p);
+  if (big && use_duo()) {
+    GemmParams q = p;
+    q.tiles_n = (int)((p.N + 127) / 128);
+    dim3 g2(q.tiles_m * q.tiles_n, q.splitk, batch);
+    hipLaunchKernelGGL((gemm_duo_kernel<AK, BKM, EPI, F32>), g2, dim3(256), 0, s, q);
+  } else if (big && use_pipe()) hipLaunchKernelGGL((gemm_pipe_kernel<AK, BKM, EPI, F32>), grid, dim3(512), 0, s, p);
   else if (big) hipLaunchKernelGGL((gemm_big_kernel<AK, BKM, EPI, F32>), grid, dim3(512), 0, s, p);
   else hipLaunchKernelGGL((gemm_small_kernel<AK, BKM, EPI, F32>), grid, dim3(256), 0, s, p);
 }
