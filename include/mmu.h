@@ -101,12 +101,17 @@ int mmu_attention_fwd(const void* QKV, int64_t ld_qkv, const float* keymask,
                       int64_t batch, int64_t L, int64_t heads,
                       float drop_p, uint64_t seed, uint64_t* dropmask, mmu_stream_t stream);
 /* dQKV [rows, ld_dqkv] bf16 from dO; `delta` workspace [batch*heads, L] f32;
- * dropmask = the forward's (required when drop_p > 0). */
+ * dropmask = the forward's (required when drop_p > 0).
+ * dbias_parts (may be NULL): f32 [(ceil(L/128) + 2 ceil(L/64)) * batch, heads*64] receives
+ * per-block column sums of dQ (rows [0, nqb*batch)), dK (next nkb*batch rows) and dV (last
+ * nkb*batch rows), every element written; summing each row range (mmu_colsum_reduce) gives
+ * the Q / K / V bias gradients without another pass over dQKV. */
 int mmu_attention_bwd(const void* QKV, int64_t ld_qkv, const float* keymask,
                       const void* O, int64_t ld_o, const void* dO, int64_t ld_do,
                       const float* LSE, float* delta, void* dQKV, int64_t ld_dqkv,
                       int64_t batch, int64_t L, int64_t heads,
-                      float drop_p, uint64_t seed, const uint64_t* dropmask, mmu_stream_t stream);
+                      float drop_p, uint64_t seed, const uint64_t* dropmask, float* dbias_parts,
+                      mmu_stream_t stream);
 
 /* ------------------------------------------------------------------ LayerNorm
  * y = LN(x) * w + b over the last dim (768), eps; x, y bf16 [rows, H]; saves

@@ -814,6 +814,34 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
       }
     }
   }
+  if (p.colsum) {  // bias-gradient partials of K and V: this block's 64 keys, per column
+    // each lane holds ONE column (32 dt + l&31) for 16 keys: in-lane sum + the other half-wave
+    float* red = (float*)smem;  // [2 waves][K 64 | V 64]
+    raw_barrier();              // every wave is done with the ring
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      float sk = 0.f, sv = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const bool ok = k0w + (r & 3) + 8 * (r >> 2) + 4 * h < L;
+        sk += ok ? dk[dt][r] : 0.f;
+        sv += ok ? dv[dt][r] : 0.f;
+      }
+      sk += __shfl_xor(sk, 32, 64);
+      sv += __shfl_xor(sv, 32, 64);
+      if (h == 0) {
+        red[w * 128 + 32 * dt + l] = sk * 0.125f;
+        red[w * 128 + 64 + 32 * dt + l] = sv;
+      }
+    }
+    raw_barrier();
+    if (t < 128) {
+      const int nqb = (L + 127) / 128, nkb = (L + 63) / 64, B = p.batch;
+      const float v = red[t] + red[128 + t];
+      const int64_t row = (int64_t)nqb * B + (t < 64 ? 0 : (int64_t)nkb * B) + (int64_t)blockIdx.x * B + b;
+      p.colsum[row * HD + hd * 64 + (t & 63)] = v;
+    }
+  }
   if (!wave_live) return;
   bf16* outb = p.out + (int64_t)b * L * p.ld_out + hd * 64;
 #pragma unroll
@@ -944,6 +972,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
       }
     }
   }
+  if (p.colsum) {  // bias-gradient partials of Q: this block's 128 queries, per column
+    // lane (query l&31) holds columns 32 dt + 8 g + 4 h + e: rows to LDS, then column sums
+    float* rows = (float*)smem;  // [4 waves][32 queries][64 cols]
+    raw_barrier();               // every wave is done with the ring
+    float* mine = rows + w * 32 * 64 + (l & 31) * 64;
+    const float sc = qv ? 0.125f : 0.f;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *(float4*)(mine + 32 * dt + 8 * g + 4 * h) =
+            make_float4(dq[dt][4 * g] * sc, dq[dt][4 * g + 1] * sc, dq[dt][4 * g + 2] * sc, dq[dt][4 * g + 3] * sc);
+    raw_barrier();
+    if (t < 64) {
+      float v = 0.f;
+      for (int r = 0; r < 128; ++r) v += rows[r * 64 + t];
+      p.colsum[((int64_t)blockIdx.x * p.batch + b) * HD + hd * 64 + t] = v;
+    }
+  }
   if (!qv) return;
   bf16* ob = p.out + ((int64_t)b * L + q) * p.ld_out + hd * 64;
 #pragma unroll
@@ -960,6 +1007,8 @@ static bool attn_dma() {
   const char* e = getenv("MMU_ATTN_DMA");  // 0 = register-staged kernels (A/B comparisons)
   return !(e && e[0] == '0');
 }
+
+bool attention_bwd_fuses_colsum() { return attn_dma(); }
 
 void attention_bwd_launch(const AttnParams& p, hipStream_t s) {
   hipLaunchKernelGGL(attn_delta_kernel, dim3((p.L + 31) / 32, p.batch * p.heads), dim3(256), 0, s, p);

@@ -210,7 +210,7 @@ int mmu_attention_fwd(const void* QKV, int64_t ld_qkv, const float* keymask, voi
 int mmu_attention_bwd(const void* QKV, int64_t ld_qkv, const float* keymask, const void* O, int64_t ld_o,
                       const void* dO, int64_t ld_do, const float* LSE, float* delta, void* dQKV, int64_t ld_dqkv,
                       int64_t batch, int64_t L, int64_t heads, float drop_p, uint64_t seed,
-                      const uint64_t* dropmask, mmu_stream_t stream) {
+                      const uint64_t* dropmask, float* dbias_parts, mmu_stream_t stream) {
   if (!QKV || !keymask || !O || !dO || !LSE || !delta || !dQKV) return fail("mmu_attention_bwd: null pointer");
   if ((uint32_t)(drop_p * 65536.0f + 0.5f) != 0 && !dropmask)
     return fail("mmu_attention_bwd: dropout needs the forward's dropmask");
@@ -222,6 +222,8 @@ int mmu_attention_bwd(const void* QKV, int64_t ld_qkv, const float* keymask, con
   p.dout = (const bf16*)dO; p.ld_do = ld_do; p.lse = (float*)LSE; p.delta = delta; p.out = (bf16*)dQKV;
   p.ld_out = ld_dqkv; p.batch = (int)batch; p.L = (int)L; p.heads = (int)heads; p.drop_p = drop_p; p.seed = seed;
   p.dropmask = (uint64_t*)dropmask;
+  p.colsum = dbias_parts;
+  if (dbias_parts && !attention_bwd_fuses_colsum()) return fail("mmu_attention_bwd: dbias_parts need MMU_ATTN_DMA != 0");
   attention_bwd_launch(p, (hipStream_t)stream);
   return check_launch("mmu_attention_bwd");
 }

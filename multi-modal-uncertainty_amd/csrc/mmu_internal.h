@@ -52,12 +52,14 @@ struct AttnParams {
   bf16* out;   // O (fwd) or dQKV (bwd)
   int64_t ld_out;
   uint64_t* dropmask;  // [batch*heads][L][ceil(L/64)] keep bits: written by fwd, read by bwd
+  float* colsum;       // bwd (optional): dQKV column-sum partials, see mmu_attention_bwd
   int batch, L, heads;
   float drop_p;
   uint64_t seed;
 };
 void attention_fwd_launch(const AttnParams& p, hipStream_t s);
 void attention_bwd_launch(const AttnParams& p, hipStream_t s);
+bool attention_bwd_fuses_colsum();
 
 void layernorm_fwd_launch(const bf16* X, const float* w, const float* b, bf16* Y, float* mean, float* rstd,
                           int64_t rows, int64_t H, float eps, int64_t group_rows, int64_t pstride, hipStream_t s);

@@ -35,7 +35,7 @@ SIGNATURES = {
     "mmu_attention_fwd": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_f32, c_u64, c_vp,
                                   c_vp]),
     "mmu_attention_bwd": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
-                                  c_i64, c_i64, c_i64, c_f32, c_u64, c_vp, c_vp]),
+                                  c_i64, c_i64, c_i64, c_f32, c_u64, c_vp, c_vp, c_vp]),
     "mmu_layernorm_fwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_i64, c_i64, c_vp]),
     "mmu_layernorm_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp, c_vp, c_vp,
                                   c_i64, c_i64, c_i64, c_vp]),

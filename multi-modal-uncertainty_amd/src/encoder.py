@@ -165,12 +165,14 @@ def layer_backward(lw, saved, dY, keymask, B, L, p_attn, p_hid, seeds, wgrad):
     # ---- attention + fused QKV
     dqkv = torch.empty(M, 3 * HID, dtype=bf16, device=dev)
     delta = torch.empty(B * HEADS, L, dtype=torch.float32, device=dev)
-    K.attention_bwd(qkv, keymask, O, dO, lse, delta, dqkv, B, L, HEADS, p_attn, seeds[0], dmask)
+    # the attention backward also emits per-block column sums of dQ / dK / dV (bias grads)
+    dbp = K.attention_dbias_parts(B, L, HEADS, dev) if wgrad else None
+    K.attention_bwd(qkv, keymask, O, dO, lse, delta, dqkv, B, L, HEADS, p_attn, seeds[0], dmask, dbp)
     if wgrad:
         def wqkv():
-            K.colsum_bf16(dqkv, lw.g_bqkv, accumulate=True)
+            K.attention_dbias_reduce(dbp, B, L, lw.g_bqkv, HEADS)
             K.gemm(dqkv, 3 * HID, False, X, HID, False, lw.g_wqkv, HID, 3 * HID, HID, M, epi=acc)
-        side.run(wqkv, dqkv, X)
+        side.run(wqkv, dqkv, X, dbp)
     dX = torch.empty(M, HID, dtype=bf16, device=dev)
     K.gemm(dqkv, 3 * HID, True, lw.wqkv16, HID, False, dX, HID, M, HID, 3 * HID,
            epi=K.epilogue(K.EPI_ADD_RES, residual=dS1))

@@ -126,9 +126,27 @@ def attention_fwd(qkv, keymask, O, lse, batch, L, heads=12, drop_p=0.0, seed=0, 
            heads, float(drop_p), int(seed), _ptr(dropmask) if dropmask is not None else None, _stream(qkv))
 
 
-def attention_bwd(qkv, keymask, O, dO, lse, delta, dqkv, batch, L, heads=12, drop_p=0.0, seed=0, dropmask=None):
+def attention_dbias_parts(batch, L, heads=12, device=None):
+    """Scratch for the fused Q/K/V bias-gradient column sums of attention_bwd."""
+    nqb, nkb = (L + 127) // 128, (L + 63) // 64
+    return torch.empty((nqb + 2 * nkb) * batch, heads * 64, dtype=torch.float32, device=device)
+
+
+def attention_dbias_reduce(parts, batch, L, g_bqkv, heads=12):
+    """g_bqkv [3 * heads * 64] += the column sums held in `parts` (Q | K | V row ranges)."""
+    nqb, nkb = (L + 127) // 128, (L + 63) // 64
+    H = heads * 64
+    r0, r1 = nqb * batch, (nqb + nkb) * batch
+    colsum_reduce(parts[:r0], g_bqkv[:H], accumulate=True)
+    colsum_reduce(parts[r0:r1], g_bqkv[H:2 * H], accumulate=True)
+    colsum_reduce(parts[r1:], g_bqkv[2 * H:], accumulate=True)
+
+
+def attention_bwd(qkv, keymask, O, dO, lse, delta, dqkv, batch, L, heads=12, drop_p=0.0, seed=0, dropmask=None,
+                  dbias_parts=None):
     """`dropmask` = the buffer the forward filled (required when drop_p > 0); `seed` is
-    kept for signature symmetry with the forward."""
+    kept for signature symmetry with the forward; `dbias_parts` (attention_dbias_parts)
+    collects the Q/K/V bias-gradient column sums."""
     _dev_check(qkv, keymask, O, dO, lse, delta, dqkv)
     if dropmask is not None:
         _dev_check(dropmask)
@@ -136,7 +154,7 @@ def attention_bwd(qkv, keymask, O, dO, lse, delta, dqkv, batch, L, heads=12, dro
             raise ValueError("attention_bwd: dropmask too small / not contiguous")
     N.call("mmu_attention_bwd", _ptr(qkv), qkv.stride(0), _ptr(keymask), _ptr(O), O.stride(0), _ptr(dO), dO.stride(0),
            _ptr(lse), _ptr(delta), _ptr(dqkv), dqkv.stride(0), batch, L, heads, float(drop_p), int(seed),
-           _ptr(dropmask) if dropmask is not None else None, _stream(qkv))
+           _ptr(dropmask) if dropmask is not None else None, _ptr(dbias_parts), _stream(qkv))
 
 
 def layernorm_fwd(X, w, b, Y, mean, rstd, eps=1e-12, group_rows=0, param_stride=0):

@@ -507,3 +507,25 @@ def test_batchnorm_eval_and_module(dev):
     close(xb.grad, xr.grad, atol_frac=3e-2)
     torch.testing.assert_close(bn.weight.grad, ref.weight.grad, rtol=3e-2, atol=3e-2 * ref.weight.grad.abs().max().item())
     torch.testing.assert_close(bn.bias.grad, ref.bias.grad, rtol=3e-2, atol=3e-2 * ref.bias.grad.abs().max().item())
+
+
+@pytest.mark.parametrize("B,L,p", [(2, 130, 0.0), (3, 513, 0.1), (1, 17, 0.0)])
+def test_attention_bwd_fused_bias_grad(dev, B, L, p):
+    """the Q/K/V bias-gradient column sums emitted by the backward kernels equal the
+    column sums of the dQKV they write (f32 accumulators vs bf16-stored rows)"""
+    k = K()
+    qkv, km = make_attn_inputs(dev, B, L, pad=True, seed=21, scale=1.0)
+    O = torch.empty(B * L, 768, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(B * 12, L, device=dev)
+    dm = k.dropmask_empty(B, L, 12, dev) if p > 0 else None
+    k.attention_fwd(qkv, km, O, lse, B, L, drop_p=p, seed=5, dropmask=dm)
+    dO = rnd(B * L, 768, dev=dev, seed=22)
+    dqkv = torch.zeros(B * L, 2304, dtype=torch.bfloat16, device=dev)
+    delta = torch.empty(B * 12, L, device=dev)
+    parts = k.attention_dbias_parts(B, L, 12, dev).fill_(float("nan"))  # every element must be written
+    k.attention_bwd(qkv, km, O, dO, lse, delta, dqkv, B, L, drop_p=p, seed=5, dropmask=dm, dbias_parts=parts)
+    assert not torch.isnan(parts).any()
+    g = torch.full((2304,), 0.5, device=dev)
+    k.attention_dbias_reduce(parts, B, L, g)
+    ref = dqkv.float().sum(0) + 0.5
+    torch.testing.assert_close(g, ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
