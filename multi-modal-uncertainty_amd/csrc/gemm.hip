@@ -744,7 +744,7 @@ void splitk_reduce_launch(const GemmParams& p, int batch, hipStream_t s) {
 // ------------------------------------------------------------------ column sums
 // grid (ceil(N/256), ceil(parts/64)): each thread sums 64 partial rows of one column and adds
 // the result into out with one float atomic (out zeroed first when not accumulating)
-constexpr int COLSUM_ROWS = 64;
+constexpr int COLSUM_ROWS = 16;  // 16 rows per thread: enough blocks to fill the chip for 1-2 K partial rows
 __global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restrict__ part, int64_t parts, int64_t N,
                                                             float* __restrict__ out) {
   const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -752,6 +752,7 @@ __global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restr
   const int64_t r0 = (int64_t)blockIdx.y * COLSUM_ROWS;
   const int64_t r1 = r0 + COLSUM_ROWS < parts ? r0 + COLSUM_ROWS : parts;
   float s = 0.f;
+#pragma unroll 8
   for (int64_t r = r0; r < r1; ++r) s += part[r * N + n];
   atomicAdd(out + n, s);
 }

@@ -24,7 +24,7 @@ import torch.nn.functional as F
 from . import kernels as K
 from .encoder import BertLayerFunction, LayerWeights, layer_forward
 from .params import ParamStore
-from .resnet import resnet152_trunk
+from .resnet import StoreConv2d, resnet152_trunk
 
 BERT_CONFIGS = {
     # name: (layers, hidden, heads, intermediate, vocab, max_pos, type_vocab)
@@ -333,11 +333,16 @@ class MultimodalBertEncoder(nn.Module):
             p = f"{prefix}encoder.layer.{i}."
             compute += [f"{p}attention.self.{s}.weight" for s in ("query", "key", "value")]
             compute += [f"{p}attention.output.dense.weight", f"{p}intermediate.dense.weight", f"{p}output.dense.weight"]
+        # bf16 conv filters for the trunk (read by StoreConv2d instead of an autocast cast per step)
+        compute += [n for n in res if named[n].dim() == 4]
         return [(n, named[n]) for n in order], compute
 
     def _attach_store(self, store, prefix):
         self._store, self._prefix = store, prefix
         self._lw = [LayerWeights(store, f"{prefix}encoder.layer.{i}.", lyr) for i, lyr in enumerate(self.encoder.layer)]
+        for name, m in self.img_encoder.named_modules(prefix=f"{prefix}img_encoder"):
+            if isinstance(m, StoreConv2d) and f"{name}.weight" in store.coffsets:
+                m.attach_compute(store, f"{name}.weight")
 
     def _refresh_views(self):
         for lw in self._lw:

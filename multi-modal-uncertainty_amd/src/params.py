@@ -139,12 +139,17 @@ class ParamStore:
         return tuple(self.params[n]._version for n in self.compute_names)
 
     def sync_compute(self):
+        """bf16 copy of every compute tensor in its STORAGE order (conv weights: O, kh, kw, I),
+        the order the fused optimizer writes them in."""
         with torch.no_grad():
             for n in self.compute_names:
-                c = self.coffsets[n]
-                p = self.params[n]
-                self.compute[c:c + p.numel()].copy_(p.detach().reshape(-1))
+                c, o, k = self.coffsets[n], self.offsets[n], self.params[n].numel()
+                self.compute[c:c + k].copy_(self.flat[o:o + k])
         self._versions = self._current_versions()
+
+    def compute_of(self, name):
+        """bf16 copy of one tensor, shaped like the parameter (conv weights channels-last)."""
+        return self._shaped(self.compute, self.coffsets[name], self.params[name])
 
     def maybe_sync_compute(self):
         """bf16 copies follow the masters; only an out-of-band write (version bump) needs a resync."""

@@ -88,6 +88,59 @@ class BatchNorm2d(nn.BatchNorm2d):
         return torch.relu(y) if relu else y
 
 
+class _ConvBF16(torch.autograd.Function):
+    """Conv2d on the bf16 filter copy kept by the parameter store (updated by the fused
+    optimizer), so no per-step autocast cast of the f32 filter; the backward adds MIOpen's
+    bf16 filter gradient straight into the f32 gradient view (one kernel instead of a cast
+    plus an AccumulateGrad add)."""
+
+    @staticmethod
+    def forward(ctx, x, w, w16, stride, padding):
+        ctx.save_for_backward(x, w16)
+        ctx.w, ctx.conf = w, (stride, padding)
+        return torch.ops.aten.convolution(x, w16, None, stride, padding, (1, 1), False, (0, 0), 1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w16 = ctx.saved_tensors
+        stride, padding = ctx.conf
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w16, None, stride, padding, (1, 1), False, (0, 0), 1,
+                                                       (need_x, need_w, False))
+        rw = None
+        if need_w:
+            if ctx.w.grad is not None:
+                ctx.w.grad.add_(dw)
+            else:
+                rw = dw.float()
+        return dx, rw, None, None, None
+
+
+class StoreConv2d(nn.Conv2d):
+    """nn.Conv2d (same parameters / state_dict) that, once the model's parameter store
+    holds a bf16 copy of its filter, convolves bf16 channels-last inputs with that copy.
+    The copy's freshness is the store's business: MultimodalBertEncoder._prepare() runs
+    check_views / maybe_sync_compute before every forward."""
+
+    _src = None
+
+    def attach_compute(self, store, name):
+        import weakref
+        self._src = (weakref.ref(store), name)
+
+    def forward(self, x):
+        src = self._src
+        if (src is not None and x.is_cuda and x.dtype == torch.bfloat16 and self.bias is None and self.groups == 1
+                and self.dilation == (1, 1)):
+            store = src[0]()
+            if store is not None:
+                w16 = store.compute_of(src[1])
+                return _ConvBF16.apply(x.contiguous(memory_format=torch.channels_last), self.weight, w16,
+                                       self.stride, self.padding)
+        return super().forward(x)
+
+
 class FusedReLU(nn.ReLU):
     """The stem's ReLU slot (torchvision child index 2): the preceding BatchNorm2d
     already applied it, so this is the identity."""
@@ -100,16 +153,16 @@ class Bottleneck(nn.Module):
     def __init__(self, cin, width, stride):
         super().__init__()
         cout = width * 4
-        self.conv1 = nn.Conv2d(cin, width, 1, bias=False)
+        self.conv1 = StoreConv2d(cin, width, 1, bias=False)
         self.bn1 = BatchNorm2d(width)
-        self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
+        self.conv2 = StoreConv2d(width, width, 3, stride=stride, padding=1, bias=False)
         self.bn2 = BatchNorm2d(width)
-        self.conv3 = nn.Conv2d(width, cout, 1, bias=False)
+        self.conv3 = StoreConv2d(width, cout, 1, bias=False)
         self.bn3 = BatchNorm2d(cout)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = None
         if stride != 1 or cin != cout:
-            self.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, stride=stride, bias=False), BatchNorm2d(cout))
+            self.downsample = nn.Sequential(StoreConv2d(cin, cout, 1, stride=stride, bias=False), BatchNorm2d(cout))
 
     def forward(self, x):
         skip = x if self.downsample is None else self.downsample(x)
@@ -122,7 +175,7 @@ def resnet152_trunk(blocks=(3, 8, 36, 3)):
     """Sequential(conv1, bn1, relu, maxpool, layer1..layer4) -> [B,2048,H/32,W/32]."""
     stem_bn = BatchNorm2d(64)
     stem_bn.fused_relu = True
-    mods = [nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False), stem_bn, FusedReLU(inplace=True),
+    mods = [StoreConv2d(3, 64, 7, stride=2, padding=3, bias=False), stem_bn, FusedReLU(inplace=True),
             nn.MaxPool2d(3, 2, 1)]
     cin = 64
     for i, (width, n) in enumerate(zip((64, 128, 256, 512), blocks)):
