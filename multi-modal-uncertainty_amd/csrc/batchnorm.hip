@@ -20,7 +20,7 @@
 // f32 partials are reduced over the block in LDS and stored as one (sum, sum2) pair per
 // channel and block -- no atomics: ~1-3 K blocks x 2C float atomics on the same addresses
 // serialise in the L2 atomic units (measured 4-10x slower than the apply pass).  The
-// finalize sums the block partials per channel in f64 (8 slices per channel + LDS).
+// finalize sums the block partials per channel in f64 (32 slices per channel + LDS).
 #include "mmu_common.h"
 #include "mmu_internal.h"
 
@@ -69,19 +69,22 @@ static __device__ __forceinline__ void bn_block_reduce(const BnGeom& g, int C, c
   }
 }
 
-// sum the nparts block partials of 16 channels per block: 8 slices x 32 (channel, component)
-// columns, f64, then LDS; returns true (and the two totals) in the thread that owns channel c
+// sum the nparts block partials of 4 channels per block: 32 slices x 8 (channel, component)
+// columns, f64, then LDS; returns true (and the two totals) in the thread that owns channel c.
+// (32 slices: the finalize is a dependent-load chain of nparts / slices loads per thread;
+// with 8 slices it cost ~9 us per BN, 2.9 ms per step over the trunk's 310 launches.)
+constexpr int BN_FIN_CH = 4;
 static __device__ __forceinline__ bool bn_sum_parts(const float2* __restrict__ part, int nparts, int C, int& c,
                                                     double& s1, double& s2) {
-  __shared__ double red[8][32];
-  const int t = threadIdx.x, col = t & 31, sl = t >> 5;
-  c = blockIdx.x * 16 + (col >> 1);
+  __shared__ double red[32][2 * BN_FIN_CH];
+  const int t = threadIdx.x, col = t & (2 * BN_FIN_CH - 1), sl = t / (2 * BN_FIN_CH);
+  c = blockIdx.x * BN_FIN_CH + (col >> 1);
   const int comp = col & 1;
   double acc = 0.0;
   if (c < C) {
     const float* p = (const float*)part + 2 * (int64_t)c + comp;
 #pragma unroll 4
-    for (int k = sl; k < nparts; k += 8) acc += (double)p[(int64_t)k * 2 * C];
+    for (int k = sl; k < nparts; k += 32) acc += (double)p[(int64_t)k * 2 * C];
   }
   red[sl][col] = acc;
   __syncthreads();
@@ -89,7 +92,7 @@ static __device__ __forceinline__ bool bn_sum_parts(const float2* __restrict__ p
   s1 = 0.0;
   s2 = 0.0;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { s1 += red[k][col]; s2 += red[k][col + 1]; }
+  for (int k = 0; k < 32; ++k) { s1 += red[k][col]; s2 += red[k][col + 1]; }
   return true;
 }
 
@@ -125,8 +128,8 @@ __global__ __launch_bounds__(BN_THREADS) void bn_fwd_finalize_kernel(
     if (!bn_sum_parts(part, nparts, C, c, s1, s2)) return;
   } else {
     const int t = threadIdx.x;
-    if (t >= 16) return;
-    c = blockIdx.x * 16 + t;
+    if (t >= BN_FIN_CH) return;
+    c = blockIdx.x * BN_FIN_CH + t;
     if (c >= C) return;
   }
   double mean, var;
@@ -304,7 +307,7 @@ void batchnorm_fwd_launch(const BnFwdParams& q, hipStream_t s) {
   float2* part = (float2*)(coef + ((3 * q.C + 3) & ~3));
   if (q.training)
     hipLaunchKernelGGL(bn_stats_kernel, G.grid, dim3(BN_THREADS), 0, s, q.X, q.rows, q.C, G.CH, G.rpb, part);
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((q.C + 15) / 16), dim3(BN_THREADS), 0, s, part, nparts, q.rows, q.C,
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((q.C + BN_FIN_CH - 1) / BN_FIN_CH), dim3(BN_THREADS), 0, s, part, nparts, q.rows, q.C,
                      q.w, q.b, q.rmean, q.rvar, q.training, q.momentum, q.eps, q.smean, q.sinvstd, q.nbt, coef);
   const bool sk = q.skip != nullptr;
 #define BN_APPLY(SK, RL)                                                                                    \
@@ -328,7 +331,7 @@ void batchnorm_bwd_launch(const BnBwdParams& q, hipStream_t s) {
   else
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<false>), G.grid, dim3(BN_THREADS), 0, s, q.dY, q.Y, q.X, q.rows, q.C,
                        G.CH, G.rpb, q.smean, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((q.C + 15) / 16), dim3(BN_THREADS), 0, s, part, nparts, q.rows, q.C,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((q.C + BN_FIN_CH - 1) / BN_FIN_CH), dim3(BN_THREADS), 0, s, part, nparts, q.rows, q.C,
                      q.w, q.smean, q.sinvstd, q.dw, q.db, coef);
   const bool ds = q.dS != nullptr;
 #define BN_BAPPLY(RL, DS)                                                                                     \

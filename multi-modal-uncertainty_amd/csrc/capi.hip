@@ -232,7 +232,7 @@ int mmu_layernorm_fwd(const void* X, const float* w, const float* b, void* Y, fl
                       int64_t H, float eps, int64_t group_rows, int64_t param_stride, mmu_stream_t stream) {
   if (!X || !w || !b || !Y) return fail("mmu_layernorm_fwd: null pointer");
   if ((mean == nullptr) != (rstd == nullptr)) return fail("mmu_layernorm_fwd: mean/rstd must both be given or NULL");
-  if (rows <= 0 || H % 256 || H > 1024) return fail("mmu_layernorm_fwd: H=%ld must be 256/512/768/1024", H);
+  if (rows <= 0 || H <= 0 || H % 256 || H > 1024) return fail("mmu_layernorm_fwd: H=%ld must be 256/512/768/1024", H);
   if (group_rows <= 0) group_rows = rows;
   if (param_stride < 0) return fail("mmu_layernorm_fwd: bad param_stride");
   layernorm_fwd_launch((const bf16*)X, w, b, (bf16*)Y, mean, rstd, rows, H, eps, group_rows, param_stride,
@@ -244,7 +244,7 @@ int mmu_layernorm_bwd(const void* dY, const void* X, const float* mean, const fl
                       void* dXdrop, float drop_p, uint64_t seed, float* part_dw, float* part_db, float* part_dbias,
                       int64_t rows, int64_t H, int64_t rows_per_part, mmu_stream_t stream) {
   if (!dY || !X || !mean || !rstd || !w || !dX) return fail("mmu_layernorm_bwd: null pointer");
-  if (rows <= 0 || H % 256 || H > 1024 || rows_per_part <= 0) return fail("mmu_layernorm_bwd: bad shape");
+  if (rows <= 0 || H <= 0 || H % 256 || H > 1024 || rows_per_part <= 0) return fail("mmu_layernorm_bwd: bad shape");
   if (drop_p < 0.f || drop_p >= 1.f) return fail("mmu_layernorm_bwd: drop_p out of range");
   layernorm_bwd_launch((const bf16*)dY, (const bf16*)X, mean, rstd, w, (bf16*)dX, (bf16*)dXdrop, drop_p, seed, part_dw,
                        part_db, part_dbias, rows, H, rows_per_part, (hipStream_t)stream);
