@@ -65,8 +65,11 @@ typedef struct mmu_epilogue {
   float drop_p;             /* BIAS_DROP_RES                                            */
   uint64_t seed;            /* dropout stream: element (z, m, n) uses counter (z*M+m)*N+n */
   float* workspace;         /* optional f32 scratch: lets a STORE/f32/no-bias product split K
-                               over workgroups (weight gradients); slabs summed in slice
-                               order, so results stay deterministic                     */
+                               over workgroups (weight gradients), and lets any 256x256-tile
+                               product run the M-tile rows of a partial last wave of tiles
+                               as a split-K tail (same epilogue, same dropout counters);
+                               slabs summed in slice order, so results stay deterministic.
+                               Stream-ordered: one workspace per stream.                */
   int64_t workspace_floats;
 } mmu_epilogue;
 

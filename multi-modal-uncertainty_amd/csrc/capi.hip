@@ -8,6 +8,7 @@
 #include <vector>
 #include "mmu_internal.h"
 #include <cstdlib>
+#include <cmath>
 
 using namespace mmu;
 
@@ -27,6 +28,19 @@ static int check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail("%s: launch failed: %s", what, hipGetErrorString(e));
   return 0;
+}
+
+// compute units of the current device (the wave size of a launch: gemm tail peeling)
+static int cu_count() {
+  static int cache[64] = {};
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return 256;
+  if (!cache[d]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || n <= 0) n = 256;
+    cache[d] = n;
+  }
+  return cache[d];
 }
 
 // ------------------------------------------------------------------ timing of mmu_gemm
@@ -148,6 +162,37 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
       p.ws = epi->workspace;
     }
   }
+  // split-K tail: peel the M-tile rows of a partial last wave of big tiles (see gemm.hip
+  // gemm_tail_kernel).  Opt-in (MMU_GEMM_TAIL=1): on the BERT shapes it measured no faster
+  // than the plain launch (profiles/r1_gemm_tail_ab.txt): a partial last wave of 3-12 tiles
+  // runs at its uncontended rate and costs about what the extra launches do
+  int64_t tail_m0 = 0;
+  int tail_s = 0;
+  if (big && p.splitk == 1 && epi && epi->workspace) {
+    const char* te = getenv("MMU_GEMM_TAIL");
+    const int cus = cu_count();
+    const int64_t per_row = batch * p.tiles_n;  // tiles per M-tile row (all batch items)
+    const int64_t tiles = per_row * p.tiles_m;
+    const int64_t rem = tiles % cus;
+    if (te && te[0] == '1' && tiles > cus && rem > 0 && rem * 4 <= cus) {
+      const int64_t peel = (rem + per_row - 1) / per_row;
+      const int64_t m0 = (int64_t)(p.tiles_m - peel) * 256;
+      const int64_t mt = M - m0, kit = (K + 63) / 64;
+      // slices: balance the slice's main loop (~1.4 us per 64-deep step) against reading
+      // the slabs back (~5 TB/s): S ~ sqrt(k-steps * 7e6 / slab bytes)
+      const double slab_bytes = 4.0 * (double)mt * (double)N * (double)batch;
+      int64_t S = (int64_t)(sqrt((double)kit * 7.0e6 / slab_bytes) + 0.5);
+      const int64_t max_s = cus / (peel * per_row) > 1 ? cus / (peel * per_row) : 1;
+      if (S > max_s) S = max_s;
+      if (S > kit) S = kit;
+      const int64_t cap = epi->workspace_floats / (batch * mt * N);
+      if (S > cap) S = cap;
+      if (S >= 2 && m0 > 0) {
+        tail_m0 = m0;
+        tail_s = (int)S;
+      }
+    }
+  }
   hipStream_t s = (hipStream_t)stream;
   bool timed;
   std::pair<hipEvent_t, hipEvent_t> ev;
@@ -159,8 +204,30 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
     ev = take_events();
     (void)hipEventRecord(ev.first, s);
   }
+  if (tail_s) {
+    GemmParams t = p;  // the peeled rows as a split-K product into f32 slabs
+    t.A = a_kmajor ? p.A + tail_m0 * lda : p.A + tail_m0;
+    t.M = M - tail_m0;
+    t.tiles_m = (int)((t.M + 255) / 256);
+    t.group_m = 1;
+    t.kind = MMU_EPI_STORE;
+    t.accumulate = 0;
+    t.bias = nullptr;
+    t.colsum = nullptr;
+    t.residual = nullptr;
+    t.aux = nullptr;
+    t.drop_p = 0.f;
+    t.splitk = tail_s;
+    t.kchunk = ((K + tail_s - 1) / tail_s + 63) / 64 * 64;
+    t.splitk = (int)((K + t.kchunk - 1) / t.kchunk);
+    t.ws = epi->workspace;
+    tail_s = t.splitk;
+    gemm_launch(t, a_kmajor != 0, b_kmajor != 0, true, true, (int)batch, s);
+    p.tiles_m -= (int)((M - tail_m0) / 256 + ((M - tail_m0) % 256 ? 1 : 0));
+  }
   gemm_launch(p, a_kmajor != 0, b_kmajor != 0, c_dtype == MMU_F32, big, (int)batch, s);
   if (p.splitk > 1) splitk_reduce_launch(p, (int)batch, s);
+  if (tail_s) gemm_tail_launch(p, c_dtype == MMU_F32, tail_m0, tail_s, epi->workspace, (int)batch, s);
   if (timed) {
     (void)hipEventRecord(ev.second, s);
     std::lock_guard<std::mutex> lk(g_t.mu);

@@ -735,6 +735,79 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   *(float4*)c = a;
 }
 
+// ------------------------------------------------------------------ split-K tail
+// The last partial wave of 256x256 tiles (e.g. 3 tiles after 6 full waves of 256 at M =
+// 131328, N = 768) would hold the whole chip for a full tile time.  The host instead
+// peels those M-tile rows off the main launch, runs them as a split-K product into f32
+// slabs (rows m0.. of the workspace, slice-major) and finishes them here: slabs summed in
+// slice order, then the product's own epilogue (bias, GELU / dropout+residual / dGELU /
+// residual, column sums) at the GLOBAL row m, so dropout counters and outputs are exactly
+// those of the unsplit launch.  Thread = one (m, 8-column octet); 4 row groups x 64 octets.
+constexpr int TAIL_RB = 8;  // rows per block (2 per thread)
+template <int EPI, bool OUT_F32>
+__global__ __launch_bounds__(256) void gemm_tail_kernel(GemmParams p, int64_t m0, int64_t mt, int S,
+                                                        const float* __restrict__ ws) {
+  const int t = threadIdx.x;
+  const int64_t n = 8 * ((int64_t)blockIdx.x * 64 + (t & 63));
+  const int64_t z = blockIdx.z;
+  if (n >= p.N) return;
+  const float* bias = (p.bias && EPI != MMU_EPI_DGELU && EPI != MMU_EPI_ADD_RES) ? p.bias + z * p.bias_bstride : nullptr;
+  const bf16* res = p.residual ? (const bf16*)p.residual + z * p.res_bstride : nullptr;
+  bf16* aux = p.aux ? (bf16*)p.aux + z * p.aux_bstride : nullptr;
+  constexpr bool LOADS = EPI == MMU_EPI_BIAS_DROP_RES || EPI == MMU_EPI_DGELU || EPI == MMU_EPI_ADD_RES;
+  const bf16* src = EPI == MMU_EPI_DGELU ? (const bf16*)aux : res;
+  const int64_t lds_ = EPI == MMU_EPI_DGELU ? p.ldx : p.ldr;
+  const float scale = p.drop_p > 0.f ? 1.0f / (1.0f - p.drop_p) : 1.0f;
+  const uint32_t thr = (uint32_t)(p.drop_p * 65536.0f + 0.5f);
+  float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (bias) {
+    const float4 b0 = *(const float4*)(bias + n), b1 = *(const float4*)(bias + n + 4);
+    bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w; bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+  }
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int64_t slab = mt * p.N;
+#pragma unroll
+  for (int i = 0; i < TAIL_RB / 4; ++i) {
+    const int64_t r = (int64_t)blockIdx.y * TAIL_RB + (t >> 6) + 4 * i;
+    if (r >= mt) break;
+    const int64_t m = m0 + r;
+    const bf16x8 in = LOADS ? *(const bf16x8*)(src + m * lds_ + n) : bf16x8{};
+    const float* w = ws + z * S * slab + r * p.N + n;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = bv[e];
+    for (int k = 0; k < S; ++k) {
+      const float4 lo = *(const float4*)(w + k * slab), hi = *(const float4*)(w + k * slab + 4);
+      v[0] += lo.x; v[1] += lo.y; v[2] += lo.z; v[3] += lo.w; v[4] += hi.x; v[5] += hi.y; v[6] += hi.z; v[7] += hi.w;
+    }
+    epi_oct<EPI, OUT_F32>(p, z, m, n, v, in, aux, scale, thr);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs[e] += v[e];
+  }
+  if (p.colsum) {
+    float* out = p.colsum + z * p.colsum_bstride + n;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) atomicAdd(out + e, cs[e]);
+  }
+}
+
+void gemm_tail_launch(const GemmParams& p, bool f32out, int64_t m0, int S, const float* ws, int batch, hipStream_t s) {
+  const int64_t mt = p.M - m0;
+  const dim3 g((unsigned)((p.N / 8 + 63) / 64), (unsigned)((mt + TAIL_RB - 1) / TAIL_RB), (unsigned)batch);
+#define TAIL(E, F) hipLaunchKernelGGL((gemm_tail_kernel<E, F>), g, dim3(256), 0, s, p, m0, mt, S, ws)
+  switch (p.kind) {
+    case MMU_EPI_STORE:
+      if (f32out) TAIL(MMU_EPI_STORE, true);
+      else TAIL(MMU_EPI_STORE, false);
+      break;
+    case MMU_EPI_BIAS_GELU: TAIL(MMU_EPI_BIAS_GELU, false); break;
+    case MMU_EPI_BIAS_DROP_RES: TAIL(MMU_EPI_BIAS_DROP_RES, false); break;
+    case MMU_EPI_DGELU: TAIL(MMU_EPI_DGELU, false); break;
+    case MMU_EPI_ADD_RES: TAIL(MMU_EPI_ADD_RES, false); break;
+  }
+#undef TAIL
+}
+
 void splitk_reduce_launch(const GemmParams& p, int batch, hipStream_t s) {
   const int64_t q = (p.M * p.N) / 4;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((q + 255) / 256), batch), dim3(256), 0, s, p.ws,

@@ -77,12 +77,14 @@ def gemm(A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, M, N_, K, epi=None, batch=1
     cdt = N.MMU_F32 if C.dtype == torch.float32 else N.MMU_BF16
     if C.dtype not in (torch.float32, torch.bfloat16):
         raise N.NativeError("gemm C must be f32 or bf16")
-    if cdt == N.MMU_F32 and (epi is None or (epi.kind == EPI_STORE and not epi.bias and not epi.colsum)):
-        if epi is None:
-            epi = epilogue(EPI_STORE)
-        if not epi.workspace:
-            ws = _splitk_workspace(C.device)
-            epi.workspace, epi.workspace_floats = ws.data_ptr(), ws.numel()
+    # the per-stream f32 scratch serves split-K weight gradients and the split-K tail of
+    # every big-tile product (mmu_gemm: the partial last wave of 256x256 tiles)
+    if epi is None:
+        epi = epilogue(EPI_STORE)
+    if not epi.workspace:  # (on a copy: a caller's epilogue may be reused on another stream)
+        epi = type(epi).from_buffer_copy(epi)
+        ws = _splitk_workspace(C.device)
+        epi.workspace, epi.workspace_floats = ws.data_ptr(), ws.numel()
     N.call("mmu_gemm", _ptr(A), lda, int(a_kmajor), _ptr(B), ldb, int(b_kmajor), _ptr(C), ldc, cdt, M, N_, K,
            batch, sA, sB, sC, ctypes.byref(epi) if epi is not None else None, _stream(C))
     if _alg["on"]:

@@ -142,6 +142,70 @@ def test_gemm_big_tiles_epilogues(dev):
     assert torch.equal(out, out2)
 
 
+@pytest.mark.parametrize("Kd", [256, 768])
+def test_gemm_split_k_tail(dev, Kd, monkeypatch):
+    """M = 257 tile rows x 3 column tiles = 771 tiles: the partial last wave (3 tiles) runs as a
+    split-K tail + finishing epilogue.  Same results as the unsplit launch (MMU_GEMM_TAIL=0):
+    identical dropout pattern, outputs within one bf16 rounding, same column sums."""
+    k = K()
+    M, N = 256 * 257, 768
+    A, B = rnd(M, Kd, dev=dev, seed=61), rnd(N, Kd, dev=dev, seed=62, scale=0.1)
+    bias = torch.randn(N, device=dev) * 0.1
+    R = rnd(M, N, dev=dev, seed=63)
+    Zr = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+    aux = (torch.rand(M, N, device=dev) + 0.5).to(torch.bfloat16)
+
+    def run(kind, **kw):
+        outs = {}
+        for tail in ("1", "0"):
+            monkeypatch.setenv("MMU_GEMM_TAIL", tail)
+            f32 = kind == "f32"
+            out = torch.full((M, N), 0.25, dtype=torch.float32 if f32 else torch.bfloat16, device=dev)
+            cs = torch.zeros(N, device=dev)
+            ax = torch.empty(M, N, dtype=torch.bfloat16, device=dev) if kind == k.EPI_BIAS_GELU else kw.get("aux")
+            e = k.epilogue(k.EPI_STORE, accumulate=True) if f32 else k.epilogue(
+                kind, colsum=cs, **{**kw, **({"aux": ax} if ax is not None else {})})
+            k.gemm(A, Kd, True, B, Kd, True, out, N, M, N, Kd, epi=e)
+            outs[tail] = (out.float(), cs, ax)
+        return outs
+
+    ref = A.float() @ B.float().t()
+    o = run(k.EPI_BIAS_DROP_RES, bias=bias * 0, residual=Zr, drop_p=0.1, seed=77)
+    assert torch.equal(o["1"][0] == 0, o["0"][0] == 0)  # same dropout counters
+    tl = slice(M - 256, M)
+    kept = o["1"][0][tl] != 0
+    close(o["1"][0][tl][kept], (ref[tl] / 0.9)[kept])
+    for kind, kw in ((k.EPI_STORE, {"bias": bias}), (k.EPI_BIAS_GELU, {"bias": bias}),
+                     (k.EPI_DGELU, {"aux": aux}), (k.EPI_ADD_RES, {"residual": R}), ("f32", {})):
+        o = run(kind, **kw)
+        a, b = o["1"][0], o["0"][0]
+        torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2)
+        torch.testing.assert_close(o["1"][1], o["0"][1], rtol=1e-3, atol=1e-1)
+        if kind == k.EPI_BIAS_GELU:
+            torch.testing.assert_close(o["1"][2].float(), o["0"][2].float(), rtol=1e-2, atol=1e-2)
+        want = {k.EPI_STORE: ref + bias, k.EPI_DGELU: ref * aux.float(), k.EPI_ADD_RES: ref + R.float(),
+                "f32": ref + 0.25}.get(kind)
+        if want is not None:
+            close(a[tl], want[tl])
+
+
+def test_gemm_split_k_tail_batched(dev, monkeypatch):
+    """batch 2 x 129 tile rows x 3 column tiles = 774 tiles: tail rows peeled in every batch item"""
+    k = K()
+    Bt, M, N, Kd = 2, 256 * 129, 768, 512
+    A, B = rnd(Bt, M, Kd, dev=dev, seed=64), rnd(Bt, N, Kd, dev=dev, seed=65, scale=0.1)
+    bias = torch.randn(Bt, N, device=dev) * 0.1
+    res = {}
+    for tail in ("1", "0"):
+        monkeypatch.setenv("MMU_GEMM_TAIL", tail)
+        C = torch.empty(Bt, M, N, dtype=torch.bfloat16, device=dev)
+        k.gemm(A, Kd, True, B, Kd, True, C, N, M, N, Kd, batch=Bt, sA=M * Kd, sB=N * Kd, sC=M * N,
+               epi=k.epilogue(k.EPI_STORE, bias=bias, bias_bstride=N))
+        res[tail] = C.float()
+    torch.testing.assert_close(res["1"], res["0"], rtol=1e-2, atol=1e-2)
+    close(res["1"][:, -256:], (A.float() @ B.float().transpose(1, 2) + bias[:, None, :])[:, -256:])
+
+
 def test_gemm_bias_dropout_residual(dev):
     k = K()
     M, N, Kd = 512, 768, 256
