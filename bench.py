@@ -121,6 +121,7 @@ def main():
     from src.testing import make_args, synthetic_batch
     from src import kernels as K
     from src.dp import GradBucketer, broadcast_parameters
+    from src import encoder
 
     # MIOpen solver choice for the ResNet convs: "find" mode over the find-db shipped in
     # multi-modal-uncertainty_amd/miopen_db (per-rank batches 256/128/64/32 pre-searched on
@@ -156,6 +157,7 @@ def main():
     if world > 1:
         dist.barrier()
     K.timing_enable(True)
+    encoder.block_timing(True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -169,6 +171,8 @@ def main():
     gemm_ms, gemm_n, gemm_flops = K.timing_read()
     alg_bytes, _ = K.timing_alg_bytes()
     K.timing_enable(False)
+    block_ms, block_n = encoder.block_timing_read()
+    encoder.block_timing(False)
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -180,6 +184,7 @@ def main():
     layer_fwd = L * (24 * H * H + 4 * L * H)
     model_flop = 3 * (12 * layer_fwd + RESNET152_FWD_FLOP)
     achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
+    block_tf = 3 * layer_fwd * B * (block_n / 2) / (block_ms * 1e-3) / 1e12 if block_ms > 0 else 0.0
     out = {
         "metric": "image+text samples/sec/node, MMBT Food-101 bs=256 seq=512; ECE/NLL parity",
         "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
@@ -196,6 +201,15 @@ def main():
                      "algorithmic_bytes_per_launch": round(alg_bytes / max(gemm_n, 1)),
                      "launches": gemm_n, "avg_launch_ms": round(gemm_ms / max(gemm_n, 1), 4),
                      "gemm_share_of_step": round(gemm_ms / args.steps / ms_step, 3) if ms_step else None},
+        # BASELINE north star: >= 40 % of the bf16 MFMA peak on the fused MMBT block (one
+        # BertLayer fwd + bwd = 3 x L (24 H^2 + 4 L H) flop per sample), timed by HIP events
+        # around every layer's forward and backward (GEMMs, attention, LayerNorms, reductions)
+        "fused_block_roofline": {
+            "bound": "mfma", "flop_per_sample_per_layer": 3 * layer_fwd,
+            "achieved": round(block_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(block_tf / PEAK_BF16_TFLOPS, 4), "target_frac": 0.40,
+            "ms_per_layer_fwd_bwd": round(block_ms / max(block_n, 1) * 2, 4), "layer_passes_timed": block_n,
+            "share_of_step": round(block_ms / args.steps / ms_step, 3) if ms_step else None},
         "model_tflops_per_step_per_rank": round(B * model_flop / 1e12, 2),
         "model_tflops_achieved": round(B * model_flop * world / (ms_step * 1e-3) / 1e12, 1),
         "final_loss": round(float(loss.item()), 4),

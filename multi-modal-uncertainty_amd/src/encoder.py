@@ -179,13 +179,42 @@ def layer_backward(lw, saved, dY, keymask, B, L, p_attn, p_hid, seeds, wgrad):
     return dX, side
 
 
+_block_events = None  # [(start, end)] HIP events around every fused-layer fwd / bwd while timing
+
+
+def block_timing(on):
+    """Time every BertLayer forward and backward on the stream it runs on (bench.py: the
+    fused-block roofline of BASELINE's north star)."""
+    global _block_events
+    _block_events = [] if on else None
+
+
+def block_timing_read():
+    """-> (total ms, number of layer passes) since block_timing(True); synchronises."""
+    if not _block_events:
+        return 0.0, 0
+    _block_events[-1][1].synchronize()
+    return sum(a.elapsed_time(b) for a, b in _block_events), len(_block_events)
+
+
+def _mark():
+    if _block_events is None:
+        return None
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    return e
+
+
 class BertLayerFunction(torch.autograd.Function):
     """One fused BertLayer; X [B*L, 768] bf16 -> Y.  ``anchor`` (the layer's query
     weight) only makes autograd run backward when the layer is trainable."""
 
     @staticmethod
     def forward(ctx, X, anchor, lw, keymask, B, L, p_attn, p_hid, seeds, on_grads_ready):
+        e0 = _mark()
         Y, saved = layer_forward(lw, X, keymask, B, L, p_attn, p_hid, seeds, save=True)
+        if e0 is not None:
+            _block_events.append((e0, _mark()))
         ctx.saved_bufs = saved
         ctx.meta = (lw, keymask, B, L, p_attn, p_hid, seeds, on_grads_ready)
         return Y
@@ -194,7 +223,10 @@ class BertLayerFunction(torch.autograd.Function):
     def backward(ctx, dY):
         lw, keymask, B, L, p_attn, p_hid, seeds, hook = ctx.meta
         wgrad = lw.trainable()
+        e0 = _mark()
         dX, side = layer_backward(lw, ctx.saved_bufs, dY.contiguous(), keymask, B, L, p_attn, p_hid, seeds, wgrad)
+        if e0 is not None:
+            _block_events.append((e0, _mark()))
         ctx.saved_bufs = None
         if wgrad and side.on:
             if hook is not None:  # the gradient all-reduce is issued behind the side stream's work
