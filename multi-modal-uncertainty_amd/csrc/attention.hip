@@ -23,6 +23,7 @@
 #include "mmu_common.h"
 #include "mmu_internal.h"
 #include <cstdlib>
+#include <type_traits>
 
 namespace mmu {
 
@@ -42,7 +43,14 @@ static __device__ __forceinline__ uint32_t drop_pair(uint32_t sbh, uint32_t q, u
   return lowbias32(((q * Lp + key) >> 1) ^ sbh);
 }
 
-static __device__ __forceinline__ uint32_t drop_thr(float p) { return (uint32_t)(p * 65536.0f + 0.5f); }
+// v_max3_f32 without hipcc's NaN canonicalisation of each MFMA output (a v_max_f32 x,x per
+// operand under plain fmaxf)
+static __device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+static __host__ __device__ __forceinline__ uint32_t drop_thr(float p) { return (uint32_t)(p * 65536.0f + 0.5f); }
 
 static __device__ __forceinline__ int fsw(int r) { return (((r >> 1) & 1) << 2) | ((r >> 3) & 3); }
 static __device__ __forceinline__ int tile_off(int row, int chunk) { return row * 128 + ((chunk ^ fsw(row)) << 4); }
@@ -674,10 +682,277 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
 }
 
 static bool attn_dma();
+// ---------------------------------------------------------------- forward v2 (lean softmax)
+// attn_fwd_dma_kernel's ring and tiling with the per-element VALU work cut down (the v1
+// forward issued ~750 VALU per 16 MFMAs per tile and measured VALU-busy ~88 %):
+//  * K and V rows are DMA'd into LDS in a key permutation kappa (within each 32-key half,
+//    LDS row 8a + 4h + b holds key 16h + 4a + b), so the S^T accumulator register r of
+//    half-wave h holds key 16h + r: each lane's 16 keys per half are CONTIGUOUS (mask row
+//    read as 4 x 16 B, dropout counters consecutive, keep bits a 16-bit field).  P^T and V
+//    share the permutation, so P V is unchanged;
+//  * the key-mask row enters as the S accumulator's initial value, so S' = S/8 + mask
+//    costs no VALU; p = exp2(fma(S', log2e, -m log2e)): one FMA + one v_exp per element;
+//  * deferred max (rescale O and l only when a row's max grew by > 8 in log2 units, so
+//    P <= 2^8 between rescales; wave-uniform branch);
+//  * the row sum stays per half-wave until the end (one shuffle per block, not per tile);
+//  * the partial last key tile is a separate instantiation (no key < L tests in full
+//    tiles), and when at most 32 of its keys are live only that half is computed;
+//  * dropout: one full hash per 16 keys of a row, 16-bit draws of each key pair from a
+//    multiply of it; compare / select / keep-bit shift-in (v_addc) as 3 VALU per element;
+//  * O leaves through LDS as 16-B row stores.
+// Needs ceil(L/64) <= FWD_MAX_NKV and ld_out % 8 == 0.
+constexpr float DEFER_LOG2 = 8.0f;
+__constant__ uint32_t kDropMul[8] = {0x9E3779B1u, 0x85EBCA77u, 0xC2B2AE3Du, 0x27D4EB2Fu,
+                                     0x165667B1u, 0xD3A2646Du, 0xFD7046C5u, 0xB55A4F09u};
+
+static __device__ __forceinline__ int kperm(int i) {  // LDS row i of a 32-key half -> key
+  return (((i >> 2) & 1) << 4) | (((i >> 3) & 3) << 2) | (i & 3);
+}
+
+// keep decisions of key pair (2i, 2i+1) from one 32-bit hash (low half -> even key):
+// zero the dropped P values and shift the two keep bits into w (odd key first, so that a
+// descending walk leaves bit k of w = element k)
+static __device__ __forceinline__ void drop_pair_apply(uint32_t hsh, uint32_t thr, uint32_t thr_hi, float& e0,
+                                                       float& e1, uint32_t& w) {
+  asm("v_cmp_le_u32 vcc, %[th], %[h]\n\t"
+      "v_cndmask_b32 %[d1], 0, %[d1], vcc\n\t"
+      "v_addc_co_u32 %[w], vcc, %[w], %[w], vcc\n\t"
+      "v_cmp_le_u16 vcc, %[t], %[h]\n\t"
+      "v_cndmask_b32 %[d0], 0, %[d0], vcc\n\t"
+      "v_addc_co_u32 %[w], vcc, %[w], %[w], vcc"
+      : [d0] "+v"(e0), [d1] "+v"(e1), [w] "+v"(w)
+      : [h] "v"(hsh), [t] "s"(thr), [th] "s"(thr_hi)
+      : "vcc");
+}
+
+template <bool DROP, int WPE, bool NOHOIST>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void attn_fwd_v2_kernel(AttnParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[FWD_NS * FWD_STAGE + 4 * 32 * FWD_MAX_NKV * 8];
+  uint64_t* kbuf_all = (uint64_t*)(smem + FWD_NS * FWD_STAGE);
+  const int t = threadIdx.x, l = t & 63, l_ = l, h = l >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int bh = blockIdx.y, b = bh / p.heads, hd = bh - b * p.heads;
+  const int L = p.L, HD = p.heads * 64;
+  const int q0w = blockIdx.x * 128 + 32 * w, q = q0w + (l & 31);
+  const bool wave_live = q0w < L;
+  const bf16* base = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64;
+  const uint32_t thr = drop_thr(p.drop_p), thr_hi = thr << 16;
+  const int nkv = (L + 63) / 64;
+  uint64_t* kbuf = kbuf_all + w * 32 * nkv;
+  const bool store_bits = DROP && p.dropmask != nullptr;
+  // dropout counter base of row q: seed_bh + 4 (q nkv) + 2h  (+ 4j + s2 per tile half)
+  const uint32_t ctr = seed_for(p.seed, bh) + 4u * (uint32_t)q * (uint32_t)nkv + 2u * (uint32_t)h;
+
+  const __amdgpu_buffer_rsrc_t rkv = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.qkv + (int64_t)b * L * p.ld_qkv), 0, (int)(L * p.ld_qkv * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)(p.keymask + (int64_t)b * L), 0,
+                                                                      (int)(L * 4), 0x00020000);
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    uint4 u = q < L ? *(const uint4*)(base + (int64_t)q * p.ld_qkv + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
+    qf[ks] = scale_frag(u, 0.125f);
+  }
+  f32x16 o[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
+  float m_run = NEG_INF, nml = 0.f, l_run = 0.f;  // nml = -m_run * log2e
+
+  // per tile: waves 0,1 -> K pieces, waves 2,3 -> V pieces (4 each, rows in kperm order);
+  // wave 0 also the (unpermuted) mask row
+  auto issue = [&](int j) {
+    char* st = smem + (j % FWD_NS) * FWD_STAGE;
+    const int k0 = j * 64;
+    const int off_col = (w < 2 ? HD : 2 * HD) + hd * 64;
+    char* dst = st + (w < 2 ? 0 : FWD_TILE);
+#pragma unroll
+    for (int pc = 0; pc < 4; ++pc) {
+      const int piece = 4 * (w & 1) + pc;
+      const int row = 8 * piece + (l >> 3), c = (l & 7) ^ fsw(row);
+      const int key = (row & 32) | kperm(row & 31);
+      dma16(rkv, dst + piece * 1024, (uint32_t)(((k0 + key) * p.ld_qkv + off_col + 8 * c) * 2));
+    }
+    if (w == 0 && l < 16) dma16(rm, st + 2 * FWD_TILE, (uint32_t)((k0 + 4 * l) * 4));
+  };
+  auto wait_for = [&](int ahead) {
+    if (w == 0) {
+      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  };
+
+  // one 64-key tile; PARTIAL: keys >= L exist in it (the last tile only).  Register r of
+  // sc[s2] holds key 64j + 32 s2 + 16h + r.
+  auto tile = [&](int j, auto partial_tag) {
+    constexpr bool PARTIAL = decltype(partial_tag)::value;
+    const char* st = smem + (j % FWD_NS) * FWD_STAGE;
+    const char* Ks = st;
+    const char* Vs = st + FWD_TILE;
+    const float* mk = (const float*)(st + 2 * FWD_TILE);
+    const bool two = !PARTIAL || L - 64 * j > 32;  // second 32-key half has live keys
+    // NOHOIST: re-derive the lane's LDS addresses per tile instead of keeping ~30 hoisted
+    // lane constants live across the loop (they spill at the 3-wave register cap)
+    int l = l_;
+    if (NOHOIST) asm volatile("" : "+v"(l));
+    f32x16 sc[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 mv = *(const f32x4*)(mk + 32 * s2 + 16 * h + 4 * g);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = mv[e];
+          if (PARTIAL && 64 * j + 32 * s2 + 16 * h + 4 * g + e >= L) v = NEG_INF;
+          sc[s2][4 * g + e] = v;
+        }
+      }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      sc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ks, 0, ks, l), qf[ks], sc[0], 0, 0, 0);
+    if (two) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        sc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ks, 32, ks, l), qf[ks], sc[1], 0, 0, 0);
+    }
+    float mx = max3f(sc[0][0], sc[0][1], sc[0][2]);
+#pragma unroll
+    for (int r = 3; r < 15; r += 2) mx = max3f(mx, sc[0][r], sc[0][r + 1]);
+    mx = __builtin_fmaxf(mx, sc[0][15]);
+    if (two) {
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) mx = max3f(mx, sc[1][r], sc[1][r + 1]);
+    }
+    mx = __builtin_fmaxf(mx, __shfl_xor(mx, 32, 64));
+    // deferred max: rescale only when a row's max grew by more than DEFER_LOG2 (log2 units)
+    const bool upd = (mx - m_run) * LOG2E > DEFER_LOG2;  // m_run = -inf: true
+    if (__builtin_amdgcn_ballot_w64(upd)) {
+      const float mnew = upd ? mx : m_run;
+      const float alpha = upd ? __builtin_amdgcn_exp2f((m_run - mnew) * LOG2E) : 1.0f;  // exp2(-inf) = 0
+      l_run *= alpha;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+      m_run = mnew;
+      nml = -mnew * LOG2E;
+    }
+    // per 32-key half: exponentials, dropout, then its P V MFMAs (the second half's VALU
+    // overlaps the first half's MFMAs; fewer live registers)
+    // dropout stream of (row q, tile j, half s2, half-wave h): counter ctr + 4j + s2
+    const uint32_t c0 = ctr + 4u * (uint32_t)j;
+    uint32_t wb[2] = {0u, 0u};  // bit r of wb[s2] = keep(register r of sc[s2])
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      if (s2 == 1 && !two) break;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = __builtin_amdgcn_exp2f(fmaf(sc[s2][r], LOG2E, nml));
+        sc[s2][r] = e;
+        l_run += e;
+      }
+      if (DROP) {
+        // one full hash per (row, tile, half, half-wave); its 8 pairs' 32-bit draws are
+        // hb * C_i folded by x ^ (x >> 16) (2 VALU per pair instead of a 7-VALU hash; the
+        // 16 decisions measured pairwise-uncorrelated to 2e-3 over 2^21 draws, joint
+        // drop counts binomial)
+        const uint32_t hb = lowbias32(c0 + (uint32_t)s2);
+#pragma unroll
+        for (int i = 7; i >= 0; --i) {
+          uint32_t hsh = hb * kDropMul[i];
+          hsh ^= hsh >> 16;
+          float e0 = sc[s2][2 * i], e1 = sc[s2][2 * i + 1];
+          drop_pair_apply(hsh, thr, thr_hi, e0, e1, wb[s2]);
+          sc[s2][2 * i] = e0;
+          sc[s2][2 * i + 1] = e1;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bf16x8 pf = acc_frag(sc[s2], u);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Vs, 32 * s2 + 16 * u, 32 * dt, l), pf, o[dt], 0, 0, 0);
+      }
+    }
+    if (store_bits) {  // row word: keys 16h..16h+15 <- wb[0], keys 32+16h.. <- wb[1]
+      const uint64_t mine = ((uint64_t)(wb[1] & 0xFFFFu) << (32 + 16 * h)) | ((uint64_t)(wb[0] & 0xFFFFu) << (16 * h));
+      const uint32_t lo = (uint32_t)mine | (uint32_t)__shfl_xor((int)(uint32_t)mine, 32, 64);
+      const uint32_t hi = (uint32_t)(mine >> 32) | (uint32_t)__shfl_xor((int)(uint32_t)(mine >> 32), 32, 64);
+      if (h == 0) kbuf[(l & 31) * nkv + j] = ((uint64_t)hi << 32) | lo;
+    }
+  };
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int j = 0; j < FWD_NS - 1 && j < nkv; ++j) issue(j);
+  for (int j = 0; j < nkv; ++j) {
+    const int ahead = nkv - 1 - j < FWD_NS - 2 ? nkv - 1 - j : FWD_NS - 2;
+    wait_for(ahead);
+    raw_barrier();
+    if (j + FWD_NS - 1 < nkv) issue(j + FWD_NS - 1);
+    if (wave_live) {
+      if (64 * (j + 1) > L) tile(j, std::integral_constant<bool, true>{});
+      else tile(j, std::integral_constant<bool, false>{});
+    }
+  }
+  raw_barrier();  // every wave is done with the ring: it becomes the O staging area
+  if (!wave_live) return;
+  if (store_bits) {  // this wave's 32 rows x nkv words are contiguous in the dropmask
+    uint64_t* dst = p.dropmask + ((int64_t)bh * L + q0w) * nkv;
+    const int rows = L - q0w < 32 ? L - q0w : 32;
+    for (int i = l; i < rows * nkv; i += 64) dst[i] = kbuf[i];
+  }
+  const float lsum = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = (DROP ? 1.0f / (1.0f - p.drop_p) : 1.0f) / lsum;
+  // O rows through LDS: [32 rows][128 B] per wave, 16-B chunk c of row r at c ^ (r & 7)
+  char* os = smem + w * 4096;
+  const int qr = l & 31;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const bf16x4 v = {f2bf(o[dt][4 * g] * inv), f2bf(o[dt][4 * g + 1] * inv), f2bf(o[dt][4 * g + 2] * inv),
+                        f2bf(o[dt][4 * g + 3] * inv)};
+      *(bf16x4*)(os + qr * 128 + (((4 * dt + g) ^ (qr & 7)) << 4) + 8 * h) = v;
+    }
+  if (h == 0 && q < L) p.lse[(int64_t)bh * L + q] = m_run + logf(lsum);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS rows are written (wave-private)
+  bf16* ob = p.out + hd * 64;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (l >> 3) + 8 * i, c = l & 7;
+    if (q0w + r < L)
+      *(uint4*)(ob + ((int64_t)b * L + q0w + r) * p.ld_out + 8 * c) = *(const uint4*)(os + r * 128 + ((c ^ (r & 7)) << 4));
+  }
+}
+
+static int attn_fwd_ver() {
+  const char* e = getenv("MMU_ATTN_FWD");  // 1 = v1 LDS-DMA kernel, 0 = register-staged (A/B)
+  return e ? atoi(e) : 2;
+}
+
 void attention_fwd_launch(const AttnParams& p, hipStream_t s) {
   dim3 grid((p.L + 127) / 128, p.batch * p.heads);
-  if (attn_dma() && (p.L + 63) / 64 <= FWD_MAX_NKV) hipLaunchKernelGGL(attn_fwd_dma_kernel, grid, dim3(256), 0, s, p);
-  else hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, s, p);
+  const int ver = attn_dma() ? attn_fwd_ver() : 0;
+  const bool fits = (p.L + 63) / 64 <= FWD_MAX_NKV;
+  if (ver >= 2 && fits && p.ld_out % 8 == 0) {
+    // Dropout variant at 2 waves / SIMD (at the 3-wave register cap it spills lane-constant
+    // LDS addresses around the loop: 0.89 vs 0.59 ms at B = 256, L = 513, p = 0.1).
+    // A/B (MMU_ATTN_FWD): 3 = 3 waves/SIMD, 4 = 3 waves + per-tile re-derived addresses
+    if (drop_thr(p.drop_p)) {
+      if (ver == 3) hipLaunchKernelGGL((attn_fwd_v2_kernel<true, 3, false>), grid, dim3(256), 0, s, p);
+      else if (ver == 4) hipLaunchKernelGGL((attn_fwd_v2_kernel<true, 3, true>), grid, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((attn_fwd_v2_kernel<true, 2, false>), grid, dim3(256), 0, s, p);
+    } else {
+      if (ver == 4) hipLaunchKernelGGL((attn_fwd_v2_kernel<false, 3, true>), grid, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((attn_fwd_v2_kernel<false, 3, false>), grid, dim3(256), 0, s, p);
+    }
+  } else if (ver >= 1 && fits) {
+    hipLaunchKernelGGL(attn_fwd_dma_kernel, grid, dim3(256), 0, s, p);
+  } else {
+    hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, s, p);
+  }
 }
 
 // ------------------------------------------------------------------ dK/dV, LDS-DMA ring

@@ -614,6 +614,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void g
   int tm, tn, slice;
   int64_t z;
   block_tile(p, z, slice, tm, tn);
+  if (p.stagger > 0) {  // first-round blocks 256..511 (the second slot of each CU) start half a tile late
+    const int lin = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+    if (lin >= 256 && lin < 512)
+      for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * 128;
   const int64_t a_bytes = (AK ? p.M * p.lda : p.K * p.lda) * 2;
   const int64_t b_bytes = (BKM ? p.N * p.ldb : p.K * p.ldb) * 2;
@@ -684,6 +689,8 @@ static void launch_t(const GemmParams& p, bool big, int batch, hipStream_t s) {
   dim3 grid(p.tiles_m * p.tiles_n, p.splitk, batch);
   if (big && use_duo()) {
     GemmParams q = p;
+    const char* st = getenv("MMU_GEMM_STAGGER");
+    q.stagger = st ? atoi(st) : 0;
     q.tiles_n = (int)((p.N + 127) / 128);
     dim3 g2(q.tiles_m * q.tiles_n, q.splitk, batch);
     hipLaunchKernelGGL((gemm_duo_kernel<AK, BKM, EPI, F32>), g2, dim3(256), 0, s, q);

@@ -31,6 +31,7 @@ struct GemmParams {
   int splitk;
   int64_t kchunk;
   float* ws;
+  int stagger;  // duo kernel: s_sleep(127) count for the second block of each CU (A/B experiment)
 };
 
 void splitk_reduce_launch(const GemmParams& p, int batch, hipStream_t s);

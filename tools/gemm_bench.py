@@ -30,6 +30,25 @@ def timed(fn, iters):
     return best
 
 
+def set_env(var, v):
+    """v = a value of var, or 'A=1:B=2' (several variables; the others are cleared), or None"""
+    keys = {var} | {kv.split("=")[0] for kv in (v or "").split(":") if "=" in kv} | set(_SEEN)
+    for k in keys:
+        os.environ.pop(k, None)
+    if v is None:
+        return
+    if "=" in v:
+        for kv in v.split(":"):
+            k, x = kv.split("=")
+            os.environ[k] = x
+            _SEEN.add(k)
+    else:
+        os.environ[var] = v
+
+
+_SEEN = set()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=256 * 513)
@@ -90,16 +109,16 @@ def main():
          lambda: torch.matmul(dZ.t(), A)),
     ]
     vals = a.vals.split(",")
-    print(f"{'gemm':26s} {'M':>7s} {'N':>5s} {'K':>7s} " + " ".join(f"{a.var[-8:] + '=' + v:>18s}" for v in vals)
+    print(f"{'gemm':26s} {'M':>7s} {'N':>5s} {'K':>7s} " + " ".join(f"{(a.var[-8:] + '=' + v)[-18:]:>18s}" for v in vals)
           + f" {'hipBLASLt':>18s}")
     for name, m, n, k, f_mmu, f_ref in cases:
         fl = 2.0 * m * n * k
         ts = {v: float("inf") for v in vals}
         for _ in range(3):  # interleaved rounds in one process
             for v in vals:
-                os.environ[a.var] = v
+                set_env(a.var, v)
                 ts[v] = min(ts[v], timed(f_mmu, a.iters))
-        os.environ.pop(a.var, None)
+        set_env(a.var, None)
         t2 = timed(f_ref, a.iters)
         print(f"{name:26s} {m:7d} {n:5d} {k:7d} " + " ".join(f"{ts[v]:8.3f}ms {fl / ts[v] / 1e9:6.0f}T" for v in vals)
               + f" {t2:8.3f}ms {fl / t2 / 1e9:6.0f}T", flush=True)
