@@ -3,8 +3,12 @@
 One step = one optimizer step of the reference train loop over a synthetic Food-101
 batch (src/framework.py:276-319 with accum = 1, freeze epochs over, every one of the
 169.3 M parameters trainable): ResNet-152 + 12 fused BERT layers forward, CE loss,
-backward, (N>1: RCCL gradient all-reduce), fused BertAdam.  Global batch 256 of
-(224x224 image, 508 word-pieces -> 513 tokens) split over the N ranks.
+backward, (N>1: RCCL gradient all-reduce), fused BertAdam.  Each rank trains on a batch of
+256 (224x224 image, 508 word-pieces -> 513 tokens) -- the metric's bs=256, which in the
+reference is the per-process DataLoader batch (train.py:41,238) -- so per-GPU work is fixed
+as N grows ("scaling": "weak") and every rank's ResNet BatchNorm normalises over the same
+256 samples as the reference's single process does.  --global-batch G instead splits G
+samples over the N ranks ("scaling": "strong"; DESIGN.md §6 has both measured).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -36,7 +40,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--global-batch", type=int, default=256)
+    ap.add_argument("--per-rank-batch", type=int, default=256, help="samples per rank per step (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="split this many samples over the ranks instead (strong scaling)")
     ap.add_argument("--text-len", type=int, default=508, help="word-pieces per sample (L = 5 + this)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=2)
@@ -110,8 +116,13 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
-    if args.global_batch % world:
-        raise SystemExit("global batch must divide evenly over ranks")
+    if args.global_batch is None:
+        args.global_batch = args.per_rank_batch * world
+        scaling = "weak"
+    else:
+        if args.global_batch % world:
+            raise SystemExit("global batch must divide evenly over ranks")
+        scaling = "strong"
     B = args.global_batch // world
     T = args.text_len
     L = T + 5
@@ -189,7 +200,7 @@ def main():
         "metric": "image+text samples/sec/node, MMBT Food-101 bs=256 seq=512; ECE/NLL parity",
         "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded; random-init weights)",
+        "scaling": scaling, "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded; random-init weights)",
         "config": {"workload": "mmbt_train_step", "model": "MMBT bert-base-uncased + resnet152",
                    "global_batch": args.global_batch, "per_rank_batch": B, "seq_len": 512, "tokens": L,
                    "parallelism": f"dp{world}", "grad_accum": 1, "optimizer": "BertAdam (fused HIP)",

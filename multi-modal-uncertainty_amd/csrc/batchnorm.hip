@@ -15,12 +15,13 @@
 // running variance is updated with the unbiased one, momentum-weighted.
 //
 // Work split: a block owns a chunk of CH <= 512 channels (grid.y) and a range of rows
-// (grid.x) sized to ~64 K elements; a thread owns 8 consecutive channels (16-B bf16
+// (grid.x) sized to 4 K - 64 K elements (~1 K blocks per launch, see bn_grid); a thread owns 8 consecutive channels (16-B bf16
 // accesses, a row chunk is read as CH*2 contiguous bytes) of every rpi-th row.  Per-thread
 // f32 partials are reduced over the block in LDS and stored as one (sum, sum2) pair per
 // channel and block -- no atomics: ~1-3 K blocks x 2C float atomics on the same addresses
 // serialise in the L2 atomic units (measured 4-10x slower than the apply pass).  The
 // finalize sums the block partials per channel in f64 (32 slices per channel + LDS).
+#include <stdlib.h>
 #include "mmu_common.h"
 #include "mmu_internal.h"
 
@@ -281,15 +282,25 @@ struct BnGrid {
   int64_t rpb;
   dim3 grid;
 };
-// channel chunk: the largest of 512, 256, ..., 8 dividing C; rows per block ~64 K elements,
-// a multiple of the rows per iteration, and few enough row blocks that blocks x C partial
-// pairs fit BN_MAX_PART_ELEMS
+// channel chunk: the largest of 512, 256, ..., 8 dividing C.  Rows per block: the tensor
+// split into ~BN_TARGET_BLOCKS blocks, but each block between BN_MIN and 64 K elements (a
+// multiple of the rows per iteration), and few enough row blocks that blocks x C partial
+// pairs fit BN_MAX_PART_ELEMS.  (A fixed 64 K elements per block left the trunk's small
+// tensors on 24-200 blocks -- e.g. layer3's 256-channel 14x14 maps at batch 32 -- i.e. on
+// a tenth of the CUs, latency-bound.)  MMU_BN_TARGET / MMU_BN_MIN override, for A/B runs.
+static int64_t bn_env(const char* name, int64_t dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoll(v) : dflt;
+}
 static BnGrid bn_grid(int64_t rows, int C) {
+  static const int64_t target = bn_env("MMU_BN_TARGET", 1024), min_elems = bn_env("MMU_BN_MIN", 4096);
   BnGrid g;
   g.CH = 512;
   while (C % g.CH) g.CH >>= 1;
   const int rpi = BN_THREADS / (g.CH / 8);
-  int64_t rpb = BN_ELEMS_PER_BLOCK / g.CH;
+  int64_t per = rows * (int64_t)C / target;
+  per = per < min_elems ? min_elems : per > BN_ELEMS_PER_BLOCK ? BN_ELEMS_PER_BLOCK : per;
+  int64_t rpb = (per + g.CH - 1) / g.CH;
   rpb = (rpb + rpi - 1) / rpi * rpi;
   const int64_t max_parts = BN_MAX_PART_ELEMS / C;
   if ((rows + rpb - 1) / rpb > max_parts) rpb = ((rows + max_parts - 1) / max_parts + rpi - 1) / rpi * rpi;

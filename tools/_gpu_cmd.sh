@@ -1,6 +1,11 @@
 set -o pipefail
-for v in 3 4; do
-MMU_ATTN_FWD=$v timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q -k "attention" --timeout 120 --timeout-method thread > gpurun_out/t_attn$v.log 2>&1
-rc=$?; tail -2 gpurun_out/t_attn$v.log; [ $rc -eq 0 ] || exit $rc
-done
-timeout -k 10 300 python tools/attn_bench.py --var MMU_ATTN_FWD --vals 1,2,3,4 > gpurun_out/attn_v2c.txt 2>&1
+for cfg in "1 65536" "1024 4096" "2048 4096" "512 8192"; do
+set -- $cfg
+for b in 32 256; do
+echo "== target=$1 min=$2 batch=$b" >> gpurun_out/bn_ab.txt
+MMU_BN_TARGET=$1 MMU_BN_MIN=$2 timeout -k 10 120 python -u tools/bn_bench.py --batch $b >> gpurun_out/bn_ab.txt 2>&1 || exit 1
+done; done
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --global-batch 32 --no-cpu-baseline > gpurun_out/bench_b32.log 2>&1 || exit 1
+MMU_GEMM_TAIL=1 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --global-batch 32 --no-cpu-baseline > gpurun_out/bench_b32_tail.log 2>&1 || exit 1
+timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench_b256.log 2>&1 || exit 1
+for f in bench_b32 bench_b32_tail bench_b256; do grep -o '"ms_per_step": [0-9.]*' gpurun_out/$f.log; done

@@ -1,8 +1,9 @@
 """BatchNorm kernels (mmu_batchnorm_fwd/bwd) at ResNet-152 shapes, B=256, against the
 bytes they must move (fwd: 3 passes of X [+ skip], bwd: 6 reads + 1-2 writes).
 
-  python tools/bn_bench.py
+  python tools/bn_bench.py [--batch N]   (MMU_BN_TARGET / MMU_BN_MIN: grid A/B)
 """
+import argparse
 import os
 import sys
 
@@ -14,9 +15,13 @@ from gemm_bench import timed  # noqa: E402
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    N = ap.parse_args().batch
     dev, cl = "cuda", torch.channels_last
-    for (N, C, H, W, skip) in [(256, 64, 112, 112, False), (256, 64, 56, 56, False), (256, 256, 56, 56, True),
-                               (256, 256, 14, 14, False), (256, 1024, 14, 14, True), (256, 2048, 7, 7, True)]:
+    for (C, H, W, skip) in [(64, 112, 112, False), (64, 56, 56, False), (256, 56, 56, True), (128, 28, 28, False),
+                            (512, 28, 28, True), (256, 14, 14, False), (1024, 14, 14, True), (512, 7, 7, False),
+                            (2048, 7, 7, True)]:
         x = torch.randn(N, C, H, W, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
         s = torch.randn_like(x) if skip else None
         Y, dX = torch.empty_like(x), torch.empty_like(x)

@@ -5,6 +5,7 @@ update kernel (one per optimizer step), so MIOpen's first-call solver search and
 the warm-up never enter the numbers.
 
   python tools/prof_summary.py gpurun_out/prof1/run_kernel_trace.csv [--md out.md]
+  python tools/prof_summary.py gpurun_out/prof1/run_results.db [--md out.md]
 """
 import argparse
 import csv
@@ -39,7 +40,12 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--md", default=None)
     a = ap.parse_args()
-    rows = list(csv.DictReader(open(a.trace)))
+    if a.trace.endswith(".db"):  # rocprofv3's default rocpd (sqlite) output
+        import sqlite3
+        cur = sqlite3.connect(a.trace).execute("select name, start, end from kernels")
+        rows = [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e} for n, s, e in cur]
+    else:
+        rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     adam = [i for i, r in enumerate(rows) if "adam_update_kernel" in r["Kernel_Name"]]
     if len(adam) < 2:
