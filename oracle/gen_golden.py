@@ -9,6 +9,11 @@ Run:  python -m oracle.gen_golden          (needs /root/reference; CPU only)
   from the global RNG (src/mmbt.py:199), plus image features, embeddings, pooled
   output, CE loss (eval) and a train-mode (BN batch stats, dropout 0) loss with
   per-tensor grad norms.
+* FLAVA fixtures: the reference ``src/model.py`` FlavaFusionTransfomer /
+  FlavaFusionTransfomerwithCLSToken with weights from
+  oracle/flava_ref.make_state_dict (strict), synthetic embeddings (seeded):
+  eval logits + losses, a train-mode loss (dropout 0) with per-tensor grad norms,
+  and the MIMO permutations of data_forming_func_transformer (src/dataset.py:30-54).
 * framework fixture: the reference ``Model_.train_loop`` (src/framework.py:213)
   with ``_construct_default_callbacks`` (src/training_loop.py:23-47) driving
   oracle/tiny_model.TinyMMBT for 2 epochs x 3 steps; history + checkpoint keys.
@@ -136,6 +141,75 @@ def gen_mmbt(tag, cfg, B, T, lens, seed=0, wseed=0):
     print(f"wrote mmbt_{tag}: loss_eval={out['loss_eval']:.6f} loss_train={out['loss_train']:.6f}")
 
 
+def _reference_function(relpath, name):
+    """One top-level function of a reference module whose other imports are absent here
+    (src/dataset.py needs torchvision transforms, a tokenizer, ViltProcessor): the
+    function's own definition is compiled from the reference file and run in a
+    namespace holding torch.  Used to record golden outputs only."""
+    import ast
+    src_path = os.path.join(REF, relpath)
+    tree = ast.parse(open(src_path).read(), filename=src_path)
+    node = next(n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == name)
+    ns = {"torch": torch}
+    exec(compile(ast.Module(body=[node], type_ignores=[]), src_path, "exec"), ns)
+    return ns[name]
+
+
+def gen_flava(tag, cfg, B, L_img, L_txt, seed):
+    from oracle import flava_ref as FR
+    _import_reference(__import__("oracle.weights", fromlist=["SMALL"]).SMALL, 0.0)
+    from src import model as ref_model  # the reference's own module
+    forming = _reference_function("src/dataset.py", "data_forming_func_transformer")
+    cls = ref_model.FlavaFusionTransfomerwithCLSToken if cfg.clstoken else ref_model.FlavaFusionTransfomer
+    torch.manual_seed(4321)
+    model = cls(out_dim=cfg.out_dim, num_classes=cfg.n_classes, multimodal_num_attention_heads=cfg.heads,
+                multimodal_num_hidden_layers=cfg.layers, drop=cfg.drop, avg_pool=cfg.avg_pool)
+    sd = FR.make_state_dict(seed, cfg)
+    ref_keys = list(model.state_dict().keys())
+    model.load_state_dict(sd, strict=True)
+    img, txt, y = FR.make_inputs(B, L_img, L_txt, cfg.n_classes, cfg.out_dim, seed + 1)
+    out = {"img_sum": np.float64(img.double().sum()), "txt_sum": np.float64(txt.double().sum()),
+           "y": y.numpy(), "B": np.int64(B), "L_img": np.int64(L_img), "L_txt": np.int64(L_txt),
+           "seed": np.int64(seed)}
+    model.eval()
+    with torch.no_grad():
+        logits = model((img, txt))
+        out["logits"] = logits.numpy()
+        out["loss_eval"] = np.float64(model.compute_loss(logits, y, eval=True))
+    model.train()
+    model.zero_grad()
+    x2, y2 = forming((img, txt), y, phase="train",
+                                                       model_type="Vanilla" if cfg.out_dim == 1 else "MultiHead")
+    logits = model(x2)
+    loss = model.compute_loss(logits, y2)
+    loss.backward()
+    out["logits_train"] = logits.detach().numpy()
+    out["loss_train"] = np.float64(loss.detach())
+    names = [n for n, _ in model.named_parameters()]
+    out["grad_norms"] = np.array([float(p.grad.double().norm()) for _, p in model.named_parameters()])
+    out["proj_bias_grad"] = model.image_to_mm_projection.bias.grad.numpy()
+    # MIMO-shuffle-instance: the permutations the reference draws from the global RNG
+    torch.manual_seed(99)
+    (pi, pt), py = forming((img, txt), y, phase="train",
+                                                             model_type="MIMO-shuffle-instance")
+    out["mimo_y"] = py.numpy()
+    out["mimo_img_rowsum"] = pi.double().sum((1, 2)).numpy()
+    out["mimo_txt_rowsum"] = pt.double().sum((1, 2)).numpy()
+    os.makedirs(OUT, exist_ok=True)
+    np.savez_compressed(os.path.join(OUT, f"flava_{tag}.npz"), **out)
+    with open(os.path.join(OUT, f"flava_{tag}_keys.json"), "w") as f:
+        json.dump({"state_dict_keys": ref_keys, "named_parameters": names}, f)
+    print(f"wrote flava_{tag}: loss_eval={out['loss_eval']:.6f} loss_train={out['loss_train']:.6f}")
+
+
+FLAVA_CASES = {  # tag: (cfg kwargs, B, L_img, L_txt, seed)
+    "vanilla": (dict(out_dim=1), 6, 9, 7, 10),
+    "multihead_avgpool": (dict(out_dim=2, avg_pool=True), 5, 11, 6, 11),
+    "cls_multihead": (dict(out_dim=2, clstoken=True), 4, 8, 5, 12),
+    "full_b32": (dict(out_dim=2), 32, 197, 77, 13),
+}
+
+
 def gen_framework():
     from oracle.weights import SMALL
     from oracle.tiny_model import TinyMMBT, tiny_batches, acc
@@ -175,18 +249,22 @@ def gen_framework():
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("--what", default="all", choices=["all", "small", "full", "framework"])
+    ap.add_argument("--what", default="all", choices=["all", "small", "full", "framework", "flava"])
     a = ap.parse_args()
     sys.path.insert(0, REPO)
     from oracle.weights import SMALL, FULL
     # each generator imports the reference fresh with its own stub config -> run each in a subprocess
     if a.what == "all":
         import subprocess
-        for w in ("small", "full", "framework"):
+        for w in ("small", "full", "framework", "flava"):
             subprocess.check_call([sys.executable, "-m", "oracle.gen_golden", "--what", w], cwd=REPO)
     elif a.what == "small":
         gen_mmbt("small_t16", SMALL, B=2, T=16, lens=[16, 9], seed=0)
     elif a.what == "full":
         gen_mmbt("full_t508", FULL, B=2, T=508, lens=[508, 300], seed=1)
+    elif a.what == "flava":
+        from oracle.flava_ref import FlavaConfig
+        for tag, (kw, B, Li, Lt, seed) in FLAVA_CASES.items():
+            gen_flava(tag, FlavaConfig(**kw), B, Li, Lt, seed)
     else:
         gen_framework()
