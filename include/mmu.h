@@ -49,7 +49,10 @@ enum {
   MMU_EPI_BIAS_GELU = 1,    /* z = acc+bias; C = gelu_erf(z); aux (optional) = gelu'(z)  */
   MMU_EPI_BIAS_DROP_RES = 2,/* C = residual + dropout(acc+bias)                          */
   MMU_EPI_DGELU = 3,        /* C = acc * aux   (aux = the forward's gelu'(z))            */
-  MMU_EPI_ADD_RES = 4       /* C = acc + residual                                        */
+  MMU_EPI_ADD_RES = 4,      /* C = acc + residual                                        */
+  MMU_EPI_BIAS_DROP_QGELU = 5 /* u = dropout(acc+bias); C = u*sigmoid(1.702u); aux (optional)
+                               = keep/(1-p) * d(u*sigmoid(1.702u))/du: FLAVA ResidualAttentionBlock
+                               mlp c_fc -> Dropout -> QuickGELU (src/model.py:183-185,196-198) */
 };
 typedef struct mmu_epilogue {
   int32_t kind;
@@ -135,6 +138,30 @@ int mmu_layernorm_bwd(const void* dY, const void* X, const float* mean, const fl
                       const float* w, void* dX, void* dXdrop, float drop_p, uint64_t seed,
                       float* part_dw, float* part_db, float* part_dbias,
                       int64_t rows, int64_t H, int64_t rows_per_part, mmu_stream_t stream);
+
+/* Pre-LN block backward (FLAVA ResidualAttentionBlock, src/model.py:210-212: x + f(LN(x))):
+ * dX = LN'(dY) + dRes; part_dbias = column sums of that total dX (the bias gradient of the
+ * Linear whose output was added to the residual stream).  No dropout output. */
+int mmu_layernorm_bwd_res(const void* dY, const void* X, const float* mean, const float* rstd,
+                          const float* w, const void* dRes, void* dX,
+                          float* part_dw, float* part_db, float* part_dbias,
+                          int64_t rows, int64_t H, int64_t rows_per_part, mmu_stream_t stream);
+
+/* ------------------------------------------------------------------ FLAVA attention
+ * nn.MultiheadAttention(x, x, x) with batch_first=False applied to an [S, N, E] tensor
+ * (src/model.py:193,205-207; the block receives [B, L, E], so the sequence axis is the
+ * BATCH: S = B samples, N = L token positions).  QKV [S*N, ld_qkv] bf16 = the in_proj
+ * output, row s*N + n, q at col h*D, k at E + h*D, v at 2E + h*D (E = heads*D).
+ * softmax(Q K^T / sqrt(D)) V per (n, h); no mask, no dropout (module defaults).
+ *   O [S*N, ld_o] bf16 (col h*D); LSE2 [N*heads, S] f32 = log2-sum-exp2 of the scores
+ *   scaled by log2(e)/sqrt(D) (for the backward).  D in {64, 128, 256}. */
+int mmu_seqattn_fwd(const void* QKV, int64_t ld_qkv, void* O, int64_t ld_o, float* LSE2,
+                    int64_t S, int64_t N, int64_t heads, int64_t head_dim, mmu_stream_t stream);
+/* dQKV [S*N, ld_dqkv] bf16 (every element written); delta workspace [N*heads, S] f32. */
+int mmu_seqattn_bwd(const void* QKV, int64_t ld_qkv, const void* O, int64_t ld_o,
+                    const void* dO, int64_t ld_do, const float* LSE2, float* delta,
+                    void* dQKV, int64_t ld_dqkv, int64_t S, int64_t N, int64_t heads,
+                    int64_t head_dim, mmu_stream_t stream);
 
 /* ------------------------------------------------------------------ embeddings
  * Modality-token embed + text gather + concat/gather, one pass

@@ -137,7 +137,7 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
     p.drop_p = epi->drop_p; p.seed = epi->seed;
   }
   p.kind = kind;
-  if (kind < 0 || kind > MMU_EPI_ADD_RES) return fail("mmu_gemm: bad epilogue kind %d", kind);
+  if (kind < 0 || kind > MMU_EPI_BIAS_DROP_QGELU) return fail("mmu_gemm: bad epilogue kind %d", kind);
   if (kind != MMU_EPI_STORE && c_dtype != MMU_BF16) return fail("mmu_gemm: fused epilogues write bf16");
   if (kind == MMU_EPI_DGELU && !p.aux) return fail("mmu_gemm: DGELU epilogue needs aux");
   if ((kind == MMU_EPI_BIAS_DROP_RES || kind == MMU_EPI_ADD_RES) && !p.residual)
@@ -313,10 +313,62 @@ int mmu_layernorm_bwd(const void* dY, const void* X, const float* mean, const fl
   if (!dY || !X || !mean || !rstd || !w || !dX) return fail("mmu_layernorm_bwd: null pointer");
   if (rows <= 0 || H <= 0 || H % 256 || H > 1024 || rows_per_part <= 0) return fail("mmu_layernorm_bwd: bad shape");
   if (drop_p < 0.f || drop_p >= 1.f) return fail("mmu_layernorm_bwd: drop_p out of range");
-  layernorm_bwd_launch((const bf16*)dY, (const bf16*)X, mean, rstd, w, (bf16*)dX, (bf16*)dXdrop, drop_p, seed, part_dw,
-                       part_db, part_dbias, rows, H, rows_per_part, (hipStream_t)stream);
+  layernorm_bwd_launch((const bf16*)dY, (const bf16*)X, mean, rstd, w, (bf16*)dX, (bf16*)dXdrop, nullptr, drop_p, seed,
+                       part_dw, part_db, part_dbias, rows, H, rows_per_part, (hipStream_t)stream);
   return check_launch("mmu_layernorm_bwd");
 }
+
+int mmu_layernorm_bwd_res(const void* dY, const void* X, const float* mean, const float* rstd, const float* w,
+                          const void* dRes, void* dX, float* part_dw, float* part_db, float* part_dbias, int64_t rows,
+                          int64_t H, int64_t rows_per_part, mmu_stream_t stream) {
+  if (!dY || !X || !mean || !rstd || !w || !dX || !dRes) return fail("mmu_layernorm_bwd_res: null pointer");
+  if (rows <= 0 || H <= 0 || H % 256 || H > 1024 || rows_per_part <= 0) return fail("mmu_layernorm_bwd_res: bad shape");
+  layernorm_bwd_launch((const bf16*)dY, (const bf16*)X, mean, rstd, w, (bf16*)dX, nullptr, (const bf16*)dRes, 0.f, 0,
+                       part_dw, part_db, part_dbias, rows, H, rows_per_part, (hipStream_t)stream);
+  return check_launch("mmu_layernorm_bwd_res");
+}
+
+static int seqattn_check(const char* what, int64_t ld_qkv, int64_t S, int64_t N, int64_t heads, int64_t D) {
+  if (S <= 0 || N <= 0 || heads <= 0) return fail("%s: bad shape", what);
+  if (D != 64 && D != 128 && D != 256) return fail("%s: head_dim %ld not in {64, 128, 256}", what, D);
+  if (ld_qkv < 3 * heads * D || ld_qkv % 8) return fail("%s: ld_qkv too small / unaligned", what);
+  if (N * heads > 65535) return fail("%s: N*heads > 65535", what);
+  return 0;
+}
+
+int mmu_seqattn_fwd(const void* QKV, int64_t ld_qkv, void* O, int64_t ld_o, float* LSE2, int64_t S, int64_t N,
+                    int64_t heads, int64_t head_dim, mmu_stream_t stream) {
+  if (!QKV || !O || !LSE2) return fail("mmu_seqattn_fwd: null pointer");
+  if (seqattn_check("mmu_seqattn_fwd", ld_qkv, S, N, heads, head_dim)) return 1;
+  if (ld_o < heads * head_dim || ld_o % 4) return fail("mmu_seqattn_fwd: bad ld_o");
+  SeqAttnParams p{};
+  p.qkv = (const bf16*)QKV; p.ld_qkv = ld_qkv;
+  p.out = (bf16*)O; p.ld_out = ld_o;
+  p.lse2 = LSE2;
+  p.S = (int)S; p.N = (int)N; p.heads = (int)heads; p.D = (int)head_dim; p.E = (int)(heads * head_dim);
+  p.scale = 1.0f / sqrtf((float)head_dim);
+  seqattn_fwd_launch(p, (hipStream_t)stream);
+  return check_launch("mmu_seqattn_fwd");
+}
+
+int mmu_seqattn_bwd(const void* QKV, int64_t ld_qkv, const void* O, int64_t ld_o, const void* dO, int64_t ld_do,
+                    const float* LSE2, float* delta, void* dQKV, int64_t ld_dqkv, int64_t S, int64_t N, int64_t heads,
+                    int64_t head_dim, mmu_stream_t stream) {
+  if (!QKV || !O || !dO || !LSE2 || !delta || !dQKV) return fail("mmu_seqattn_bwd: null pointer");
+  if (seqattn_check("mmu_seqattn_bwd", ld_qkv, S, N, heads, head_dim)) return 1;
+  if (ld_dqkv < 3 * heads * head_dim || ld_dqkv % 4 || ld_o % 4 || ld_do % 8) return fail("mmu_seqattn_bwd: bad ld");
+  SeqAttnParams p{};
+  p.qkv = (const bf16*)QKV; p.ld_qkv = ld_qkv;
+  p.o = (const bf16*)O; p.ld_o = ld_o;
+  p.dout = (const bf16*)dO; p.ld_do = ld_do;
+  p.out = (bf16*)dQKV; p.ld_out = ld_dqkv;
+  p.lse2 = (float*)LSE2; p.delta = delta;
+  p.S = (int)S; p.N = (int)N; p.heads = (int)heads; p.D = (int)head_dim; p.E = (int)(heads * head_dim);
+  p.scale = 1.0f / sqrtf((float)head_dim);
+  seqattn_bwd_launch(p, (hipStream_t)stream);
+  return check_launch("mmu_seqattn_bwd");
+}
+
 
 int mmu_embed_fwd(const int64_t* ids, const int64_t* seg, const int64_t* txt_mask, const float* proj, const float* word,
                   const float* pos, const float* type, const float* ln_w, const float* ln_b, float eps, int64_t cls_id,

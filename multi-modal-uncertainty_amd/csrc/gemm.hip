@@ -110,6 +110,27 @@ static __device__ __forceinline__ void epi_oct(const GemmParams& p, int64_t z, i
     }
 #pragma unroll
     for (int r = 0; r < 8; ++r) v[r] += bf2f(in[r]);  // residual
+  } else if (EPI == MMU_EPI_BIAS_DROP_QGELU) {  // FLAVA mlp: u = dropout(z); C = u*sigmoid(1.702u)
+    uint32_t keep = 0xFFu;                         // aux (optional) = dC/dz = keep*scale*qgelu'(u)
+    if (thr) {
+      const uint64_t q0 = (uint64_t)((z * p.M + m) * p.N + n) >> 2;
+      keep = mmu_keep4(p.seed, q0, thr) | (mmu_keep4(p.seed, q0 + 1, thr) << 4);
+    }
+    float d[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const float kz = ((keep >> r) & 1) ? scale : 0.f;
+      const float u = v[r] * kz;
+      const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u * -2.4554669595930157f));  // 1.702 log2 e
+      v[r] = u * sg;
+      d[r] = kz * fmaf(1.702f * u * sg, 1.0f - sg, sg);
+    }
+    if (aux) {
+      bf16x8 o;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) o[r] = f2bf(d[r]);
+      *(bf16x8*)(aux + m * p.ldx + n) = o;
+    }
   } else if (EPI == MMU_EPI_DGELU) {  // in = aux = gelu'(z) saved by the forward epilogue
 #pragma unroll
     for (int r = 0; r < 8; ++r) v[r] *= bf2f(in[r]);
@@ -717,6 +738,7 @@ void gemm_launch(const GemmParams& p, bool ak, bool bk, bool f32out, bool big, i
     case MMU_EPI_BIAS_DROP_RES: launch_e<MMU_EPI_BIAS_DROP_RES, false>(p, ak, bk, big, batch, s); break;
     case MMU_EPI_DGELU: launch_e<MMU_EPI_DGELU, false>(p, ak, bk, big, batch, s); break;
     case MMU_EPI_ADD_RES: launch_e<MMU_EPI_ADD_RES, false>(p, ak, bk, big, batch, s); break;
+    case MMU_EPI_BIAS_DROP_QGELU: launch_e<MMU_EPI_BIAS_DROP_QGELU, false>(p, ak, bk, big, batch, s); break;
   }
 }
 
@@ -811,6 +833,7 @@ void gemm_tail_launch(const GemmParams& p, bool f32out, int64_t m0, int S, const
     case MMU_EPI_BIAS_DROP_RES: TAIL(MMU_EPI_BIAS_DROP_RES, false); break;
     case MMU_EPI_DGELU: TAIL(MMU_EPI_DGELU, false); break;
     case MMU_EPI_ADD_RES: TAIL(MMU_EPI_ADD_RES, false); break;
+    case MMU_EPI_BIAS_DROP_QGELU: TAIL(MMU_EPI_BIAS_DROP_QGELU, false); break;
   }
 #undef TAIL
 }

@@ -72,7 +72,8 @@ template <int NV>  // H = 256 * NV
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ X,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ w, bf16* __restrict__ dX,
-                                                     bf16* __restrict__ dXd, float drop_p, uint64_t seed,
+                                                     bf16* __restrict__ dXd, const bf16* __restrict__ dR,
+                                                     float drop_p, uint64_t seed,
                                                      float* __restrict__ pdw, float* __restrict__ pdb,
                                                      float* __restrict__ pdbias, int64_t rows, int rpp) {
   constexpr int H = 256 * NV, nv = NV;
@@ -124,9 +125,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dY
       if (i < nv) {
         const int c = 256 * i + 4 * l;
         float dx[4];
+        bf16x4 rr{};
+        if (dR) rr = *(const bf16x4*)(dR + row * H + c);  // pre-LN block: + the residual's gradient
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           dx[e] = R.rs * (g[i][e] - s1 - xh[i][e] * s2);
+          if (dR) dx[e] += bf2f(rr[e]);
           aw[i][e] += dy[i][e] * xh[i][e];
           ab[i][e] += dy[i][e];
         }
@@ -183,11 +187,11 @@ void layernorm_fwd_launch(const bf16* X, const float* w, const float* b, bf16* Y
 }
 
 void layernorm_bwd_launch(const bf16* dY, const bf16* X, const float* mean, const float* rstd, const float* w,
-                          bf16* dX, bf16* dXdrop, float drop_p, uint64_t seed, float* pdw, float* pdb,
+                          bf16* dX, bf16* dXdrop, const bf16* dR, float drop_p, uint64_t seed, float* pdw, float* pdb,
                           float* pdbias, int64_t rows, int64_t H, int64_t rpp, hipStream_t s) {
   const dim3 g((unsigned)((rows + rpp - 1) / rpp));
-#define LNB(NV) hipLaunchKernelGGL(ln_bwd_kernel<NV>, g, dim3(256), 0, s, dY, X, mean, rstd, w, dX, dXdrop, drop_p, \
-                                   seed, pdw, pdb, pdbias, rows, (int)rpp)
+#define LNB(NV) hipLaunchKernelGGL(ln_bwd_kernel<NV>, g, dim3(256), 0, s, dY, X, mean, rstd, w, dX, dXdrop, dR, \
+                                   drop_p, seed, pdw, pdb, pdbias, rows, (int)rpp)
   switch (H / 256) {
     case 1: LNB(1); break;
     case 2: LNB(2); break;

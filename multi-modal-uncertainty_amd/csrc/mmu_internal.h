@@ -66,8 +66,26 @@ bool attention_bwd_fuses_colsum();
 void layernorm_fwd_launch(const bf16* X, const float* w, const float* b, bf16* Y, float* mean, float* rstd,
                           int64_t rows, int64_t H, float eps, int64_t group_rows, int64_t pstride, hipStream_t s);
 void layernorm_bwd_launch(const bf16* dY, const bf16* X, const float* mean, const float* rstd, const float* w,
-                          bf16* dX, bf16* dXdrop, float drop_p, uint64_t seed, float* pdw, float* pdb,
+                          bf16* dX, bf16* dXdrop, const bf16* dR, float drop_p, uint64_t seed, float* pdw, float* pdb,
                           float* pdbias, int64_t rows, int64_t H, int64_t rows_per_part, hipStream_t s);
+
+// FLAVA attention over the sequence (= batch) axis, flava.hip
+struct SeqAttnParams {
+  const bf16* qkv;
+  int64_t ld_qkv;
+  const bf16* o;
+  int64_t ld_o;
+  const bf16* dout;
+  int64_t ld_do;
+  bf16* out;  // O (fwd) or dQKV (bwd)
+  int64_t ld_out;
+  float* lse2;   // [N*heads][S] log2-sum-exp2 of the log2-scaled scores
+  float* delta;  // bwd workspace [N*heads][S]
+  int S, N, heads, E, D;
+  float scale;
+};
+void seqattn_fwd_launch(const SeqAttnParams& p, hipStream_t s);
+void seqattn_bwd_launch(const SeqAttnParams& p, hipStream_t s);
 
 struct EmbedParams {
   const int64_t *ids, *seg, *txt_mask, *idx;

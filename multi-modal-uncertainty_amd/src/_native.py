@@ -13,7 +13,7 @@ c_i64, c_i32, c_f32, c_u64, c_vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_floa
 c_f32p, c_i64p, c_dp = ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)
 
 MMU_BF16, MMU_F32 = 0, 1
-EPI_STORE, EPI_BIAS_GELU, EPI_BIAS_DROP_RES, EPI_DGELU, EPI_ADD_RES = range(5)
+EPI_STORE, EPI_BIAS_GELU, EPI_BIAS_DROP_RES, EPI_DGELU, EPI_ADD_RES, EPI_BIAS_DROP_QGELU = range(6)
 
 
 class Epilogue(ctypes.Structure):
@@ -39,6 +39,11 @@ SIGNATURES = {
     "mmu_layernorm_fwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_i64, c_i64, c_vp]),
     "mmu_layernorm_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp, c_vp, c_vp,
                                   c_i64, c_i64, c_i64, c_vp]),
+    "mmu_layernorm_bwd_res": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                      c_i64, c_vp]),
+    "mmu_seqattn_fwd": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp]),
+    "mmu_seqattn_bwd": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64,
+                                c_i64, c_vp]),
     "mmu_embed_fwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_i64, c_i64, c_vp,
                               c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_f32, c_f32, c_u64, c_vp, c_vp, c_vp, c_vp,
                               c_vp]),

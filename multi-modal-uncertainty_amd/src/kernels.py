@@ -9,7 +9,8 @@ import ctypes
 import torch
 
 from . import _native as N
-from ._native import Epilogue, EPI_STORE, EPI_BIAS_GELU, EPI_BIAS_DROP_RES, EPI_DGELU, EPI_ADD_RES  # noqa: F401
+from ._native import (Epilogue, EPI_STORE, EPI_BIAS_GELU, EPI_BIAS_DROP_RES, EPI_DGELU, EPI_ADD_RES,  # noqa: F401
+                      EPI_BIAS_DROP_QGELU)
 
 
 def _dev_check(*ts):
@@ -176,6 +177,34 @@ def layernorm_bwd(dY, X, mean, rstd, w, dX, dXdrop=None, drop_p=0.0, seed=0, par
     N.call("mmu_layernorm_bwd", _ptr(dY), _ptr(X), _ptr(mean), _ptr(rstd), _ptr(w), _ptr(dX), _ptr(dXdrop),
            float(drop_p), int(seed), _ptr(part_dw), _ptr(part_db), _ptr(part_dbias), rows, H, LN_ROWS_PER_PART,
            _stream(X))
+
+
+def layernorm_bwd_res(dY, X, mean, rstd, w, dRes, dX, part_dw=None, part_db=None, part_dbias=None):
+    """Pre-LN backward: dX = LN'(dY) + dRes (part_dbias = column sums of that dX)."""
+    _dev_check(dY, X, mean, rstd, w, dRes, dX)
+    rows, H = X.shape
+    N.call("mmu_layernorm_bwd_res", _ptr(dY), _ptr(X), _ptr(mean), _ptr(rstd), _ptr(w), _ptr(dRes), _ptr(dX),
+           _ptr(part_dw), _ptr(part_db), _ptr(part_dbias), rows, H, LN_ROWS_PER_PART, _stream(X))
+
+
+def seqattn_fwd(qkv, O, lse2, S, N_, heads):
+    """FLAVA attention over the sequence (= batch) axis; see mmu_seqattn_fwd."""
+    _dev_check(qkv, O, lse2)
+    _want(qkv, torch.bfloat16, "seqattn qkv")
+    D = qkv.shape[1] // (3 * heads)
+    if lse2.numel() < S * N_ * heads:
+        raise ValueError("seqattn_fwd: lse2 too small")
+    N.call("mmu_seqattn_fwd", _ptr(qkv), qkv.stride(0), _ptr(O), O.stride(0), _ptr(lse2), S, N_, heads, D,
+           _stream(qkv))
+
+
+def seqattn_bwd(qkv, O, dO, lse2, delta, dqkv, S, N_, heads):
+    _dev_check(qkv, O, dO, lse2, delta, dqkv)
+    D = qkv.shape[1] // (3 * heads)
+    if delta.numel() < S * N_ * heads:
+        raise ValueError("seqattn_bwd: delta too small")
+    N.call("mmu_seqattn_bwd", _ptr(qkv), qkv.stride(0), _ptr(O), O.stride(0), _ptr(dO), dO.stride(0), _ptr(lse2),
+           _ptr(delta), _ptr(dqkv), dqkv.stride(0), S, N_, heads, D, _stream(qkv))
 
 
 def ln_parts(rows):

@@ -8,7 +8,10 @@ Cited reference lines:
 * LayerNorm (fp32 inside)       src/model.py:174-180 (nn.LayerNorm, eps 1e-5)
 * QuickGELU                     src/model.py:183-185   x * sigmoid(1.702 x)
 * ResidualAttentionBlock        src/model.py:188-212   pre-LN; x + attn(ln_1 x); x + mlp(ln_2 x);
-                                mlp = c_fc -> Dropout -> QuickGELU -> c_proj -> Dropout (:196-200)
+                                mlp = OrderedDict(c_fc, dropout, gelu, c_proj, dropout) (:196-200):
+                                the repeated "dropout" key keeps its FIRST position, so the
+                                Sequential is c_fc -> Dropout -> QuickGELU -> c_proj (no
+                                trailing dropout)
 * nn.MultiheadAttention quirk   src/model.py:193,207   batch_first=False while the block receives
                                 [B, L, E]: the attention runs over the BATCH axis (sequence = B,
                                 "batch" = the L token positions), per head of E / n_head dims
@@ -124,8 +127,7 @@ def block(x, sd, i, cfg, train=False, gen=None):
     h = _ln(x, sd, p + "ln_2.") @ sd[p + "mlp.c_fc.weight"].t() + sd[p + "mlp.c_fc.bias"]
     h = _dropout(h, cfg.drop, train, gen)
     h = h * torch.sigmoid(1.702 * h)
-    h = h @ sd[p + "mlp.c_proj.weight"].t() + sd[p + "mlp.c_proj.bias"]
-    return x + _dropout(h, cfg.drop, train, gen)
+    return x + h @ sd[p + "mlp.c_proj.weight"].t() + sd[p + "mlp.c_proj.bias"]
 
 
 def forward(sd, img, txt, cfg, train=False, gen=None):

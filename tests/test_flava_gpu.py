@@ -1,0 +1,166 @@
+"""FLAVA fusion transformer on the HIP path (src/model.py) against plain PyTorch fp32 (kernels)
+and against the oracle pinned to the reference's own src/model.py (tests/golden/flava_*).
+
+Tolerances: bf16 activations with f32 accumulation -> kernel outputs within 1e-2 of their
+scale; model logits within 2e-2 * max|logit| + 2e-3 (the MMBT bar); per-tensor
+gradient norms within 5 %.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def K():
+    from src import kernels
+    return kernels
+
+
+def rnd(*shape, dev, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dev).to(torch.bfloat16)
+
+
+def close(a, b, frac=1e-2):
+    a, b = a.float(), b.float()
+    scale = b.abs().max().item() + 1e-6
+    err = (a - b).abs().max().item()
+    assert err <= frac * scale, f"max err {err:.3e} vs scale {scale:.3e}"
+
+
+def seq_ref(qkv, S, N, heads):
+    """nn.MultiheadAttention math over the sample axis (src/model.py:205-207), fp32."""
+    E = qkv.shape[1] // 3
+    D = E // heads
+    q, k, v = (t.float().reshape(S, N * heads, D).transpose(0, 1) for t in qkv.split(E, dim=1))
+    a = torch.softmax(q @ k.transpose(1, 2) / math.sqrt(D), dim=-1)
+    return (a @ v).transpose(0, 1).reshape(S * N, E)
+
+
+@pytest.mark.parametrize("S,N,heads", [(5, 3, 3), (64, 2, 3), (100, 3, 3), (130, 2, 3), (70, 2, 12), (33, 2, 6)])
+def test_seqattn_fwd_bwd(dev, S, N, heads):
+    k = K()
+    E = 768
+    qkv = rnd(S * N, 3 * E, dev=dev, seed=1)
+    O = torch.empty(S * N, E, dtype=torch.bfloat16, device=dev)
+    lse2 = torch.empty(N * heads, S, device=dev)
+    k.seqattn_fwd(qkv, O, lse2, S, N, heads)
+    q32 = qkv.float().requires_grad_(True)
+    ref = seq_ref(q32, S, N, heads)
+    close(O, ref)
+    dO = rnd(S * N, E, dev=dev, seed=2)
+    ref.backward(dO.float())
+    dqkv = torch.full((S * N, 3 * E), float("nan"), dtype=torch.bfloat16, device=dev)
+    delta = torch.empty(N * heads, S, device=dev)
+    k.seqattn_bwd(qkv, O, dO, lse2, delta, dqkv, S, N, heads)
+    assert torch.isfinite(dqkv.float()).all(), "dQKV not fully written"
+    for i in range(3):
+        close(dqkv[:, i * E:(i + 1) * E], q32.grad[:, i * E:(i + 1) * E], frac=2e-2)
+
+
+def test_gemm_bias_dropout_quickgelu(dev):
+    k = K()
+    M, N, Kd = 300, 384, 256
+    A, B = rnd(M, Kd, dev=dev, seed=3), rnd(N, Kd, dev=dev, seed=4, scale=0.1)
+    bias = torch.randn(N, device=dev) * 0.1
+    C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    aux = torch.empty_like(C)
+    k.gemm(A, Kd, True, B, Kd, True, C, N, M, N, Kd, epi=k.epilogue(k.EPI_BIAS_DROP_QGELU, bias=bias, aux=aux))
+    z = (A.float() @ B.float().t() + bias).requires_grad_(True)
+    ref = z * torch.sigmoid(1.702 * z)
+    close(C, ref)
+    ref.backward(torch.ones_like(ref))
+    close(aux, z.grad)
+    # with dropout: dropped elements are exactly 0 in both outputs, kept ones are qgelu(z / (1-p))
+    p = 0.25
+    k.gemm(A, Kd, True, B, Kd, True, C, N, M, N, Kd,
+           epi=k.epilogue(k.EPI_BIAS_DROP_QGELU, bias=bias, aux=aux, drop_p=p, seed=1234))
+    kept = aux.float() != 0
+    frac = 1 - kept.float().mean().item()
+    assert abs(frac - p) < 0.02, frac
+    u = z.detach() / (1 - p)
+    close(torch.where(kept, C.float(), 0.0), torch.where(kept, u * torch.sigmoid(1.702 * u), 0.0))
+    assert (C.float()[~kept] == 0).all()
+
+
+def test_layernorm_bwd_res(dev):
+    k = K()
+    M, H = 300, 768
+    x = rnd(M, H, dev=dev, seed=5)
+    w, b = torch.rand(H, device=dev) + 0.5, torch.randn(H, device=dev) * 0.1
+    y = torch.empty_like(x)
+    mean, rstd = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    k.layernorm_fwd(x, w, b, y, mean, rstd, 1e-5)
+    dy, dres = rnd(M, H, dev=dev, seed=6), rnd(M, H, dev=dev, seed=7)
+    P = k.ln_parts(M)
+    pw, pb, pbias = (torch.empty(P, H, device=dev) for _ in range(3))
+    dx = torch.empty_like(x)
+    k.layernorm_bwd_res(dy, x, mean, rstd, w, dres, dx, pw, pb, pbias)
+    xr = x.float().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    torch.nn.functional.layer_norm(xr, (H,), wr, br, 1e-5).backward(dy.float())
+    close(dx, xr.grad + dres.float())
+    close(pw.sum(0), wr.grad)
+    close(pb.sum(0), br.grad)
+    close(pbias.sum(0), (xr.grad + dres.float()).sum(0))
+
+
+CASES = {"vanilla": dict(out_dim=1), "multihead_avgpool": dict(out_dim=2, avg_pool=True),
+         "cls_multihead": dict(out_dim=2, clstoken=True), "full_b32": dict(out_dim=2)}
+
+
+def build(tag, dev):
+    import os
+    from oracle import flava_ref as FR
+    from src.model import FlavaFusionTransfomer, FlavaFusionTransfomerwithCLSToken
+    gold = os.path.join(os.path.dirname(__file__), "golden", f"flava_{tag}.npz")
+    g = np.load(gold)
+    cfg = FR.FlavaConfig(**CASES[tag])
+    sd = FR.make_state_dict(int(g["seed"]), cfg)
+    cls = FlavaFusionTransfomerwithCLSToken if cfg.clstoken else FlavaFusionTransfomer
+    m = cls(out_dim=cfg.out_dim, num_classes=cfg.n_classes, multimodal_num_attention_heads=cfg.heads,
+            multimodal_num_hidden_layers=cfg.layers, drop=cfg.drop, avg_pool=cfg.avg_pool)
+    m.load_state_dict(sd, strict=True)
+    m = m.to(dev)
+    img, txt, y = FR.make_inputs(int(g["B"]), int(g["L_img"]), int(g["L_txt"]), cfg.n_classes, cfg.out_dim,
+                                 int(g["seed"]) + 1)
+    return g, cfg, sd, m, img.to(dev), txt.to(dev), y.to(dev)
+
+
+@pytest.mark.parametrize("tag", list(CASES))
+def test_flava_matches_reference_golden(dev, tag):
+    g, cfg, sd, m, img, txt, y = build(tag, dev)
+    m.eval()
+    with torch.no_grad():
+        lo = m((img, txt))
+    ref = torch.as_tensor(g["logits"]).to(dev)
+    tol = 2e-2 * ref.abs().max().item() + 2e-3
+    assert (lo - ref).abs().max().item() <= tol, ((lo - ref).abs().max().item(), tol)
+    assert abs(m.compute_loss(lo, y, eval=True).item() - float(g["loss_eval"])) < 2e-2
+    # train step (dropout 0): loss and every parameter's gradient norm
+    m.train()
+    y2 = y.unsqueeze(1).repeat(1, cfg.out_dim)
+    loss = m.compute_loss(m((img, txt)), y2)
+    loss.backward()
+    assert abs(loss.item() - float(g["loss_train"])) < 2e-2 * max(1.0, float(g["loss_train"]))
+    norms = np.array([float(p.grad.double().norm()) for _, p in m.named_parameters()])
+    ref_n = g["grad_norms"]
+    rel = np.abs(norms - ref_n) / np.maximum(ref_n, 1e-3 * ref_n.max())
+    assert rel.max() < 5e-2, (rel.max(), [n for (n, _), r in zip(m.named_parameters(), rel) if r >= 5e-2])
+
+
+def test_flava_mc_dropout_and_eval_determinism(dev):
+    g, cfg, sd, m, img, txt, y = build("vanilla", dev)
+    for blk in m.mm_encoder.resblocks:
+        blk.mlp.dropout.p = 0.2
+    m.eval()
+    with torch.no_grad():
+        a, b = m((img, txt)), m((img, txt))
+    assert torch.equal(a, b), "eval must not drop"
+    m.train()
+    with torch.no_grad():
+        c, d = m((img, txt)), m((img, txt))
+    assert not torch.equal(c, d), "train-mode passes must draw fresh dropout masks"
