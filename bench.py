@@ -12,6 +12,8 @@ samples over the N ranks ("scaling": "strong"; DESIGN.md §6 has both measured).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+  python bench.py --workload flava     BASELINE config 5: the FLAVA fusion transformer
+                                       (src/model.py) train step on synthetic embeddings
 
 Rank 0 prints one JSON line (see README/DESIGN for the field definitions).
 """
@@ -45,6 +47,9 @@ def parse():
                     help="split this many samples over the ranks instead (strong scaling)")
     ap.add_argument("--text-len", type=int, default=508, help="word-pieces per sample (L = 5 + this)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", default="mmbt", choices=["mmbt", "flava"])
+    ap.add_argument("--flava-batch", type=int, default=128, help="FLAVA per-rank batch (train.py --batch_size)")
+    ap.add_argument("--flava-tokens", type=str, default="197,77", help="FLAVA image,text embedding lengths")
     ap.add_argument("--cpu-batch", type=int, default=2)
     ap.add_argument("--cpu-threads", type=int, default=16)
     return ap.parse_args()
@@ -106,6 +111,116 @@ def gemm_traffic():
     return {"bytes": round(d["traffic_bytes_per_launch"]), "source": os.path.relpath(files[-1], here)}
 
 
+def flava_cpu_baseline(args, L_img, L_txt, B=16):
+    """The oracle's fp32 FLAVA train step (oracle/flava_ref.py) on host cores."""
+    from oracle import flava_ref as FR
+    torch.set_num_threads(args.cpu_threads)
+    cfg = FR.FlavaConfig(out_dim=2)
+    sd = {k: v.requires_grad_(True) for k, v in FR.make_state_dict(0, cfg).items()}
+    img, txt, y = FR.make_inputs(B, L_img, L_txt, 2, 2, 0)
+    opt = torch.optim.AdamW(list(sd.values()), lr=1e-4, betas=(0.9, 0.98), eps=1e-9, weight_decay=0.001)
+
+    def one():
+        opt.zero_grad()
+        i2, t2, y2 = FR.data_forming(img, txt, y, "train", "MultiHead")
+        FR.compute_loss(FR.forward(sd, i2, t2, cfg, train=True), y2).backward()
+        opt.step()
+    one()
+    n = 3
+    t0 = time.perf_counter()
+    for _ in range(n):
+        one()
+    dt = time.perf_counter() - t0
+    return {"value": round(B * n / dt, 3), "unit": "samples/s", "cores": args.cpu_threads, "kind": "port",
+            "sample": f"oracle fp32 FLAVA train step (fwd+bwd+AdamW), B={B}, L={L_img}+{L_txt}, {n} timed steps "
+                      f"after 1 warm-up, torch CPU {torch.get_num_threads()} threads"}
+
+
+def bench_flava(args, world, rank, dev):
+    """BASELINE config 5: one optimizer step of the FLAVA fusion transformer (reference
+    train.py:184-216 setup: MultiHead out_dim 2, AdamW, per-batch cosine schedule) on a
+    synthetic batch of precomputed FLAVA embeddings [B, 197, 768] + [B, 77, 768]."""
+    from src import encoder
+    from src.model import FlavaFusionTransfomer
+    from transformers.optimization import get_cosine_schedule_with_warmup
+    L_img, L_txt = (int(v) for v in args.flava_tokens.split(","))
+    B = args.flava_batch
+    torch.manual_seed(1234)
+    model = FlavaFusionTransfomer(out_dim=2, num_classes=2, avg_pool=False).to(dev)
+    if world > 1:
+        for p in model.parameters():
+            dist.broadcast(p.data, 0)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, betas=(0.9, 0.98), eps=1e-9, weight_decay=0.001)
+    sched = get_cosine_schedule_with_warmup(opt, 100, 10000)
+    g = torch.Generator().manual_seed(100 + rank)
+    img = torch.randn(B, L_img, 768, generator=g).to(dev)
+    txt = torch.randn(B, L_txt, 768, generator=g).to(dev)
+    y = torch.randint(0, 2, (B,), generator=g).to(dev).unsqueeze(1).repeat(1, 2)
+    model.train()
+    params = list(model.parameters())
+
+    def step():
+        opt.zero_grad()
+        loss = model.compute_loss(model((img, txt)), y)
+        loss.backward()
+        if world > 1:
+            grads = [p.grad for p in params]
+            flat = torch._utils._flatten_dense_tensors(grads)
+            dist.all_reduce(flat)
+            flat.mul_(1.0 / world)
+            for gr, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
+                gr.copy_(f)
+        opt.step()
+        sched.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    encoder.block_timing(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    block_ms, block_n = encoder.block_timing_read()
+    encoder.block_timing(False)
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    E, L = 768, L_img + L_txt
+    # per sample and layer, forward: L (24 E^2 + 4 S E) with the attention's sequence S = B
+    layer_fwd = L * (24 * E * E + 4 * B * E)
+    block_tf = 3 * layer_fwd * B * (block_n / 2) / (block_ms * 1e-3) / 1e12 if block_ms > 0 else 0.0
+    ms_step = 1000.0 * dt / args.steps
+    out = {
+        "metric": "FLAVA fusion-transformer train samples/sec (BASELINE config 5, Hateful Memes embeddings)",
+        "value": round(B * world * args.steps / dt, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded FLAVA-shaped embeddings; random-init weights)",
+        "config": {"workload": "flava_fusion_train_step", "model": "FlavaFusionTransfomer 3 layers x 768, 3 heads",
+                   "per_rank_batch": B, "global_batch": B * world, "tokens": f"{L_img}+{L_txt}",
+                   "model_type": "MultiHead", "optimizer": "AdamW (torch)", "parallelism": f"dp{world}"},
+        "fused_block_roofline": {
+            "bound": "mfma", "flop_per_sample_per_layer": 3 * layer_fwd, "achieved": round(block_tf, 1),
+            "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(block_tf / PEAK_BF16_TFLOPS, 4),
+            "ms_per_layer_fwd_bwd": round(block_ms / max(block_n, 1) * 2, 4), "layer_passes_timed": block_n,
+            "share_of_step": round(block_ms / args.steps / ms_step, 3) if ms_step else None},
+        "final_loss": round(float(loss.item()), 4),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = flava_cpu_baseline(args, L_img, L_txt)
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -116,6 +231,13 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    if args.workload == "flava":
+        out = bench_flava(args, world, rank, dev)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if args.global_batch is None:
         args.global_batch = args.per_rank_batch * world
         scaling = "weak"

@@ -184,3 +184,120 @@ class SyntheticFood101(Dataset):
         img = torch.randn(3, 224, 224, generator=g)
         y = torch.randint(0, self.n_classes, (1,), generator=g)
         return ids, torch.ones(T), img, y
+
+
+# ------------------------------------------------------------------------------ FLAVA
+# Precomputed FLAVA embeddings of Hateful Memes (src/dataset.py:177-226, 287-336 of the
+# reference; BASELINE config 5).  The embeddings are written by data/encoding_with_flava.py
+# (needs the remote facebook/flava-full weights: not reproducible offline), one
+# `<name>.img` [L_img, 768] and `<name>.text` [L_txt, 768] tensor file per meme.
+def data_forming_func_transformer(x, y, phase, model_type):
+    """Labels per member / MIMO instance shuffles (reference src/dataset.py:30-54)."""
+    img, txt = x
+    if model_type == "Vanilla" and phase == "train":
+        y = y.unsqueeze(1).repeat(1, 1)
+    elif model_type == "MultiHead" and phase == "train":
+        y = y.unsqueeze(1).repeat(1, 2)
+    elif model_type == "MIMO-shuffle-instance" and phase == "train":
+        idx = torch.randperm(img.size(0))
+        img = img[idx]
+        y_img = y[idx]
+        idx = torch.randperm(img.size(0))
+        txt = txt[idx]
+        y_txt = y[idx]
+        y = torch.stack([y_img, y_txt], dim=1)
+    return (img, txt), y
+
+
+class BaseDataset(Dataset):
+    """`<predix_dir>/<phase>.jsonl` metadata minus the listed encoder failures
+    (reference src/dataset.py:177-193)."""
+
+    def __init__(self, predix_dir, phase, label_dict=None, error_cases_remover=True, **kwargs):
+        import pandas as pd
+        self.meta_data = pd.read_json(os.path.join(predix_dir, f"{phase}.jsonl"), lines=True)
+        self.label_dict = label_dict
+        print(f"Loaded {len(self.meta_data)} samples from {phase} set.")
+        if error_cases_remover:
+            with open(os.path.join(predix_dir, "flava_embeds", f"{phase}_error_cases.txt"), "r") as f:
+                error_cases = [int(x) for x in f.read().split("\n")[:-1]]
+            self.meta_data = self.meta_data.drop(labels=error_cases, axis=0)
+            print(f"Loaded {len(self.meta_data)} samples from {phase} set after removing {len(error_cases)} "
+                  f"error cases.")
+
+    def __len__(self):
+        return len(self.meta_data)
+
+
+class FlavaEncodedDataset(BaseDataset):
+    """(image embeddings, text embeddings, label) per meme (reference src/dataset.py:196-213).
+    The tensor files are read with torch.load(weights_only=True): they hold plain tensors."""
+
+    def __init__(self, predix_dir, phase, label_dict, error_cases_remover=True, **kwargs):
+        super().__init__(predix_dir, phase, label_dict, error_cases_remover, **kwargs)
+        assert "name_extractor" in kwargs
+        self.name_extractor = kwargs["name_extractor"]
+        self.emb_dir = os.path.join(predix_dir, "flava_embeds")
+
+    def __getitem__(self, idx):
+        save_name = self.name_extractor(self.meta_data.iloc[idx]["img"])
+        img = torch.load(os.path.join(self.emb_dir, save_name + ".img"), weights_only=True)
+        txt = torch.load(os.path.join(self.emb_dir, save_name + ".text"), weights_only=True)
+        label = torch.LongTensor([self.label_dict.index(self.meta_data.iloc[idx]["label"])])
+        return img, txt, label
+
+
+def collate_fn_flava(batch):
+    """Zero-pad image / text embedding sequences to the batch maximum (reference :216-226)."""
+    from torch.nn.utils.rnn import pad_sequence
+    imgs, txts, labels = [], [], []
+    for i, t, lab in batch:
+        imgs.append(i)
+        txts.append(t)
+        labels.append(lab)
+    imgs = pad_sequence(imgs, batch_first=True, padding_value=0.)
+    txts = pad_sequence(txts, batch_first=True, padding_value=0.)
+    return (imgs, txts), torch.tensor(labels)
+
+
+def get_dataset(training, dev, testing, collate_func, args, sampler=None):
+    """Loaders over the (optionally sub-sampled) training set (reference :287-321)."""
+    torch.manual_seed(args.seed)
+    n = len(training) if args.sample_size is None else args.sample_size
+    training_sub = torch.utils.data.Subset(training, list(range(len(training)))[:n])
+    mk = lambda ds, shuffle, smp=None: torch.utils.data.DataLoader(  # noqa: E731
+        ds, batch_size=args.batch_size, shuffle=shuffle and smp is None, sampler=smp, collate_fn=collate_func,
+        pin_memory=torch.cuda.is_available())
+    if sampler is not None:
+        sampler = sampler(training_sub)
+    train = mk(training_sub, True, sampler)
+    print("training_loader LENGTH:", len(train))
+    return train, mk(dev, False), mk(testing, False)
+
+
+def get_dataset_flava(args, datapath, sampler=None):
+    kw = dict(name_extractor=args.name_extractor)
+    return get_dataset(FlavaEncodedDataset(datapath, "train", args.labels, args.error_cases_remover, **kw),
+                       FlavaEncodedDataset(datapath, "dev", args.labels, args.error_cases_remover, **kw),
+                       FlavaEncodedDataset(datapath, "test", args.labels, args.error_cases_remover, **kw),
+                       collate_fn_flava, args, sampler)
+
+
+class SyntheticFlava(Dataset):
+    """Seeded stand-in for FlavaEncodedDataset items: 197 image-patch embeddings (FLAVA
+    ViT-B/16 at 224^2 + CLS) and a text embedding sequence of random length <= max_text."""
+
+    def __init__(self, n, l_img=197, max_text=77, min_text=None, n_classes=2, width=768, seed=0):
+        self.n, self.l_img, self.max_text, self.n_classes, self.width = n, l_img, max_text, n_classes, width
+        self.min_text = max_text if min_text is None else min_text
+        self.seed = seed
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        g = torch.Generator().manual_seed(self.seed * 1000003 + i)
+        T = int(torch.randint(self.min_text, self.max_text + 1, (1,), generator=g))
+        img = torch.randn(self.l_img, self.width, generator=g)
+        txt = torch.randn(T, self.width, generator=g)
+        return img, txt, torch.randint(0, self.n_classes, (1,), generator=g)

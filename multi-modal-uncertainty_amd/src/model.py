@@ -32,6 +32,7 @@ from typing import Any
 import torch
 import torch.nn as nn
 
+from . import encoder as _enc  # block_timing: bench.py's fused-block roofline
 from . import kernels as K
 
 bf16 = torch.bfloat16
@@ -133,6 +134,7 @@ class BlockFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, heads, drop, seed, win, bin_, wo, bo, l1w, l1b, w1, b1, w2, b2, l2w, l2b):
+        e0 = _enc._mark()
         B, L, E = x.shape
         M, dev = B * L, x.device
         X = _rows(x.contiguous())
@@ -160,12 +162,15 @@ class BlockFunction(torch.autograd.Function):
                epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=b2, residual=x1))
         ctx.save_for_backward(X, h1, m1, r1, qkv, O, lse2, x1, h2, m2, r2, Hh, Zd, Win, Wo, W1, W2, l1w, l2w)
         ctx.meta = (B, L, E, heads)
+        if e0 is not None:
+            _enc._block_events.append((e0, _enc._mark()))
         return y.view(B, L, E)
 
     @staticmethod
     def backward(ctx, dy):
         (X, h1, m1, r1, qkv, O, lse2, x1, h2, m2, r2, Hh, Zd, Win, Wo, W1, W2, l1w, l2w) = ctx.saved_tensors
         B, L, E, heads = ctx.meta
+        e0 = _enc._mark()
         M, dev, f32 = B * L, X.device, torch.float32
         dY = _rows(dy.contiguous()).to(bf16)
         acc = K.epilogue(K.EPI_STORE, accumulate=True)
@@ -213,6 +218,8 @@ class BlockFunction(torch.autograd.Function):
         for k, part in (("l1w", pw1), ("l1b", pb1)):
             g[k] = torch.zeros(E, dtype=f32, device=dev)
             K.colsum_reduce(part, g[k])
+        if e0 is not None:
+            _enc._block_events.append((e0, _enc._mark()))
         return (dx.view(B, L, E), None, None, None, g["win"], g["bin"], g["wo"], g["bo"], g["l1w"], g["l1b"],
                 g["w1"], g["b1"], g["w2"], g["b2"], g["l2w"], g["l2b"])
 

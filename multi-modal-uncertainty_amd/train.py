@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""MMBT training entry point -- same command line as the reference train.py
-(flags train.py:31-90, MMBT setup :132-162, resume :269-285, callbacks :287-305,
-Model_.train_loop :312-330) on the MI355X HIP path.
+"""MMBT / FLAVA training entry point -- same command line as the reference train.py
+(flags train.py:31-90, MMBT setup :132-162, FLAVA setup :184-216, resume :269-285,
+callbacks :287-305, Model_.train_loop :312-330) on the MI355X HIP path.
 
 Additions (all optional):
   --gin_file F [F ...] / --gin_param 'train.lr=5e-5'   gin-style bindings onto the flags (src/gin.py)
@@ -9,7 +9,8 @@ Additions (all optional):
   data parallel      launch with torch.distributed.run: one rank per GPU, RCCL all-reduce,
                      train set sharded per rank, val/test evaluated whole on every rank,
                      rank 0 writes history / checkpoints.
-The ViLT / FLAVA branches (other model families) are out of scope and refused.
+  --synthetic with --framework flava: seeded FLAVA embeddings (197 image + <= 77 text tokens)
+The ViLT branch (another model family, remote weights) is out of scope and refused.
 """
 import argparse
 import logging
@@ -114,6 +115,57 @@ def setup_mmbt(args):
     return args, model, optimizer, scheduler
 
 
+def setup_flava(args, steps_per_epoch):
+    """reference train.py:184-216: fusion transformer, AdamW, cosine schedule with warmup."""
+    from functools import partial
+    from transformers.optimization import get_cosine_schedule_with_warmup
+    from src.model import FlavaFusionTransfomer, FlavaFusionTransfomerwithCLSToken
+    model_cls = FlavaFusionTransfomerwithCLSToken if args.clstoken else FlavaFusionTransfomer
+    model = model_cls(out_dim=1 if args.model_type == "Vanilla" else 2, num_classes=args.n_classes,
+                      multimodal_num_attention_heads=args.multimodal_num_attention_heads,
+                      multimodal_num_hidden_layers=args.multimodal_num_hidden_layers,
+                      drop=args.dropout, avg_pool=args.avg_pool)
+    optimizer = torch.optim.AdamW(model.parameters(), lr=args.lr, betas=(0.9, 0.98), eps=1.0e-9,
+                                  weight_decay=args.wd)
+    scheduler = get_cosine_schedule_with_warmup(optimizer, num_warmup_steps=steps_per_epoch * 3,
+                                                num_training_steps=steps_per_epoch * args.n_epochs)
+    args.scheduler_step_on, args.scheduler_metric = "batch", None
+    args.data_forming_func = partial(dataset.data_forming_func_transformer, model_type=args.model_type)
+    args.metrics = [acc]
+    return args, model, optimizer, scheduler
+
+
+def flava_data(args, rank=0, world=1):
+    sampler = (lambda ds: torch.utils.data.DistributedSampler(ds, world, rank, shuffle=True, seed=args.seed)) \
+        if world > 1 else None
+    if args.synthetic:
+        n = args.synthetic
+        tr = dataset.SyntheticFlava(n, min_text=8, n_classes=args.n_classes, seed=1)
+        va = dataset.SyntheticFlava(max(n // 8, args.batch_size), min_text=8, n_classes=args.n_classes, seed=2)
+        te = dataset.SyntheticFlava(max(n // 8, args.batch_size), min_text=8, n_classes=args.n_classes, seed=3)
+        return dataset.get_dataset(tr, va, te, dataset.collate_fn_flava, args, sampler)
+    return dataset.get_dataset_flava(args, args.datapath, sampler)
+
+
+def _dp_wrap_flat(model, optimizer):
+    """DP for a model without the MMBT parameter store (FLAVA): one flat RCCL all-reduce
+    (average) of every gradient before each optimizer step."""
+    import torch.distributed as dist
+    for p in model.parameters():
+        dist.broadcast(p.data, 0)
+    step = optimizer.step
+
+    def dp_step(*a, **k):
+        grads = [p.grad for p in model.parameters() if p.grad is not None]
+        flat = torch._utils._flatten_dense_tensors(grads)
+        dist.all_reduce(flat)
+        flat.mul_(1.0 / dist.get_world_size())
+        for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
+            g.copy_(f)
+        return step(*a, **k)
+    optimizer.step = dp_step
+
+
 def food101_data(args, rank=0, world=1):
     if args.synthetic:
         from src.testing import _Vocab
@@ -172,14 +224,19 @@ def main(argv=None):
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         args.device = local
     print(args)
-    if args.framework != "mmbt":
-        raise NotImplementedError(f"--framework {args.framework}: only the MMBT path is built for MI355X "
-                                  f"(ViLT / FLAVA are other model families, SURVEY §2)")
-    assert args.dataset == "food101", "MMBT is only supported for food101"
-    train, valid, test, n_classes, vocab = food101_data(args, rank, world)
-    args.n_classes, args.vocab = n_classes, vocab
-    args.total_steps = len(train) / args.gradient_accumulation_steps * args.n_epochs
-    args, model, optimizer, scheduler = setup_mmbt(args)
+    if args.framework == "vilt":
+        raise NotImplementedError("--framework vilt: ViLT needs remote weights and is another model family "
+                                  "(SURVEY §2); the MMBT and FLAVA paths are built for MI355X")
+    if args.framework == "flava":
+        train, valid, test = flava_data(args, rank, world)
+        args, model, optimizer, scheduler = setup_flava(args, len(train))
+    else:
+        assert args.dataset == "food101", "MMBT is only supported for food101"
+        train, valid, test, n_classes, vocab = food101_data(args, rank, world)
+        args.n_classes, args.vocab = n_classes, vocab
+        args.total_steps = len(train) / args.gradient_accumulation_steps * args.n_epochs
+        args, model, optimizer, scheduler = setup_mmbt(args)
+    mmbt = args.framework == "mmbt"
     os.makedirs(args.save_path, exist_ok=True)
     history_csv_path = os.path.join(args.save_path, "history.csv")
     if args.resume:
@@ -207,13 +264,16 @@ def main(argv=None):
     if (args.use_gpu or world > 1) and torch.cuda.is_available():
         m.to(torch.device("cuda:{}".format(args.device)))
     elif not torch.cuda.is_available():
-        raise RuntimeError("the MMBT path runs on MI355X HIP kernels: no GPU visible")
+        raise RuntimeError("the MMBT / FLAVA paths run on MI355X HIP kernels: no GPU visible")
     if world > 1:
-        _dp_wrap(model, optimizer, args.gradient_accumulation_steps)
+        if mmbt:
+            _dp_wrap(model, optimizer, args.gradient_accumulation_steps)
+        else:
+            _dp_wrap_flat(model, optimizer)
     m.train_loop(train, valid_generator=valid, test_generator=test, steps_per_epoch=len(train),
                  validation_steps=len(valid), test_steps=len(test), epochs=args.n_epochs, callbacks=callbacks,
                  patience=args.patience, epoch_start=epoch_start, scheduler_step_on=args.scheduler_step_on,
-                 auc=args.auc, vilt=False, mmbt=True, freeze_img=args.freeze_img, freeze_txt=args.freeze_txt,
+                 auc=args.auc, vilt=False, mmbt=mmbt, freeze_img=args.freeze_img, freeze_txt=args.freeze_txt,
                  gradient_accumulation_steps=args.gradient_accumulation_steps,
                  scheduler_metric=args.scheduler_metric)
     if world > 1:

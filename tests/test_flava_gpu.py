@@ -164,3 +164,18 @@ def test_flava_mc_dropout_and_eval_determinism(dev):
     with torch.no_grad():
         c, d = m((img, txt)), m((img, txt))
     assert not torch.equal(c, d), "train-mode passes must draw fresh dropout masks"
+
+
+def test_train_entry_point_flava_synthetic(dev, tmp_path):
+    """train.py --framework flava (reference train.py:184-216 + Model_.train_loop) end to end."""
+    import os
+    import sys
+    import pandas as pd
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "multi-modal-uncertainty_amd"))
+    import train
+    train.main(["--framework", "flava", "--synthetic", "64", "--batch_size", "16", "--n_epochs", "2",
+                "--save_path", str(tmp_path), "--use_gpu", "--model_type", "MultiHead", "--lr", "1e-4",
+                "--dataset", "hateful-meme-dataset"])
+    h = pd.read_csv(tmp_path / "history.csv")
+    assert len(h) == 2 and {"loss", "acc", "val_loss", "val_acc", "val_auc", "test_auc"} <= set(h.columns)
+    assert np.isfinite(h["loss"]).all()

@@ -14,7 +14,7 @@ from collections import defaultdict
 
 CATS = [
     ("mmu GEMM (BERT layers)", r"mmu::gemm_|gemm_(small|big)_kernel|mmu::splitk"),
-    ("mmu attention", r"mmu::attn_"),
+    ("mmu attention", r"mmu::attn_|mmu::seqattn_"),
     ("mmu LayerNorm", r"mmu::ln_|ln_fwd_kernel|ln_bwd_kernel"),
     ("mmu embed / pool", r"mmu::embed|mmu::row_pool|embed_fwd_kernel|embed_bwd"),
     ("mmu BertAdam", r"mmu::adam"),
@@ -39,6 +39,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--md", default=None)
+    ap.add_argument("--marker", default="adam_update_kernel",
+                    help="a kernel launched once per step (FLAVA / torch AdamW: nll_loss_forward)")
     a = ap.parse_args()
     if a.trace.endswith(".db"):  # rocprofv3's default rocpd (sqlite) output
         import sqlite3
@@ -47,7 +49,7 @@ def main():
     else:
         rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    adam = [i for i, r in enumerate(rows) if "adam_update_kernel" in r["Kernel_Name"]]
+    adam = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
     if len(adam) < 2:
         raise SystemExit("need >= 2 optimizer steps in the trace")
     lo, hi = adam[-2] + 1, adam[-1] + 1
@@ -65,7 +67,7 @@ def main():
         per_cat[c][0] += 1
         per_cat[c][1] += d
     busy = sum(v[1] for v in per_cat.values())
-    lines = [f"# One steady-state training step (between the last two BertAdam updates)", "",
+    lines = [f"# One steady-state training step (between the last two `{a.marker}` launches)", "",
              f"step wall (first dispatch start -> last end): {wall:.2f} ms; summed kernel time {busy:.2f} ms; "
              f"dispatches {len(win)}", "", "| category | launches | ms | % of kernel time |", "|---|---|---|---|"]
     for c, (n, ms) in sorted(per_cat.items(), key=lambda kv: -kv[1][1]):
