@@ -110,6 +110,18 @@ struct TileLoader {
   }
 };
 
+// Buffer descriptor from provably wave-uniform inputs: with the base / size words in
+// VGPRs hipcc wraps EVERY buffer op in a readfirstlane "waterfall" loop (~10 instructions
+// and a branch per DMA; 68 such loops in the dK/dV kernel).  Inputs derived from the
+// kernel arguments and blockIdx are uniform; readfirstlane makes that visible.
+static __device__ __forceinline__ __amdgpu_buffer_rsrc_t urs(const void* base, int bytes) {
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane(bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+}
+
 // ---- LDS-DMA helpers (buffer_load ... lds: lane-linear LDS destination, per-lane source)
 static __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t off) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (MMU_LDS(void)*)lds, 16, off, 0, 0, 0);
@@ -289,10 +301,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
   const int nkv = (L + 63) / 64;
   uint64_t* kbuf = kbuf_all + w * 32 * nkv;  // [32 rows][nkv] keep words of this wave
 
-  const __amdgpu_buffer_rsrc_t rkv = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.qkv + (int64_t)b * L * p.ld_qkv), 0, (int)(L * p.ld_qkv * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)(p.keymask + (int64_t)b * L), 0,
-                                                                      (int)(L * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rkv = urs((void*)(p.qkv + (int64_t)b * L * p.ld_qkv), (int)(L * p.ld_qkv * 2));
+  const __amdgpu_buffer_rsrc_t rm = urs((void*)(p.keymask + (int64_t)b * L), (int)(L * 4));
   bf16x8 qf[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
@@ -743,10 +753,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   // dropout counter base of row q: seed_bh + 4 (q nkv) + 2h  (+ 4j + s2 per tile half)
   const uint32_t ctr = seed_for(p.seed, bh) + 4u * (uint32_t)q * (uint32_t)nkv + 2u * (uint32_t)h;
 
-  const __amdgpu_buffer_rsrc_t rkv = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.qkv + (int64_t)b * L * p.ld_qkv), 0, (int)(L * p.ld_qkv * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)(p.keymask + (int64_t)b * L), 0,
-                                                                      (int)(L * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rkv = urs((void*)(p.qkv + (int64_t)b * L * p.ld_qkv), (int)(L * p.ld_qkv * 2));
+  const __amdgpu_buffer_rsrc_t rm = urs((void*)(p.keymask + (int64_t)b * L), (int)(L * 4));
   bf16x8 qf[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
@@ -970,6 +978,9 @@ constexpr int DK_ROWS = 32 * 4 + 32 * 4 + 32 * 8;          // -lse (as lse), del
 constexpr int DK_STAGE = 2 * DK_TILE + DK_ROWS;            // 8704 B
 
 
+// DROP is a template parameter: a runtime `drop ? keepword : ~0` select around the LDS read
+// made hipcc branch around every one of the 16 per-tile keep-word loads.
+template <bool DROP>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void attn_dkdv_dma_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) char smem[DK_NS * DK_STAGE];
   const int t = threadIdx.x, l = t & 63, h = l >> 5;
@@ -978,23 +989,20 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
   const int L = p.L, HD = p.heads * 64;
   const int k0w = blockIdx.x * 64 + 32 * w, key = k0w + (l & 31);
   const bool wave_live = k0w < L, kv = key < L;
-  const bool drop = drop_thr(p.drop_p) != 0;
+  const bool drop = DROP;
   const float zs = drop ? 1.0f / (1.0f - p.drop_p) : 1.0f;
+  const uint32_t lanebit = 1u << (l & 31);
   const int nkv = (L + 63) / 64;
   const float mkey = kv ? p.keymask[(int64_t)b * L + key] * LOG2E : NEG_INF;
   const bf16* base = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64;
 
   // operand buffers of this (batch item, head): rows beyond L are out of range -> zero
-  const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.qkv + (int64_t)b * L * p.ld_qkv), 0, (int)(L * p.ld_qkv * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rdo = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.dout + (int64_t)b * L * p.ld_do), 0, (int)(L * p.ld_do * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)(p.lse + (int64_t)bh * L), 0,
-                                                                      (int)(L * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)(p.delta + (int64_t)bh * L), 0,
-                                                                      (int)(L * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(drop ? p.dropmask + (int64_t)bh * L * nkv : p.dropmask), 0, drop ? (int)(L * nkv * 8) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rq = urs((void*)(p.qkv + (int64_t)b * L * p.ld_qkv), (int)(L * p.ld_qkv * 2));
+  const __amdgpu_buffer_rsrc_t rdo = urs((void*)(p.dout + (int64_t)b * L * p.ld_do), (int)(L * p.ld_do * 2));
+  const __amdgpu_buffer_rsrc_t rl = urs((void*)(p.lse + (int64_t)bh * L), (int)(L * 4));
+  const __amdgpu_buffer_rsrc_t rd = urs((void*)(p.delta + (int64_t)bh * L), (int)(L * 4));
+  const __amdgpu_buffer_rsrc_t rk =
+      urs((void*)(drop ? p.dropmask + (int64_t)bh * L * nkv : p.dropmask), drop ? (int)(L * nkv * 8) : 0);
 
   bf16x8 kf[4], vf[4];
 #pragma unroll
@@ -1058,11 +1066,23 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
     const char* Ds = st + DK_TILE;
     const float* lse = (const float*)(st + 2 * DK_TILE);
     const float* dlt = lse + 32;
-    const uint32_t* kbit = (const uint32_t*)(st + 2 * DK_TILE + 256);  // [32 rows][2 halves]
+    const uint32_t* kbit = (const uint32_t*)(st + 2 * DK_TILE + 256) + w;  // [32 rows][2 halves], this wave's half
     if (wave_live) {
+      // row constants of the 16 query rows a lane's registers hold: r -> row (r&3) + 8(r>>2) + 4h,
+      // i.e. four runs of 4 consecutive rows -> 16-B LDS reads (keep words: stride-2 pairs)
+      f32x4 nl4[4], dl4[4];
+      uint32_t kwr[16];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        nl4[j] = -*(const f32x4*)(lse + 8 * j + 4 * h);
+        dl4[j] = *(const f32x4*)(dlt + 8 * j + 4 * h);
+        if (DROP)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) kwr[4 * j + i] = kbit[2 * (8 * j + 4 * h + i)];
+      }
       f32x16 sc, dp;  // S starts at -lse of its query row (row constant as initial accumulator)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { sc[r] = -lse[(r & 3) + 8 * (r >> 2) + 4 * h]; dp[r] = 0.f; }
+      for (int r = 0; r < 16; ++r) { sc[r] = nl4[r >> 2][r & 3]; dp[r] = 0.f; }
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Qs, 0, ks, l), kf[ks], sc, 0, 0, 0);
@@ -1071,12 +1091,16 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
       f32x16 pz;  // dropped P (for dV)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int ql = (r & 3) + 8 * (r >> 2) + 4 * h;
         const float pr = __builtin_amdgcn_exp2f(fmaf(sc[r], LOG2E, mkey));
-        const uint32_t kw = drop ? kbit[2 * ql + w] : ~0u;
-        const float z = ((kw >> (l & 31)) & 1u) ? zs : 0.f;
-        pz[r] = pr * z;
-        sc[r] = pr * (dp[r] * z - dlt[ql]);  // dS
+        const float dl = dl4[r >> 2][r & 3];
+        if (DROP) {
+          const float z = (kwr[r] & lanebit) ? zs : 0.f;
+          pz[r] = pr * z;
+          sc[r] = pr * fmaf(dp[r], z, -dl);  // dS
+        } else {
+          pz[r] = pr;
+          sc[r] = pr * (dp[r] - dl);
+        }
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
@@ -1154,12 +1178,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   const int nkv = (L + 63) / 64;
   const bf16* base = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64;
 
-  const __amdgpu_buffer_rsrc_t rkv = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.qkv + (int64_t)b * L * p.ld_qkv), 0, (int)(L * p.ld_qkv * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)(p.keymask + (int64_t)b * L), 0,
-                                                                      (int)(L * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(drop ? p.dropmask + (int64_t)bh * L * nkv : p.dropmask), 0, drop ? (int)(L * nkv * 8) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rkv = urs((void*)(p.qkv + (int64_t)b * L * p.ld_qkv), (int)(L * p.ld_qkv * 2));
+  const __amdgpu_buffer_rsrc_t rm = urs((void*)(p.keymask + (int64_t)b * L), (int)(L * 4));
+  const __amdgpu_buffer_rsrc_t rk =
+      urs((void*)(drop ? p.dropmask + (int64_t)bh * L * nkv : p.dropmask), drop ? (int)(L * nkv * 8) : 0);
 
   bf16x8 qf[4], df[4];
   const bf16* dob = p.dout + ((int64_t)b * L + q) * p.ld_do + hd * 64;
@@ -1291,8 +1313,10 @@ void attention_bwd_launch(const AttnParams& p, hipStream_t s) {
     hipLaunchKernelGGL(attn_dq_dma_kernel, dim3((p.L + 127) / 128, p.batch * p.heads), dim3(256), 0, s, p);
   else
     hipLaunchKernelGGL(attn_dq_kernel, dim3((p.L + 127) / 128, p.batch * p.heads), dim3(256), 0, s, p);
-  if (attn_dma())
-    hipLaunchKernelGGL(attn_dkdv_dma_kernel, dim3((p.L + 63) / 64, p.batch * p.heads), dim3(128), 0, s, p);
+  if (attn_dma() && drop_thr(p.drop_p))
+    hipLaunchKernelGGL(attn_dkdv_dma_kernel<true>, dim3((p.L + 63) / 64, p.batch * p.heads), dim3(128), 0, s, p);
+  else if (attn_dma())
+    hipLaunchKernelGGL(attn_dkdv_dma_kernel<false>, dim3((p.L + 63) / 64, p.batch * p.heads), dim3(128), 0, s, p);
   else
     hipLaunchKernelGGL(attn_dkdv_kernel, dim3((p.L + 63) / 64, p.batch * p.heads), dim3(128), 0, s, p);
 }

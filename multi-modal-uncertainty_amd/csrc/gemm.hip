@@ -868,15 +868,30 @@ void colsum_reduce_launch(const float* part, int64_t parts, int64_t N, float* ou
 }
 
 // bf16 [M,N] column sums: each block sums 256 rows x 512 columns, one atomic per column
+// column sums of a bf16 [M, N] matrix: block = 64 octets of columns x COLSUM_BF16_ROWS rows
+// (4 waves, 4 loads in flight each), one float atomic per column per block (~M/1024 atomics
+// per address: 256-row blocks put ~140 same-address atomics in the L2 queue at M = 35 K)
+constexpr int COLSUM_BF16_ROWS = 1024;
 __global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16* __restrict__ X, int64_t M, int64_t N,
                                                           int64_t ld, float* __restrict__ out) {
-  const int64_t r0 = (int64_t)blockIdx.y * 256;
+  const int64_t r0 = (int64_t)blockIdx.y * COLSUM_BF16_ROWS;
+  const int64_t r1 = r0 + COLSUM_BF16_ROWS < M ? r0 + COLSUM_BF16_ROWS : M;
   const int64_t c = ((int64_t)blockIdx.x * 64 + (threadIdx.x & 63)) * 8;
   const int wv = threadIdx.x >> 6;
   __shared__ float red[4][64 * 8];
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (c < N) {
-    for (int64_t r = r0 + wv; r < r0 + 256 && r < M; r += 4) {
+    int64_t r = r0 + wv;
+    for (; r + 12 < r1; r += 16) {
+      bf16x8 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *(const bf16x8*)(X + (r + 4 * u) * ld + c);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[e] += bf2f(v[u][e]);
+    }
+    for (; r < r1; r += 4) {
       const bf16x8 v = *(const bf16x8*)(X + r * ld + c);
 #pragma unroll
       for (int e = 0; e < 8; ++e) s[e] += bf2f(v[e]);
@@ -898,7 +913,8 @@ void colsum_bf16_launch(const bf16* X, int64_t M, int64_t N, int64_t ld, float* 
                         hipStream_t s) {
   (void)part;
   if (!acc) (void)hipMemsetAsync(out, 0, sizeof(float) * N, s);
-  hipLaunchKernelGGL(colsum_bf16_kernel, dim3((unsigned)((N / 8 + 63) / 64), (unsigned)((M + 255) / 256)),
+  hipLaunchKernelGGL(colsum_bf16_kernel, dim3((unsigned)((N / 8 + 63) / 64),
+                                              (unsigned)((M + COLSUM_BF16_ROWS - 1) / COLSUM_BF16_ROWS)),
                      dim3(256), 0, s, X, M, N, ld, out);
 }
 

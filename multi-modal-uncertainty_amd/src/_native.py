@@ -7,7 +7,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmmu_hip.so")
+# MMU_LIB_PATH: load another build of the same ABI (A/B timing of two kernel versions,
+# tools/ab_build.sh); the default is the in-tree build
+LIB_PATH = os.environ.get("MMU_LIB_PATH") or os.path.join(_HERE, "libmmu_hip.so")
 
 c_i64, c_i32, c_f32, c_u64, c_vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p
 c_f32p, c_i64p, c_dp = ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)

@@ -179,3 +179,13 @@ def test_train_entry_point_flava_synthetic(dev, tmp_path):
     h = pd.read_csv(tmp_path / "history.csv")
     assert len(h) == 2 and {"loss", "acc", "val_loss", "val_acc", "val_auc", "test_auc"} <= set(h.columns)
     assert np.isfinite(h["loss"]).all()
+
+
+@pytest.mark.parametrize("M,N", [(37, 768), (5000, 2304), (35072, 768)])
+def test_colsum_bf16(dev, M, N):
+    k = K()
+    X = rnd(M, N, dev=dev, seed=8)
+    out = torch.full((N,), 3.0, device=dev)
+    k.colsum_bf16(X, out, accumulate=True)
+    ref = X.float().sum(0) + 3.0
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-3 * M ** 0.5)
