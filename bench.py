@@ -14,6 +14,8 @@ samples over the N ranks ("scaling": "strong"; DESIGN.md §6 has both measured).
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
   python bench.py --workload flava     BASELINE config 5: the FLAVA fusion transformer
                                        (src/model.py) train step on synthetic embeddings
+  python bench.py --workload uncertainty   BASELINE config 3: 5-member deep ensemble x
+                                       MC-dropout T=30 evaluation (NLL / ECE) of MMBT
 
 Rank 0 prints one JSON line (see README/DESIGN for the field definitions).
 """
@@ -47,7 +49,10 @@ def parse():
                     help="split this many samples over the ranks instead (strong scaling)")
     ap.add_argument("--text-len", type=int, default=508, help="word-pieces per sample (L = 5 + this)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", default="mmbt", choices=["mmbt", "flava"])
+    ap.add_argument("--workload", default="mmbt", choices=["mmbt", "flava", "uncertainty"])
+    ap.add_argument("--members", type=int, default=5, help="uncertainty: deep-ensemble members K")
+    ap.add_argument("--mc-samples", type=int, default=30, help="uncertainty: MC-dropout passes T")
+    ap.add_argument("--eval-batch", type=int, default=32, help="uncertainty: samples per rank per step")
     ap.add_argument("--flava-batch", type=int, default=128, help="FLAVA per-rank batch (train.py --batch_size)")
     ap.add_argument("--flava-tokens", type=str, default="197,77", help="FLAVA image,text embedding lengths")
     ap.add_argument("--cpu-batch", type=int, default=2)
@@ -221,6 +226,123 @@ def bench_flava(args, world, rank, dev):
     return out
 
 
+def uncertainty_cpu_baseline(args, L_text, B=2, passes=2):
+    """The oracle's fp32 MC-dropout forward (oracle/mmbt_ref.py) on host cores: one member,
+    ResNet features computed once (as the HIP path does), ``passes`` dropout passes."""
+    from oracle import mmbt_ref as R
+    from oracle.weights import FULL, make_state_dict
+    torch.set_num_threads(args.cpu_threads)
+    sd = make_state_dict(0, FULL)
+    g = torch.Generator().manual_seed(0)
+    txt = torch.randint(1000, 30522, (B, L_text), generator=g)
+    mask = torch.ones(B, L_text, dtype=torch.long)
+    img = torch.randn(B, 3, 224, 224, generator=g)
+    gen = torch.Generator().manual_seed(1)
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        feats = R.image_encoder(sd, img, FULL)
+        t1 = time.perf_counter()
+        for _ in range(passes):
+            R.forward(sd, txt, mask, mask, img, FULL, dropout=0.1, gen=gen, feats=feats)
+        t2 = time.perf_counter()
+    # one evaluated sample = K ResNet trunks + K x T MC-dropout encoder passes
+    per_sample = (args.members * (t1 - t0) + args.members * args.mc_samples * (t2 - t1) / passes) / B
+    return {"value": round(1.0 / per_sample, 5), "unit": "samples/s", "cores": args.cpu_threads, "kind": "port",
+            "sample": f"oracle fp32 eval: 1 member, ResNet once + {passes} MC-dropout encoder passes, B={B}, "
+                      f"L={L_text + 5}, timed and scaled to K={args.members} trunks + K x T={args.mc_samples} "
+                      f"encoder passes per sample, torch CPU {torch.get_num_threads()} threads"}
+
+
+def bench_uncertainty(args, world, rank, dev):
+    """BASELINE config 3: a K-member deep ensemble x T-pass MC-dropout evaluation of MMBT
+    (src/uncertainty.py; K = 5, T = 30 by default) on a synthetic batch per rank: the K
+    ResNet-152 trunks once per batch, the K*T*B encoder passes as ONE batched launch per op,
+    then NLL / ECE over the batch (mmu_uncertainty, mmu_ece_bins).  Samples are sharded over
+    ranks (weak scaling; the only exchange is the metric sums, outside the timed loop)."""
+    from src.mmbt import MultimodalBertClf
+    from src.testing import make_args, synthetic_batch
+    from src.uncertainty import EnsembleMMBT, UncertaintyMeter
+    torch.backends.cudnn.benchmark = os.environ.get("MMU_MIOPEN_FIND", "1") == "1"
+    Km, T_mc, B, T = args.members, args.mc_samples, args.eval_batch, args.text_len
+    L = T + 5
+    members = []
+    for k in range(Km):
+        torch.manual_seed(1000 + k)
+        members.append(MultimodalBertClf(make_args()).to(dev).eval())
+    ens = EnsembleMMBT(members)
+    x, y = synthetic_batch(B, T, seed=200 + rank, device=dev)
+    events = []
+    layer = ens._layer
+
+    def timed_layer(*a, **kw):
+        if not timing:
+            return layer(*a, **kw)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = layer(*a, **kw)
+        e1.record()
+        events.append((e0, e1))
+        return out
+    ens._layer = timed_layer
+    timing = False
+    meter = UncertaintyMeter(15)
+
+    def step():
+        with torch.no_grad():
+            lo = ens.logits(*x, mc_samples=T_mc)                         # [K, T, B, C]
+            flat = lo.permute(2, 0, 1, 3).reshape(B, Km * T_mc, lo.shape[-1])
+            meter.update(flat, y)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    timing = True
+    meter = UncertaintyMeter(15)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    timing = False
+    layer_ms = sum(a.elapsed_time(b) for a, b in events)
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    res = meter.result()
+    H = 768
+    layer_fwd = L * (24 * H * H + 4 * L * H)             # per sequence per layer, forward
+    seqs = Km * T_mc * B
+    block_tf = layer_fwd * seqs * len(events) / (layer_ms * 1e-3) / 1e12 if layer_ms else 0.0
+    flop_step = seqs * 12 * layer_fwd + Km * B * RESNET152_FWD_FLOP
+    ms_step = 1000.0 * dt / args.steps
+    out = {
+        "metric": "MMBT deep-ensemble x MC-dropout eval samples/sec (BASELINE config 3; NLL / ECE)",
+        "value": round(B * world * args.steps / dt, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded; random-init members)",
+        "config": {"workload": "mmbt_ensemble_mc_dropout_eval", "model": "MMBT bert-base-uncased + resnet152",
+                   "members": Km, "mc_samples": T_mc, "per_rank_batch": B, "global_batch": B * world,
+                   "seq_len": 512, "tokens": L, "encoder_passes_per_step": seqs, "parallelism": f"dp{world}"},
+        # the batched encoder layer (all K*T*B sequences of one layer: QKV / attention / Wo /
+        # LN / FFN / LN forward), timed by HIP events around every layer launch group
+        "fused_block_roofline": {
+            "bound": "mfma", "flop_per_sequence_per_layer": layer_fwd, "achieved": round(block_tf, 1),
+            "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(block_tf / PEAK_BF16_TFLOPS, 4),
+            "ms_per_layer": round(layer_ms / max(len(events), 1), 3), "layer_launch_groups_timed": len(events),
+            "share_of_step": round(layer_ms / args.steps / ms_step, 3) if ms_step else None},
+        "model_tflops_achieved": round(flop_step * world / (ms_step * 1e-3) / 1e12, 1),
+        "nll": round(res["nll"], 5), "ece": round(res["ece"], 5), "acc": round(res["acc"], 5),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = uncertainty_cpu_baseline(args, T)
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -231,8 +353,8 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
-    if args.workload == "flava":
-        out = bench_flava(args, world, rank, dev)
+    if args.workload in ("flava", "uncertainty"):
+        out = (bench_flava if args.workload == "flava" else bench_uncertainty)(args, world, rank, dev)
         if rank == 0:
             print(json.dumps(out), flush=True)
         if world > 1:

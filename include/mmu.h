@@ -261,6 +261,9 @@ int mmu_ece_bins(const float* conf, const float* correct, int64_t S, int64_t n_b
  * the launch stream (bench.py roofline).  Reads back (host sync) only in _read.
  */
 int mmu_timing_enable(int on);
+/* paused != 0: launches are not recorded (already recorded ones are kept) -- the
+ * ResNet 1x1-conv products run through mmu_gemm but are not BERT-layer GEMMs. */
+int mmu_timing_pause(int paused);
 int mmu_timing_read(double* total_ms, int64_t* launches, double* flops);
 
 #ifdef __cplusplus

@@ -48,6 +48,7 @@ namespace {
 struct Timing {
   std::mutex mu;
   bool on = false;
+  bool paused = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pool, used;
   std::vector<double> flops;
 } g_t;
@@ -77,6 +78,12 @@ int mmu_timing_enable(int on) {
   for (auto& e : g_t.used) g_t.pool.push_back(e);
   g_t.used.clear();
   g_t.flops.clear();
+  return 0;
+}
+
+int mmu_timing_pause(int paused) {
+  std::lock_guard<std::mutex> lk(g_t.mu);
+  g_t.paused = paused != 0;
   return 0;
 }
 
@@ -198,7 +205,7 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
   std::pair<hipEvent_t, hipEvent_t> ev;
   {
     std::lock_guard<std::mutex> lk(g_t.mu);
-    timed = g_t.on;
+    timed = g_t.on && !g_t.paused;
   }
   if (timed) {
     ev = take_events();

@@ -64,6 +64,7 @@ SIGNATURES = {
     "mmu_uncertainty": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mmu_ece_bins": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "mmu_timing_enable": (c_i32, [c_i32]),
+    "mmu_timing_pause": (c_i32, [c_i32]),
     "mmu_timing_read": (c_i32, [c_dp, c_i64p, c_dp]),
 }
 

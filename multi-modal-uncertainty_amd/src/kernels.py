@@ -308,6 +308,24 @@ def timing_enable(on=True):
     _alg.update(on=bool(on), bytes=0.0, n=0)
 
 
+class timing_paused:
+    """Context: mmu_gemm launches inside are neither event-timed nor counted (bench.py's
+    GEMM roofline covers the BERT-layer products only)."""
+
+    def __enter__(self):
+        self.was = _alg["on"]
+        if self.was:
+            N.call("mmu_timing_pause", 1)
+            _alg["on"] = False
+        return self
+
+    def __exit__(self, *exc):
+        if self.was:
+            N.call("mmu_timing_pause", 0)
+            _alg["on"] = True
+        return False
+
+
 def timing_read():
     ms, n, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
     N.call("mmu_timing_read", ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl))

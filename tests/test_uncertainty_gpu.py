@@ -1,0 +1,126 @@
+"""End-to-end parity of the K-member ensemble x T-pass MC-dropout path (src/uncertainty.py,
+SURVEY §8a A12, BASELINE config 3) on MI355X.
+
+* T = 1, no dropout: member k's logits from the ONE batched-over-members encoder equal the
+  CPU oracle's fp32 forward with member k's weights (oracle/mmbt_ref.py:158, restating
+  src/mmbt.py:245-250) within the bf16 tolerance of test_mmbt_gpu, and equal member k's
+  own single-model HIP forward.
+* NLL through UncertaintyMeter (mmu_uncertainty + mmu_ece_bins) equals the oracle metric
+  (oracle/uncertainty_ref.py) on the oracle's logits within 2e-2 relative; ECE is compared
+  on the HIP logits (it is a step function of the confidences; "parity unpinned" vs the
+  reference, which has no ECE).
+* MC-dropout: with dropout 0 the T passes are identical to the T = 1 logits; with dropout
+  0.1 the passes differ, are reproducible from the torch seed, and every pass stays a
+  finite perturbation of the deterministic logits.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def tol_check(got, ref, rel=2e-2, abs_=2e-3, what=""):
+    got, ref = np.asarray(got, dtype=np.float64), np.asarray(ref, dtype=np.float64)
+    err = np.abs(got - ref).max()
+    scale = np.abs(ref).max()
+    assert err <= rel * scale + abs_, f"{what}: max err {err:.3e} vs scale {scale:.3e}"
+    return err
+
+
+def members(dev, K, **over):
+    from oracle.weights import SMALL, make_state_dict
+    from src.mmbt import MultimodalBertClf
+    from src.testing import small_args
+    over.setdefault("img_precision", "fp32")
+    out, sds = [], []
+    for k in range(K):
+        torch.manual_seed(k)
+        m = MultimodalBertClf(small_args(**over))
+        sd = make_state_dict(k, SMALL)
+        m.load_state_dict(sd, strict=True)
+        out.append(m.to(dev).eval())
+        sds.append(sd)
+    return out, sds
+
+
+@pytest.fixture(scope="module")
+def batch():
+    from src.testing import synthetic_batch
+    from oracle.weights import SMALL
+    return synthetic_batch(4, 24, lens=[24, 17, 9, 24], vocab=SMALL.vocab, seed=21)
+
+
+def test_ensemble_members_match_oracle_and_single_forward(dev, batch):
+    from oracle import mmbt_ref as R
+    from oracle.weights import SMALL
+    from src.uncertainty import EnsembleMMBT
+    K = 3
+    ms, sds = members(dev, K)
+    (txt, seg, mask, img), y = batch
+    xd = tuple(t.to(dev) for t in (txt, seg, mask, img))
+    ens = EnsembleMMBT(ms)
+    with torch.no_grad():
+        lo = ens.logits(*xd, mc_samples=1)
+    assert lo.shape == (K, 1, 4, 101)
+    for k in range(K):
+        ref = R.forward(sds[k], txt, mask, seg, img, SMALL)
+        tol_check(lo[k, 0].cpu(), ref, what=f"member {k} vs oracle")
+        with torch.no_grad():
+            single = ms[k](*xd).cpu()
+        tol_check(lo[k, 0].cpu(), single, rel=1e-2, abs_=1e-3, what=f"member {k} vs its own forward")
+
+
+def test_ensemble_nll_ece_vs_oracle_metrics(dev, batch):
+    from oracle import mmbt_ref as R
+    from oracle import uncertainty_ref as U
+    from oracle.weights import SMALL
+    from src.uncertainty import EnsembleMMBT, UncertaintyMeter
+    K = 2
+    ms, sds = members(dev, K)
+    (txt, seg, mask, img), y = batch
+    xd = tuple(t.to(dev) for t in (txt, seg, mask, img))
+    with torch.no_grad():
+        lo = EnsembleMMBT(ms).logits(*xd, mc_samples=1)                      # [K, 1, B, C]
+    flat = lo.permute(2, 0, 1, 3).reshape(4, K, -1)                           # [B, K*T, C]
+    meter = UncertaintyMeter(15)
+    p_bar = meter.update(flat, y.to(dev)).cpu().numpy()
+    res = meter.result()
+    ref_logits = np.stack([R.forward(sds[k], txt, mask, seg, img, SMALL).numpy() for k in range(K)])
+    p_ref = U.probs_mean(ref_logits, member_axes=(0,))
+    assert np.abs(p_bar - p_ref).max() < 2e-2
+    assert abs(res["nll"] - U.nll(p_ref, y.numpy())) <= 2e-2 * U.nll(p_ref, y.numpy())
+    p_hip = U.probs_mean(flat.cpu().double().numpy().transpose(1, 0, 2), member_axes=(0,))
+    assert abs(res["ece"] - U.ece(p_hip, y.numpy())) < 1e-5
+    assert abs(res["acc"] - U.accuracy(p_hip, y.numpy())) < 1e-12
+    assert res["n"] == 4
+
+
+def test_mc_dropout_passes(dev, batch):
+    from src.uncertainty import EnsembleMMBT
+    (txt, seg, mask, img), y = batch
+    xd = tuple(t.to(dev) for t in (txt, seg, mask, img))
+    # dropout 0 everywhere: the T passes replicate the deterministic logits
+    ms0, _ = members(dev, 2, bert_hidden_dropout=0.0, bert_attn_dropout=0.0)
+    ens0 = EnsembleMMBT(ms0)
+    with torch.no_grad():
+        det = ens0.logits(*xd, mc_samples=1)
+        rep = ens0.logits(*xd, mc_samples=3, mc_dropout=True)
+    assert rep.shape == (2, 3, 4, 101)
+    for t in range(3):
+        tol_check(rep[:, t].cpu(), det[:, 0].cpu(), rel=1e-3, abs_=1e-4, what=f"p=0 pass {t}")
+    # BERT dropout 0.1 (the reference's BertConfig default): passes differ, seed-reproducible
+    ms1, _ = members(dev, 2)
+    ens1 = EnsembleMMBT(ms1)
+    with torch.no_grad():
+        det1 = ens1.logits(*xd, mc_samples=1)
+        torch.manual_seed(7)
+        a = ens1.logits(*xd, mc_samples=4)
+        torch.manual_seed(7)
+        b = ens1.logits(*xd, mc_samples=4)
+    assert torch.isfinite(a).all()
+    assert torch.equal(a, b)
+    d = (a[:, 1:] - a[:, :1]).abs().amax().item()
+    assert d > 1e-3, "MC-dropout passes are identical"
+    spread = (a - det1).abs().amax().item()
+    assert spread < 0.5 * det1.abs().amax().item() + 1.0

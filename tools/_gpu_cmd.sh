@@ -1,6 +1,5 @@
 set -o pipefail
-for i in 1 2; do
-for lib in ab/head.so multi-modal-uncertainty_amd/src/libmmu_hip.so; do
-echo "== $lib" >> gpurun_out/attn_ab.txt
-MMU_LIB_PATH=$lib timeout -k 10 200 python -u tools/attn_bench.py --iters 10 >> gpurun_out/attn_ab.txt 2>&1 || exit 1
-done; done
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_gpu.log 2>&1 || { tail -30 gpurun_out/t_gpu.log; exit 1; }
+tail -2 gpurun_out/t_gpu.log
+timeout -k 10 400 python -u bench.py --workload uncertainty --steps 3 --warmup 1 > gpurun_out/bench_unc.log 2>&1 || { tail -30 gpurun_out/bench_unc.log; exit 1; }
+tail -1 gpurun_out/bench_unc.log
