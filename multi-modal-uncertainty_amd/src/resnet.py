@@ -4,8 +4,12 @@ Child order and parameter names follow torchvision's resnet152 so that
 ``ImageEncoder.model = Sequential(children[:-2])`` yields the reference keys
 ``enc.img_encoder.model.{0..7}.*``.  No pretrained weights exist offline: weights
 use torchvision's default init (He-normal fan_out convs, BN gamma 1 / beta 0).
-On MI355X the trunk's convs run through MIOpen in bf16, channels-last (ImageEncoder), and
-every BatchNorm2d [+ residual] [+ ReLU] through mmu_batchnorm_fwd/bwd.
+On MI355X the trunk's convs run in bf16, channels-last (ImageEncoder): the 1x1 stride-1
+products through mmu_gemm where measured faster (_mmu_1x1), the rest through MIOpen; every
+BatchNorm2d [+ residual] [+ ReLU] through mmu_batchnorm_fwd/bwd.  In an identity-skip
+Bottleneck the block input feeds both conv1 and bn3's residual: bn3's backward hands its
+skip gradient to conv1's backward (_SkipGrad), whose dX GEMM adds it in the epilogue
+(EPI_ADD_RES) instead of autograd summing the two in a separate pass.
 """
 import torch
 import torch.nn as nn
@@ -18,8 +22,8 @@ class _BatchNormAct(torch.autograd.Function):
     mmu_batchnorm_fwd / mmu_batchnorm_bwd (batch statistics, running stats updated)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, skip, bn, relu):
-        ctx.bias_ref = bias
+    def forward(ctx, x, weight, bias, skip, bn, relu, sink=None):
+        ctx.bias_ref, ctx.sink = bias, sink
         Y = torch.empty_like(x)
         C = x.shape[1]
         smean = torch.empty(C, dtype=torch.float32, device=x.device)
@@ -46,7 +50,9 @@ class _BatchNormAct(torch.autograd.Function):
         K.batchnorm_bwd(dY, Y if ctx.relu else None, x, weight, smean, sinv, ctx.relu, dX, dS, dw, db)
         rw = dw if (want_w and weight.grad is None) else None
         rb = db if (want_b and ctx.bias_ref.grad is None) else None
-        return dX, rw, rb, dS, None, None
+        if ctx.sink is not None and dS is not None:  # conv1's dX GEMM adds it (EPI_ADD_RES)
+            ctx.sink.g, dS = dS, None
+        return dX, rw, rb, dS, None, None, None
 
 
 class BatchNorm2d(nn.BatchNorm2d):
@@ -60,7 +66,7 @@ class BatchNorm2d(nn.BatchNorm2d):
     fused_relu = False
     MIOPEN_MIN_BATCH = 8
 
-    def forward(self, x, skip=None, relu=None):
+    def forward(self, x, skip=None, relu=None, skip_sink=None):
         relu = self.fused_relu if relu is None else relu
         hip = (x.is_cuda and x.dtype == torch.bfloat16 and (skip is None or skip.dtype == torch.bfloat16)
                and x.shape[1] % 8 == 0)
@@ -69,7 +75,7 @@ class BatchNorm2d(nn.BatchNorm2d):
             if skip is not None:
                 skip = skip.contiguous(memory_format=torch.channels_last)
             if self.training and self.track_running_stats:
-                return _BatchNormAct.apply(x, self.weight, self.bias, skip, self, relu)
+                return _BatchNormAct.apply(x, self.weight, self.bias, skip, self, relu, skip_sink)
             if not self.training:
                 Y = torch.empty_like(x)
                 K.batchnorm_fwd(x, Y, self.weight, self.bias, self.running_mean, self.running_var, False,
@@ -117,6 +123,94 @@ class _ConvBF16(torch.autograd.Function):
         return dx, rw, None, None, None
 
 
+class _SkipGrad:
+    """The gradient of an identity-skip Bottleneck's residual input, handed from bn3's
+    backward to conv1's backward (which autograd always runs later: conv1 feeds bn3)."""
+    __slots__ = ("g",)
+
+    def __init__(self):
+        self.g = None
+
+
+def _rows(t):
+    """[N, C, H, W] channels-last -> its [N*H*W, C] row-major view."""
+    return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
+
+
+def _mmu_1x1(cin, cout, M, H):
+    """Which products of a 1x1 stride-1 conv (rows M = N*H*W) run on mmu_gemm instead of
+    MIOpen, from profiles/r1_conv1x1_b256.txt / _b32.txt (same-box timings, both engines):
+    dX always for the reducing convs (cin > cout) and for M >= 12544; the forward for
+    25088 <= M <= 50176 (and not the widening 14x14 product at batch 256); the weight
+    gradient for 12544 <= M <= 50176 at H <= 14.  mmu_gemm needs N % 128 == 0 for its
+    output columns (and M-major A rows % 128 for dW)."""
+    fwd = cout % 128 == 0 and cin % 64 == 0 and 25088 <= M <= 50176 and (cin > cout or M < 50176)
+    dx = cin % 128 == 0 and cout % 64 == 0 and (cin > cout or M >= 12544)
+    dw = cin % 128 == 0 and cout % 128 == 0 and 12544 <= M <= 50176 and H <= 14
+    return fwd, dx, dw
+
+
+class _Conv1x1(torch.autograd.Function):
+    """1x1 stride-1 convolution of a channels-last bf16 map, as products over its [N*H*W, C]
+    rows:  Y = X W^T,  dX = dY W (+ the skip gradient: EPI_ADD_RES),  dW += dY^T X (f32,
+    split-K, straight into the gradient store) -- each on mmu_gemm or MIOpen per _mmu_1x1.
+    The GEMMs are excluded from bench.py's BERT-layer GEMM timing (timing_paused)."""
+
+    @staticmethod
+    def forward(ctx, x, w, w16, sink):
+        Nb, C, H, W = x.shape
+        Co = w16.shape[0]
+        M = Nb * H * W
+        use_f, use_d, use_w = _mmu_1x1(C, Co, M, H)
+        if use_f:
+            y = torch.empty((Nb, Co, H, W), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+            with K.timing_paused():
+                K.gemm(_rows(x), C, 1, w16.view(Co, C), C, 1, _rows(y), Co, M, Co, C)
+        else:
+            y = torch.ops.aten.convolution(x, w16, None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1)
+        ctx.save_for_backward(x, w16)
+        ctx.w, ctx.sink, ctx.use = w, sink, (use_d, use_w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w16 = ctx.saved_tensors
+        use_d, use_w = ctx.use
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        Nb, C, H, W = x.shape
+        Co = w16.shape[0]
+        M = Nb * H * W
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        skip = None
+        if ctx.sink is not None:
+            skip, ctx.sink.g = ctx.sink.g, None
+        dx = rw = None
+        with K.timing_paused():
+            if need_x and use_d:
+                dx = torch.empty_like(x, memory_format=torch.channels_last)
+                epi = K.epilogue(K.EPI_ADD_RES, residual=_rows(skip)) if skip is not None else None
+                K.gemm(_rows(dy), Co, 1, w16.view(Co, C), C, 0, _rows(dx), C, M, C, Co, epi=epi)
+                skip = None
+            mx, mw = need_x and not use_d, need_w and not use_w
+            if mx or mw:
+                gx, gw, _ = torch.ops.aten.convolution_backward(dy, x, w16, None, (1, 1), (0, 0), (1, 1), False,
+                                                                (0, 0), 1, (mx, mw, False))
+                if mx:
+                    dx = gx if skip is None else gx + skip
+                if mw:
+                    if ctx.w.grad is not None:
+                        ctx.w.grad.add_(gw)
+                    else:
+                        rw = gw.float()
+            if need_w and use_w:
+                g = ctx.w.grad
+                if g is None:
+                    g = rw = torch.zeros_like(ctx.w, memory_format=torch.contiguous_format)
+                K.gemm(_rows(dy), Co, 0, _rows(x), C, 0, g.view(Co, C), C, Co, C, M,
+                       epi=K.epilogue(K.EPI_STORE, accumulate=True))
+        return dx, rw, None, None
+
+
 class StoreConv2d(nn.Conv2d):
     """nn.Conv2d (same parameters / state_dict) that, once the model's parameter store
     holds a bf16 copy of its filter, convolves bf16 channels-last inputs with that copy.
@@ -129,15 +223,36 @@ class StoreConv2d(nn.Conv2d):
         import weakref
         self._src = (weakref.ref(store), name)
 
-    def forward(self, x):
+    def _compute_weight(self, x):
         src = self._src
         if (src is not None and x.is_cuda and x.dtype == torch.bfloat16 and self.bias is None and self.groups == 1
                 and self.dilation == (1, 1)):
             store = src[0]()
             if store is not None:
-                w16 = store.compute_of(src[1])
-                return _ConvBF16.apply(x.contiguous(memory_format=torch.channels_last), self.weight, w16,
-                                       self.stride, self.padding)
+                return store.compute_of(src[1])
+        return None
+
+    def _is_1x1(self):
+        return self.kernel_size == (1, 1) and self.stride == (1, 1) and self.padding == (0, 0)
+
+    def takes_skip_grad(self, x):
+        """True when this conv's backward will add a _SkipGrad into its dX GEMM."""
+        if not (self._is_1x1() and torch.is_grad_enabled() and x.requires_grad):
+            return False
+        if self._compute_weight(x) is None:
+            return False
+        N_, C, H, W = x.shape
+        return _mmu_1x1(C, self.out_channels, N_ * H * W, H)[1]
+
+    def forward(self, x, sink=None):
+        w16 = self._compute_weight(x)
+        if w16 is not None:
+            x = x.contiguous(memory_format=torch.channels_last)
+            if self._is_1x1():
+                return _Conv1x1.apply(x, self.weight, w16, sink)
+            return _ConvBF16.apply(x, self.weight, w16, self.stride, self.padding)
+        if sink is not None:
+            raise RuntimeError("StoreConv2d: a skip-gradient sink needs the bf16 1x1 path")
         return super().forward(x)
 
 
@@ -165,10 +280,15 @@ class Bottleneck(nn.Module):
             self.downsample = nn.Sequential(StoreConv2d(cin, cout, 1, stride=stride, bias=False), BatchNorm2d(cout))
 
     def forward(self, x):
+        sink = None
+        if (self.downsample is None and self.training and self.bn3.track_running_stats and x.is_cuda
+                and x.dtype == torch.bfloat16 and self.conv1.takes_skip_grad(x)):
+            x = x.contiguous(memory_format=torch.channels_last)
+            sink = _SkipGrad()
         skip = x if self.downsample is None else self.downsample(x)
-        y = self.bn1(self.conv1(x), relu=True)
+        y = self.bn1(self.conv1(x, sink=sink), relu=True)
         y = self.bn2(self.conv2(y), relu=True)
-        return self.bn3(self.conv3(y), skip=skip, relu=True)
+        return self.bn3(self.conv3(y), skip=skip, relu=True, skip_sink=sink)
 
 
 def resnet152_trunk(blocks=(3, 8, 36, 3)):

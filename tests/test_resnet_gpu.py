@@ -1,0 +1,75 @@
+"""ResNet-152 Bottleneck on the bf16 training path (src/resnet.py): the 1x1 stride-1 convs on
+mmu_gemm (forward, dX with the identity-skip gradient added in the GEMM epilogue, dW into
+the f32 gradient) against the same block with every conv product on MIOpen and autograd
+summing the skip gradient.  Shapes are chosen so that every branch of _mmu_1x1 runs:
+  1024 -> 256 at 14x14, batch 128 (M = 25088): fwd, dX + skip, dW on conv1 and conv3
+  256 -> 64 at 56x56, batch 4 (M = 12544): conv1 dX + skip with K = 64; the rest MIOpen
+Tolerance: bf16 products (f32 accumulation) on both sides; relative Frobenius error <= 2e-2.
+(A max-error bound is the wrong yardstick here: the two engines round differently, which
+flips a few ReLU masks in bn1 / bn2 at pre-activations near 0, and one flipped element
+moves its whole upstream gradient.)
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+class _Store:
+    """stand-in for the parameter store: bf16 channels-last copies of the conv filters"""
+
+    def __init__(self, mod):
+        self.w = {n: p.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+                  for n, p in mod.named_parameters() if p.dim() == 4}
+
+    def compute_of(self, name):
+        return self.w[name]
+
+
+def _run(block, x, g):
+    from src import resnet as R
+    xx = x.clone().requires_grad_(True)
+    for p in block.parameters():
+        p.grad = None
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        used_sink = block.downsample is None and block.conv1.takes_skip_grad(xx)
+        y = block(xx)
+    y.float().backward(g)
+    assert isinstance(block.conv1, R.StoreConv2d)
+    return y.float(), xx.grad.float(), {n: p.grad.float().clone() for n, p in block.named_parameters()}, used_sink
+
+
+def _close(a, b, what, frac=2e-2):
+    err = (a - b).double().norm().item()
+    scale = b.double().norm().item() + 1e-12
+    assert err <= frac * scale, f"{what}: |err| {err:.3e} vs |ref| {scale:.3e}"
+
+
+@pytest.mark.parametrize("cin,width,hw,batch", [(1024, 256, 14, 128), (256, 64, 56, 4)])
+def test_bottleneck_mmu_1x1_matches_miopen(dev, monkeypatch, cin, width, hw, batch):
+    from src import resnet as R
+    torch.manual_seed(0)
+    block = R.Bottleneck(cin, width, 1)
+    for m in block.modules():
+        if isinstance(m, torch.nn.Conv2d):
+            torch.nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+    block = block.to(dev).train()
+    store = _Store(block)
+    for n, m in block.named_modules():
+        if isinstance(m, R.StoreConv2d):
+            m.attach_compute(store, f"{n}.weight")
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(batch, cin, hw, hw, generator=g).clamp_(min=0).to(dev).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(batch, cin, hw, hw, generator=g).to(dev).contiguous(memory_format=torch.channels_last)
+    M = batch * hw * hw
+    assert R._mmu_1x1(cin, width, M, hw)[1]
+    y1, dx1, gr1, sink1 = _run(block, x, gy)
+    assert sink1, "the identity-skip gradient must go through conv1's dX GEMM"
+    monkeypatch.setattr(R, "_mmu_1x1", lambda *a: (False, False, False))
+    y0, dx0, gr0, sink0 = _run(block, x, gy)
+    assert not sink0
+    _close(y1, y0, "output")
+    _close(dx1, dx0, "input grad")
+    for n in gr0:
+        _close(gr1[n], gr0[n], f"grad {n}")

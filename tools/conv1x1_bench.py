@@ -27,7 +27,8 @@ def main():
     torch.backends.cudnn.benchmark = True
     dev, cl = "cuda", torch.channels_last
     # (Cin, Cout, H): layer2..4 conv1 / conv3 (every stride-1 1x1 with both widths % 128 == 0)
-    shapes = [(512, 128, 28), (128, 512, 28), (1024, 256, 14), (256, 1024, 14), (2048, 512, 7), (512, 2048, 7)]
+    shapes = [(256, 64, 56), (64, 256, 56), (512, 128, 28), (128, 512, 28), (1024, 256, 14), (256, 1024, 14),
+              (2048, 512, 7), (512, 2048, 7)]
     print(f"batch {N}; us per call (best of 10); TF/s in brackets")
     for cin, cout, H in shapes:
         x = (torch.randn(N, cin, H, H, device=dev) * 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
@@ -45,21 +46,36 @@ def main():
         dX = torch.empty(M, cin, dtype=torch.bfloat16, device=dev)
         dW = torch.zeros(cout, cin, dtype=torch.float32, device=dev)
         acc = K.epilogue(K.EPI_STORE, accumulate=True)
-        t_gf = timed(lambda: K.gemm(X2, cin, 1, W2, cin, 1, Y, cout, M, cout, cin), 10)
-        t_gd = timed(lambda: K.gemm(dY2, cout, 1, W2, cin, 0, dX, cin, M, cin, cout), 10)
-        t_gw = timed(lambda: K.gemm(dY2, cout, 0, X2, cin, 0, dW, cin, cout, cin, M, epi=acc), 10)
+        skip = (torch.randn(M, cin, device=dev) * 0.5).to(torch.bfloat16)
+        ok_f, ok_d, ok_w = cout % 128 == 0, cin % 128 == 0, cout % 128 == 0 and cin % 128 == 0
+        nan = float("nan")
+        t_gf = timed(lambda: K.gemm(X2, cin, 1, W2, cin, 1, Y, cout, M, cout, cin), 10) if ok_f else nan
+        t_gd = timed(lambda: K.gemm(dY2, cout, 1, W2, cin, 0, dX, cin, M, cin, cout), 10) if ok_d else nan
+        t_gw = timed(lambda: K.gemm(dY2, cout, 0, X2, cin, 0, dW, cin, cout, cin, M, epi=acc), 10) if ok_w else nan
+        # the Bottleneck's identity-skip join: MIOpen dX + autograd's add vs one GEMM with ADD_RES
+        res = K.epilogue(K.EPI_ADD_RES, residual=skip)
+        t_ma = timed(lambda: cbw(dy, x, w, None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1,
+                                 (True, False, False))[0].permute(0, 2, 3, 1).reshape(M, cin) + skip, 10)
+        t_ga = timed(lambda: K.gemm(dY2, cout, 1, W2, cin, 0, dX, cin, M, cin, cout, epi=res), 10) if ok_d else nan
         # parity of the three products against MIOpen (bf16 outputs; dW in f32)
         ref_y = conv(x, w, None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1).permute(0, 2, 3, 1).reshape(M, cout)
         rdx, rdw, _ = cbw(dy, x, w, None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1, (True, True, False))
         dW.zero_()
-        K.gemm(dY2, cout, 0, X2, cin, 0, dW, cin, cout, cin, M, epi=acc)
-        K.gemm(X2, cin, 1, W2, cin, 1, Y, cout, M, cout, cin)
-        K.gemm(dY2, cout, 1, W2, cin, 0, dX, cin, M, cin, cout)
-        e = [float((a.float() - b.float()).abs().max() / b.float().abs().max())
-             for a, b in ((Y, ref_y), (dX, rdx.permute(0, 2, 3, 1).reshape(M, cin)), (dW, rdw.reshape(cout, cin)))]
+        e = [nan, nan, nan]
+        rel = lambda a, b: float((a.float() - b.float()).abs().max() / b.float().abs().max())  # noqa: E731
+        if ok_w:
+            K.gemm(dY2, cout, 0, X2, cin, 0, dW, cin, cout, cin, M, epi=acc)
+            e[2] = rel(dW, rdw.reshape(cout, cin))
+        if ok_f:
+            K.gemm(X2, cin, 1, W2, cin, 1, Y, cout, M, cout, cin)
+            e[0] = rel(Y, ref_y)
+        if ok_d:
+            K.gemm(dY2, cout, 1, W2, cin, 0, dX, cin, M, cin, cout, epi=res)
+            e[1] = rel(dX, rdx.permute(0, 2, 3, 1).reshape(M, cin) + skip)
         f = lambda t: f"{t * 1e3:7.1f} ({fl / t / 1e9:5.0f})"  # noqa: E731
-        print(f"{cin:4d}->{cout:4d} {H:2d}x{H:<2d} M={M:7d} | MIOpen fwd {f(t_mf)} dX {f(t_md)} dW {f(t_mw)} | "
-              f"mmu fwd {f(t_gf)} dX {f(t_gd)} dW {f(t_gw)} | rel err {e[0]:.1e} {e[1]:.1e} {e[2]:.1e}", flush=True)
+        print(f"{cin:4d}->{cout:4d} {H:2d}x{H:<2d} M={M:7d} | MIOpen fwd {f(t_mf)} dX {f(t_md)} dW {f(t_mw)} "
+              f"dX+add {t_ma * 1e3:7.1f} | mmu fwd {f(t_gf)} dX {f(t_gd)} dW {f(t_gw)} dX+add {t_ga * 1e3:7.1f} | "
+              f"rel err {e[0]:.1e} {e[1]:.1e} {e[2]:.1e}", flush=True)
 
 
 if __name__ == "__main__":
