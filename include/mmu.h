@@ -194,6 +194,13 @@ int mmu_embed_bwd(const void* dX, const int64_t* ids, const int64_t* seg,
                   float drop_txt, float drop_img, uint64_t seed, float* d_word, float* d_pos, float* d_type, float* d_ln_w, float* d_ln_b,
                   float* d_proj, float* ws, mmu_stream_t stream);
 
+/* Image transform tail of the Food-101 pipeline (src/dataset.py:488-498: ToTensor +
+ * Normalize) on the device: in = uint8 crops [B,H,W,3] (HWC, as decoded), n = B*H*W*3;
+ * out = (in/255 - mean[c]) / std[c] with c = index % 3, i.e. the channels-last
+ * [B,3,H,W] image, f32 (out_dtype MMU_F32) or bf16 (MMU_BF16).  mean / std: 3 host floats. */
+int mmu_image_normalize(const uint8_t* in, int64_t n, const float* mean, const float* stdv, void* out,
+                        int out_dtype, mmu_stream_t stream);
+
 /* AdaptiveAvgPool2d((n,1)) + flatten + transpose of the ResNet map
  * (src/mmbt.py:30,42-44): fmap NHWC bf16 [B,Hh,Ww,C] -> out f32 [B,n,C]; and its backward. */
 int mmu_row_pool_fwd(const void* fmap, int64_t B, int64_t Hh, int64_t Ww, int64_t C, int64_t n,

@@ -416,6 +416,17 @@ int mmu_embed_bwd(const void* dX, const int64_t* ids, const int64_t* seg, const 
   return check_launch("mmu_embed_bwd");
 }
 
+int mmu_image_normalize(const uint8_t* in, int64_t n, const float* mean, const float* stdv, void* out,
+                        int out_dtype, mmu_stream_t stream) {
+  if (!in || !out || !mean || !stdv || n < 0) return fail("mmu_image_normalize: bad args");
+  if (out_dtype != MMU_BF16 && out_dtype != MMU_F32) return fail("mmu_image_normalize: bad out_dtype");
+  for (int c = 0; c < 3; ++c)
+    if (!(stdv[c] > 0.f)) return fail("mmu_image_normalize: std must be > 0");
+  if (n == 0) return 0;
+  image_normalize_launch(in, n, mean, stdv, out, out_dtype == MMU_BF16, (hipStream_t)stream);
+  return check_launch("mmu_image_normalize");
+}
+
 int mmu_row_pool_fwd(const void* fmap, int64_t B, int64_t Hh, int64_t Ww, int64_t C, int64_t n, float* out,
                      mmu_stream_t stream) {
   if (!fmap || !out || C % 8 || n <= 0 || n > Hh) return fail("mmu_row_pool_fwd: bad args");

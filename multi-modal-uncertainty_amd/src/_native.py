@@ -52,6 +52,7 @@ SIGNATURES = {
     "mmu_embed_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64,
                               c_i64, c_i64, c_i64, c_f32, c_f32, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                               c_vp]),
+    "mmu_image_normalize": (c_i32, [c_vp, c_i64, c_f32p, c_f32p, c_vp, c_i32, c_vp]),
     "mmu_row_pool_fwd": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "mmu_row_pool_bwd": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "mmu_batchnorm_ws_bytes": (c_i64, [c_i64]),

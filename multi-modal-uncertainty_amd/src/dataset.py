@@ -8,6 +8,12 @@ Vocab/get_vocab :440-472, get_food101 :474-545).  Differences forced by the imag
   * BertTokenizer.from_pretrained needs the network: the vocab is read from a local
     file (`<DATA_DIR>/<bert_model>-vocab.txt` or $BERT_VOCAB) via transformers' BertTokenizer.
 ``SyntheticFood101`` produces batches of the same contract for benchmarks and tests.
+
+GPU input tail: with ``gpu_normalize=True`` the workers stop after
+decode / resize / center-crop (``food101_crop_u8``: uint8 HWC, 150 KB per image instead of
+602 KB of f32), and ``DevicePrefetcher`` copies the next pinned batch to the GPU on a side
+stream and runs ToTensor + Normalize there (mmu_image_normalize), one batch ahead of the
+training step.
 """
 import json
 import os
@@ -23,8 +29,7 @@ MEAN = (0.46777044, 0.44531429, 0.40661017)
 STD = (0.12221994, 0.12145835, 0.14380469)
 
 
-def food101_transform(img, size=256, crop=224):
-    """Resize shorter side to `size` (bilinear), center-crop `crop`, to [0,1] CHW, normalise."""
+def _resize_crop(img, size, crop):
     from PIL import Image
     w, h = img.size
     if w <= h:
@@ -33,10 +38,74 @@ def food101_transform(img, size=256, crop=224):
         nw, nh = int(size * w / h), size
     img = img.resize((nw, nh), Image.BILINEAR)
     left, top = int(round((nw - crop) / 2.0)), int(round((nh - crop) / 2.0))
-    img = img.crop((left, top, left + crop, top + crop))
-    a = np.asarray(img, dtype=np.float32) / 255.0
+    return np.asarray(img.crop((left, top, left + crop, top + crop)), dtype=np.uint8)
+
+
+def food101_transform(img, size=256, crop=224):
+    """Resize shorter side to `size` (bilinear), center-crop `crop`, to [0,1] CHW, normalise
+    (Resize(256) / CenterCrop(224) / ToTensor / Normalize, reference src/dataset.py:488-498)."""
+    a = _resize_crop(img, size, crop).astype(np.float32) / 255.0
     a = (a - np.array(MEAN, dtype=np.float32)) / np.array(STD, dtype=np.float32)
     return torch.from_numpy(a.transpose(2, 0, 1).copy())
+
+
+def food101_crop_u8(img, size=256, crop=224):
+    """The worker half of food101_transform: resize + center-crop only -> uint8 [crop, crop, 3]
+    (HWC); ToTensor + Normalize run on the GPU (DevicePrefetcher / mmu_image_normalize)."""
+    return torch.from_numpy(_resize_crop(img, size, crop).copy())
+
+
+class DevicePrefetcher:
+    """Wraps a DataLoader of ``collate_fn`` batches: copies batch i+1 to ``device`` on a side
+    stream (non-blocking from pinned memory) while batch i trains, and turns uint8 HWC crops
+    into the normalised channels-last image there (mmu_image_normalize; f32 images, e.g.
+    from food101_transform or SyntheticFood101, are only copied).  Yields the same
+    ((text, segment, mask, img), tgt) tuples, already on the device."""
+
+    def __init__(self, loader, device, mean=MEAN, std=STD, dtype=torch.float32):
+        self.loader, self.device, self.mean, self.std, self.dtype = loader, torch.device(device), mean, std, dtype
+        self.dataset = getattr(loader, "dataset", None)
+
+    def __len__(self):
+        return len(self.loader)
+
+    def _stage(self, batch, stream):
+        from . import kernels as K
+        (txt, seg, mask, img), tgt = batch
+        with torch.cuda.stream(stream):
+            txt, seg, mask, tgt = (t.to(self.device, non_blocking=True) for t in (txt, seg, mask, tgt))
+            if img.dtype == torch.uint8:
+                raw = img.to(self.device, non_blocking=True)
+                B, H, W, _ = raw.shape
+                img = torch.empty((B, 3, H, W), dtype=self.dtype, device=self.device,
+                                  memory_format=torch.channels_last)
+                K.image_normalize(raw, self.mean, self.std, img)
+                raw.record_stream(stream)
+            else:
+                img = img.to(self.device, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        return ((txt, seg, mask, img), tgt), ev
+
+    def __iter__(self):
+        stream = torch.cuda.Stream(device=self.device)
+        it = iter(self.loader)
+        nxt = None
+        try:
+            nxt = self._stage(next(it), stream)
+        except StopIteration:
+            return
+        while nxt is not None:
+            batch, ev = nxt
+            try:
+                nxt = self._stage(next(it), stream)
+            except StopIteration:
+                nxt = None
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_event(ev)
+            for t in (*batch[0], batch[1]):
+                t.record_stream(cur)
+            yield batch
 
 
 class Vocab(object):
@@ -147,7 +216,7 @@ def collate_fn(batch):
 
 
 def get_food101(bert_model="bert-base-uncased", datapath=None, drop_img_percent=0.0, max_seq_len=512,
-                num_image_embeds=3, batch_size=128, n_workers=20):
+                num_image_embeds=3, batch_size=128, n_workers=20, gpu_normalize=False, device=None):
     datapath = datapath or os.environ["DATA_DIR"]
     tokenizer = bert_tokenizer(bert_model).tokenize
     labels, _ = get_labels_and_frequencies(os.path.join(datapath, "train.jsonl"))
@@ -155,12 +224,14 @@ def get_food101(bert_model="bert-base-uncased", datapath=None, drop_img_percent=
     n_classes = len(labels)
 
     def make(split):
-        return JsonlDataset(os.path.join(datapath, f"{split}.jsonl"), tokenizer, food101_transform, vocab, n_classes,
+        tf = food101_crop_u8 if gpu_normalize else food101_transform
+        return JsonlDataset(os.path.join(datapath, f"{split}.jsonl"), tokenizer, tf, vocab, n_classes,
                             drop_img_percent, max_seq_len, num_image_embeds, labels)
 
     def loader(ds, shuffle):
-        return torch.utils.data.DataLoader(ds, batch_size=batch_size, shuffle=shuffle, num_workers=n_workers,
-                                           collate_fn=collate_fn, pin_memory=torch.cuda.is_available())
+        dl = torch.utils.data.DataLoader(ds, batch_size=batch_size, shuffle=shuffle, num_workers=n_workers,
+                                         collate_fn=collate_fn, pin_memory=torch.cuda.is_available())
+        return DevicePrefetcher(dl, device) if gpu_normalize else dl
 
     return loader(make("train"), True), loader(make("dev"), False), loader(make("test"), False), n_classes, vocab
 

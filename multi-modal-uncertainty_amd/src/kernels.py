@@ -231,6 +231,23 @@ def embed_bwd(dX, ids, seg, proj, word, pos, typ, ln_w, mean, rstd, cls_id, sep_
            _ptr(d_pos), _ptr(d_type), _ptr(d_ln_w), _ptr(d_ln_b), _ptr(d_proj), _ptr(ws), _stream(dX))
 
 
+def image_normalize(img_u8, mean, std, out):
+    """uint8 HWC crops [B, H, W, 3] -> out = (x/255 - mean) / std as the channels-last
+    [B, 3, H, W] image (f32 or bf16); see mmu_image_normalize."""
+    _dev_check(img_u8, out)
+    _want(img_u8, torch.uint8, "image_normalize input")
+    if not img_u8.is_contiguous() or img_u8.shape[-1] != 3:
+        raise N.NativeError("image_normalize: input must be contiguous [B, H, W, 3] uint8")
+    if out.dtype not in (torch.float32, torch.bfloat16) or out.numel() != img_u8.numel() or \
+            not out.is_contiguous(memory_format=torch.channels_last):
+        raise N.NativeError("image_normalize: out must be a channels-last f32/bf16 [B, 3, H, W] of the same size")
+    m = (ctypes.c_float * 3)(*[float(v) for v in mean])
+    s = (ctypes.c_float * 3)(*[float(v) for v in std])
+    N.call("mmu_image_normalize", _ptr(img_u8), img_u8.numel(), m, s, _ptr(out),
+           N.MMU_F32 if out.dtype == torch.float32 else N.MMU_BF16, _stream(out))
+    return out
+
+
 def row_pool_fwd(fmap_nhwc, n, out):
     _dev_check(fmap_nhwc, out)
     B, Hh, Ww, C = fmap_nhwc.shape

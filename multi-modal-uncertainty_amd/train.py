@@ -56,6 +56,8 @@ FLAGS = [
     ("--img_embed_pool_type", dict(type=str, default="avg", choices=["max", "avg"])),
     ("--img_hidden_sz", dict(type=int, default=2048)), ("--include_bn", dict(type=int, default=True)),
     ("--max_seq_len", dict(type=int, default=512)), ("--n_workers", dict(type=int, default=0)),
+    ("--gpu_normalize", dict(type=int, default=1, help="Food-101: workers ship uint8 crops, ToTensor + Normalize "
+                                                      "run on the GPU one batch ahead (src/dataset.py)")),
     ("--num_image_embeds", dict(type=int, default=3)), ("--warmup", dict(type=float, default=0.1)),
     # build additions
     ("--gin_file", dict(nargs="*", default=[])), ("--gin_param", dict(nargs="*", default=[])),
@@ -180,9 +182,11 @@ def food101_data(args, rank=0, world=1):
             ds, batch_size=args.batch_size, shuffle=shuf and smp is None, sampler=smp, num_workers=args.n_workers,
             collate_fn=dataset.collate_fn, pin_memory=True)
         return mk(tr, True, sampler), mk(va, False), mk(te, False), 101, _Vocab()
+    gpu = bool(args.gpu_normalize) and torch.cuda.is_available()
     return dataset.get_food101(datapath=args.datapath, batch_size=args.batch_size,
                                drop_img_percent=args.drop_img_percent, max_seq_len=args.max_seq_len,
-                               num_image_embeds=args.num_image_embeds, n_workers=args.n_workers)
+                               num_image_embeds=args.num_image_embeds, n_workers=args.n_workers,
+                               gpu_normalize=gpu, device=torch.device("cuda", args.device) if gpu else None)
 
 
 def _dp_wrap(model, optimizer, accum):

@@ -1,5 +1,3 @@
 set -o pipefail
-timeout -k 10 300 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/t_gpu.log 2>&1 || { grep -E "Error|FAILED|err " gpurun_out/t_gpu.log | head -30; exit 1; }
+timeout -k 10 300 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/t_gpu.log 2>&1 || { grep -E "Error|FAILED|err" gpurun_out/t_gpu.log | head -30; exit 1; }
 tail -2 gpurun_out/t_gpu.log
-timeout -k 10 400 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench.log 2>&1 || { tail -30 gpurun_out/bench.log; exit 1; }
-tail -1 gpurun_out/bench.log
