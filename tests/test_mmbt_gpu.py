@@ -188,3 +188,47 @@ def test_side_stream_weight_grads_identical(dev, monkeypatch):
         grads.append(model.store.grad.clone())  # read on the main stream right after backward
     scale = grads[0].abs().max().item()
     torch.testing.assert_close(grads[1], grads[0], rtol=1e-4, atol=1e-6 * scale)
+
+
+def test_checkpoint_roundtrip_resumes_identically(dev, tmp_path, monkeypatch):
+    """Checkpoint format: save_weights (reference src/utils.py:98-106:
+    {'model', 'optimizer'}) -> torch.load(weights_only=True) -> load_state_dict into a fresh
+    model + BertAdam (the resume path, reference train.py:269-274) continues training exactly
+    like the uninterrupted run (up to float-atomic summation order in the bias-grad sums)."""
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    from src.optim import BertAdam
+    from src.testing import synthetic_batch
+    from src.utils import save_weights
+
+    def make():
+        model, _, cfg = build("small", dev, bert_hidden_dropout=0.0, bert_attn_dropout=0.0, dropout=0.0)
+        named = list(model.named_parameters())
+        no_decay = ["bias", "LayerNorm.bias", "LayerNorm.weight"]
+        groups = [{"params": [p for n, p in named if not any(nd in n for nd in no_decay)], "weight_decay": 0.01},
+                  {"params": [p for n, p in named if any(nd in n for nd in no_decay)], "weight_decay": 0.0}]
+        return model.train(), BertAdam(groups, lr=1e-3, warmup=0.1, t_total=10.0), cfg
+
+    m1, o1, cfg = make()
+    x, y = synthetic_batch(2, 16, vocab=cfg.vocab, seed=3)
+    x, y = tuple(t.to(dev) for t in x), y.to(dev)
+
+    def step(m, o):
+        o.zero_grad()
+        m.compute_loss(m(*x), y).backward()
+        o.step()
+
+    step(m1, o1)
+    path = tmp_path / "model_last_epoch.pt"
+    save_weights(m1, o1, str(path))
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    assert set(ck) == {"model", "optimizer"} and len(ck["model"]) == len(m1.state_dict())
+    m2, o2, _ = make()
+    m2.load_state_dict(ck["model"])
+    o2.load_state_dict(ck["optimizer"])
+    for a, b in zip(m1.state_dict().values(), m2.state_dict().values()):
+        assert torch.equal(a.cpu(), b.cpu())
+    step(m1, o1)
+    step(m2, o2)
+    assert all(s["step"] == 2 for s in o2.state_dict()["state"].values())
+    for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-6, msg=n)
