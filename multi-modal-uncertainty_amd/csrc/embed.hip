@@ -103,6 +103,7 @@ void embed_fwd_launch(const EmbedParams& p, hipStream_t s) {
 //          per-64-row partial sums of dgamma / dbeta
 __global__ __launch_bounds__(256) void embed_bwd_rows_kernel(EmbedBwdParams q, EmbedParams p) {
   __shared__ float red[2][4][768];
+  __shared__ __attribute__((aligned(16))) float xch[4][768];  // per wave: a text row's dx, re-read lane-contiguous
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t S = q.n_img + 2 + q.T, rows = q.B * S, H = 768;
   float* dsum = q.ws;
@@ -149,11 +150,18 @@ __global__ __launch_bounds__(256) void embed_bwd_rows_kernel(EmbedBwdParams q, E
       for (int k = 0; k < 4; ++k) dx[k] = rs * (g[i][k] - s1 - xh[i][k] * s2);
       *(float4*)(dsum + row * H + c) = make_float4(dx[0], dx[1], dx[2], dx[3]);
       if (text) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) atomicAdd(wrow + c + k, dx[k]);
+        *(float4*)(&xch[wv][c]) = make_float4(dx[0], dx[1], dx[2], dx[3]);
       } else if (img) {
         *(float4*)(q.d_proj + (b * q.n_img + (s - 1)) * H + c) = make_float4(dx[0], dx[1], dx[2], dx[3]);
       }
+    }
+    if (text) {  // word-row scatter: every atomic instruction adds 256 contiguous bytes (lane l ->
+                 // column 64 j + l); 16-B-strided lanes ran the memory-side atomics at a fraction
+                 // of their rate.  The row sits in this wave's own LDS slice: in-order LDS, no barrier.
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int j = 0; j < 12; ++j) atomicAdd(wrow + 64 * j + l, xch[wv][64 * j + l]);
+      __builtin_amdgcn_wave_barrier();
     }
   }
 #pragma unroll
