@@ -1192,8 +1192,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     uint4 v = qv ? *(const uint4*)(dob + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
     df[ks] = *(bf16x8*)&v;
   }
+  // delta = rowsum(dO * O) of this head, from the dO fragments already in registers and the
+  // same 32 columns of O (the half-waves hold the two halves of the row); written for the
+  // dK/dV kernel that runs next (replaces the separate attn_delta_kernel pass over O and dO)
+  float dsum = 0.f;
+  {
+    const bf16* ob = p.o + ((int64_t)b * L + q) * p.ld_o + hd * 64;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      uint4 u = qv ? *(const uint4*)(ob + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
+      const bf16x8 ov = *(bf16x8*)&u;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dsum = fmaf(bf2f(ov[e]), bf2f(df[ks][e]), dsum);
+    }
+    dsum += __shfl_xor(dsum, 32, 64);
+    if (qv && h == 0) p.delta[(int64_t)bh * L + q] = dsum;
+  }
   const float nlse = qv ? -p.lse[(int64_t)bh * L + q] : -__builtin_huge_valf();
-  const float dlt = qv ? p.delta[(int64_t)bh * L + q] : 0.f;
+  const float dlt = dsum;
   const float ndz = -dlt / zs;
   f32x16 dq[2];
 #pragma unroll
@@ -1308,11 +1324,12 @@ static bool attn_dma() {
 bool attention_bwd_fuses_colsum() { return attn_dma(); }
 
 void attention_bwd_launch(const AttnParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(attn_delta_kernel, dim3((p.L + 31) / 32, p.batch * p.heads), dim3(256), 0, s, p);
-  if (attn_dma())
+  if (attn_dma()) {  // the dQ kernel computes (and stores) delta itself
     hipLaunchKernelGGL(attn_dq_dma_kernel, dim3((p.L + 127) / 128, p.batch * p.heads), dim3(256), 0, s, p);
-  else
+  } else {
+    hipLaunchKernelGGL(attn_delta_kernel, dim3((p.L + 31) / 32, p.batch * p.heads), dim3(256), 0, s, p);
     hipLaunchKernelGGL(attn_dq_kernel, dim3((p.L + 127) / 128, p.batch * p.heads), dim3(256), 0, s, p);
+  }
   if (attn_dma() && drop_thr(p.drop_p))
     hipLaunchKernelGGL(attn_dkdv_dma_kernel<true>, dim3((p.L + 63) / 64, p.batch * p.heads), dim3(128), 0, s, p);
   else if (attn_dma())
