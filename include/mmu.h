@@ -201,6 +201,15 @@ int mmu_embed_bwd(const void* dX, const int64_t* ids, const int64_t* seg,
 int mmu_image_normalize(const uint8_t* in, int64_t n, const float* mean, const float* stdv, void* out,
                         int out_dtype, mmu_stream_t stream);
 
+/* MaxPool2d(3, stride 2, padding 1) of the ResNet stem (torchvision resnet child 3,
+ * src/mmbt.py:19-21): x NHWC bf16 [B,H,W,C] -> y [B,OH,OW,C] + argmax (uint8 position 0..8
+ * in the window, same layout as y); backward: dy + argmax -> dx [B,H,W,C] (every element
+ * written).  C % 8 == 0, OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1. */
+int mmu_maxpool_fwd(const void* x, int64_t B, int64_t H, int64_t W, int64_t C, void* y, uint8_t* argmax,
+                    mmu_stream_t stream);
+int mmu_maxpool_bwd(const void* dy, const uint8_t* argmax, int64_t B, int64_t H, int64_t W, int64_t C, void* dx,
+                    mmu_stream_t stream);
+
 /* AdaptiveAvgPool2d((n,1)) + flatten + transpose of the ResNet map
  * (src/mmbt.py:30,42-44): fmap NHWC bf16 [B,Hh,Ww,C] -> out f32 [B,n,C]; and its backward. */
 int mmu_row_pool_fwd(const void* fmap, int64_t B, int64_t Hh, int64_t Ww, int64_t C, int64_t n,

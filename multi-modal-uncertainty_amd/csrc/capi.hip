@@ -427,6 +427,24 @@ int mmu_image_normalize(const uint8_t* in, int64_t n, const float* mean, const f
   return check_launch("mmu_image_normalize");
 }
 
+int mmu_maxpool_fwd(const void* x, int64_t B, int64_t H, int64_t W, int64_t C, void* y, uint8_t* argmax,
+                    mmu_stream_t stream) {
+  if (!x || !y || !argmax || B <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8 || H > 65536 || W > 65536)
+    return fail("mmu_maxpool_fwd: bad args");
+  maxpool3s2_fwd_launch((const bf16*)x, B, (int)H, (int)W, (int)C, (int)((H - 1) / 2 + 1), (int)((W - 1) / 2 + 1),
+                        (bf16*)y, argmax, (hipStream_t)stream);
+  return check_launch("mmu_maxpool_fwd");
+}
+
+int mmu_maxpool_bwd(const void* dy, const uint8_t* argmax, int64_t B, int64_t H, int64_t W, int64_t C, void* dx,
+                    mmu_stream_t stream) {
+  if (!dy || !dx || !argmax || B <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8 || H > 65536 || W > 65536)
+    return fail("mmu_maxpool_bwd: bad args");
+  maxpool3s2_bwd_launch((const bf16*)dy, argmax, B, (int)H, (int)W, (int)C, (int)((H - 1) / 2 + 1),
+                        (int)((W - 1) / 2 + 1), (bf16*)dx, (hipStream_t)stream);
+  return check_launch("mmu_maxpool_bwd");
+}
+
 int mmu_row_pool_fwd(const void* fmap, int64_t B, int64_t Hh, int64_t Ww, int64_t C, int64_t n, float* out,
                      mmu_stream_t stream) {
   if (!fmap || !out || C % 8 || n <= 0 || n > Hh) return fail("mmu_row_pool_fwd: bad args");

@@ -109,6 +109,10 @@ struct EmbedBwdParams {
 void embed_bwd_launch(const EmbedBwdParams& p, hipStream_t s);
 void image_normalize_launch(const uint8_t* in, int64_t n, const float* mean, const float* stdv, void* out,
                             bool out_bf16, hipStream_t s);
+void maxpool3s2_fwd_launch(const bf16* x, int64_t B, int H, int W, int C, int OH, int OW, bf16* y, uint8_t* am,
+                           hipStream_t s);
+void maxpool3s2_bwd_launch(const bf16* dy, const uint8_t* am, int64_t B, int H, int W, int C, int OH, int OW,
+                           bf16* dx, hipStream_t s);
 void row_pool_fwd_launch(const bf16* fmap, int64_t B, int64_t Hh, int64_t Ww, int64_t C, int64_t n, float* out,
                          hipStream_t s);
 void row_pool_bwd_launch(const float* dout, int64_t B, int64_t Hh, int64_t Ww, int64_t C, int64_t n, bf16* dfmap,

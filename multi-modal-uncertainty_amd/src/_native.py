@@ -53,6 +53,8 @@ SIGNATURES = {
                               c_i64, c_i64, c_i64, c_f32, c_f32, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                               c_vp]),
     "mmu_image_normalize": (c_i32, [c_vp, c_i64, c_f32p, c_f32p, c_vp, c_i32, c_vp]),
+    "mmu_maxpool_fwd": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "mmu_maxpool_bwd": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "mmu_row_pool_fwd": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "mmu_row_pool_bwd": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "mmu_batchnorm_ws_bytes": (c_i64, [c_i64]),

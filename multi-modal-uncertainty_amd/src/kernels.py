@@ -248,6 +248,21 @@ def image_normalize(img_u8, mean, std, out):
     return out
 
 
+def maxpool_fwd(x, y, argmax):
+    """MaxPool2d(3, 2, 1) of a channels-last bf16 [B, C, H, W] map -> y [B, C, OH, OW]
+    (channels-last) and the uint8 argmax in y's NHWC layout; see mmu_maxpool_fwd."""
+    _dev_check(x, y, argmax)
+    _want(x, torch.bfloat16, "maxpool x")
+    B, C, H, W = x.shape
+    N.call("mmu_maxpool_fwd", _ptr(x), B, H, W, C, _ptr(y), _ptr(argmax), _stream(x))
+
+
+def maxpool_bwd(dy, argmax, dx):
+    _dev_check(dy, argmax, dx)
+    B, C, H, W = dx.shape
+    N.call("mmu_maxpool_bwd", _ptr(dy), _ptr(argmax), B, H, W, C, _ptr(dx), _stream(dx))
+
+
 def row_pool_fwd(fmap_nhwc, n, out):
     _dev_check(fmap_nhwc, out)
     B, Hh, Ww, C = fmap_nhwc.shape

@@ -256,6 +256,42 @@ class StoreConv2d(nn.Conv2d):
         return super().forward(x)
 
 
+class _MaxPool3s2(torch.autograd.Function):
+    """MaxPool2d(3, 2, 1) on a channels-last bf16 map via mmu_maxpool_fwd / _bwd (1-byte
+    argmax per output element; the backward is a gather over the covering windows)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        B, C, H, W = x.shape
+        OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        y = torch.empty((B, C, OH, OW), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+        am = torch.empty((B, OH, OW, C), dtype=torch.uint8, device=x.device)
+        K.maxpool_fwd(x, y, am)
+        ctx.save_for_backward(am)
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (am,) = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = torch.empty(ctx.shape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
+        K.maxpool_bwd(dy, am, dx)
+        return dx
+
+
+class MaxPool2d(nn.MaxPool2d):
+    """nn.MaxPool2d (torchvision's stem pool, child 3) whose 3x3 / stride-2 / pad-1 case on
+    channels-last bf16 maps runs the HIP kernels; anything else is PyTorch's."""
+
+    def forward(self, x):
+        if (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0
+                and self.kernel_size in (3, (3, 3)) and self.stride in (2, (2, 2)) and self.padding in (1, (1, 1))
+                and self.dilation in (1, (1, 1)) and not self.ceil_mode and not self.return_indices):
+            return _MaxPool3s2.apply(x.contiguous(memory_format=torch.channels_last))
+        return super().forward(x)
+
+
 class FusedReLU(nn.ReLU):
     """The stem's ReLU slot (torchvision child index 2): the preceding BatchNorm2d
     already applied it, so this is the identity."""
@@ -296,7 +332,7 @@ def resnet152_trunk(blocks=(3, 8, 36, 3)):
     stem_bn = BatchNorm2d(64)
     stem_bn.fused_relu = True
     mods = [StoreConv2d(3, 64, 7, stride=2, padding=3, bias=False), stem_bn, FusedReLU(inplace=True),
-            nn.MaxPool2d(3, 2, 1)]
+            MaxPool2d(3, 2, 1)]
     cin = 64
     for i, (width, n) in enumerate(zip((64, 128, 256, 512), blocks)):
         stage = []

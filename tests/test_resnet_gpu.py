@@ -73,3 +73,27 @@ def test_bottleneck_mmu_1x1_matches_miopen(dev, monkeypatch, cin, width, hw, bat
     _close(dx1, dx0, "input grad")
     for n in gr0:
         _close(gr1[n], gr0[n], f"grad {n}")
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (3, 16, 7, 9)])
+def test_stem_maxpool_matches_torch(dev, shape):
+    """MaxPool2d(3, 2, 1) (torchvision resnet child 3) on mmu_maxpool_fwd/bwd vs torch's
+    max_pool2d on the same bf16 channels-last input: forward bit-exact (first maximum wins
+    ties; post-ReLU maps are full of ties at 0), backward: the gradient of every window goes
+    to the same element (sums of <= 4 bf16 values in f32, rounded once)."""
+    from src import resnet as R
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(shape, generator=g).clamp_(min=0)
+    x = (x * 4).round_() / 4                              # many exact ties
+    x = x.to(dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    pool = R.MaxPool2d(3, 2, 1)
+    y = pool(x)
+    ref_x = x.detach().clone().requires_grad_(True)
+    ref = torch.nn.functional.max_pool2d(ref_x, 3, 2, 1)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(y.float(), ref.float())
+    gy = torch.randn(ref.shape, generator=g).to(dev).to(torch.bfloat16)
+    y.backward(gy)
+    ref.backward(gy)
+    torch.testing.assert_close(x.grad.float(), ref_x.grad.float(), rtol=1e-2, atol=1e-2)
+    assert (x.grad.float() != 0).sum() == (ref_x.grad.float() != 0).sum()
