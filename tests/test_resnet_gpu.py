@@ -4,10 +4,12 @@ the f32 gradient) against the same block with every conv product on MIOpen and a
 summing the skip gradient.  Shapes are chosen so that every branch of _mmu_1x1 runs:
   1024 -> 256 at 14x14, batch 128 (M = 25088): fwd, dX + skip, dW on conv1 and conv3
   256 -> 64 at 56x56, batch 4 (M = 12544): conv1 dX + skip with K = 64; the rest MIOpen
-Tolerance: bf16 products (f32 accumulation) on both sides; relative Frobenius error <= 2e-2.
-(A max-error bound is the wrong yardstick here: the two engines round differently, which
-flips a few ReLU masks in bn1 / bn2 at pre-activations near 0, and one flipped element
-moves its whole upstream gradient.)
+Yardstick: the same block in fp32 (PyTorch convs and batch norm) is the truth; the mmu
+path's relative Frobenius error against it must be within 1.25x (+1e-3) of the all-MIOpen
+bf16 path's own error.  (A fixed bound on the bf16-vs-bf16 difference is the wrong test:
+both engines round, three BatchNorm backwards amplify it through their mean subtraction,
+and a few ReLU masks flip at pre-activations near 0, so the difference sits at 2-3 % either
+way; a max-error bound is worse still, one flipped element moves its whole gradient.)
 """
 import pytest
 import torch
@@ -26,17 +28,26 @@ class _Store:
         return self.w[name]
 
 
-def _run(block, x, g):
+def _run(block, x, g, fp32=False):
     from src import resnet as R
-    xx = x.clone().requires_grad_(True)
+    xx = (x.float() if fp32 else x).clone().requires_grad_(True)
     for p in block.parameters():
         p.grad = None
-    with torch.autocast("cuda", dtype=torch.bfloat16):
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=not fp32):
         used_sink = block.downsample is None and block.conv1.takes_skip_grad(xx)
         y = block(xx)
     y.float().backward(g)
     assert isinstance(block.conv1, R.StoreConv2d)
     return y.float(), xx.grad.float(), {n: p.grad.float().clone() for n, p in block.named_parameters()}, used_sink
+
+
+def _rel(a, b):
+    return (a - b).double().norm().item() / (b.double().norm().item() + 1e-12)
+
+
+def _no_worse(mmu, miopen, ref, what, slack=1.25, eps=1e-3):
+    e1, e0 = _rel(mmu, ref), _rel(miopen, ref)
+    assert e1 <= slack * e0 + eps, f"{what}: mmu path error {e1:.3e} vs MIOpen path error {e0:.3e} (fp32 truth)"
 
 
 def _close(a, b, what, frac=2e-2):
@@ -69,10 +80,12 @@ def test_bottleneck_mmu_1x1_matches_miopen(dev, monkeypatch, cin, width, hw, bat
     monkeypatch.setattr(R, "_mmu_1x1", lambda *a: (False, False, False))
     y0, dx0, gr0, sink0 = _run(block, x, gy)
     assert not sink0
-    _close(y1, y0, "output")
-    _close(dx1, dx0, "input grad")
+    yr, dxr, grr, _ = _run(block, x, gy, fp32=True)
+    _close(y1, yr, "output vs fp32", frac=2e-2)
+    _no_worse(y1, y0, yr, "output")
+    _no_worse(dx1, dx0, dxr, "input grad")
     for n in gr0:
-        _close(gr1[n], gr0[n], f"grad {n}")
+        _no_worse(gr1[n], gr0[n], grr[n], f"grad {n}")
 
 
 @pytest.mark.parametrize("shape", [(4, 64, 112, 112), (3, 16, 7, 9)])
@@ -97,3 +110,39 @@ def test_stem_maxpool_matches_torch(dev, shape):
     ref.backward(gy)
     torch.testing.assert_close(x.grad.float(), ref_x.grad.float(), rtol=1e-2, atol=1e-2)
     assert (x.grad.float() != 0).sum() == (ref_x.grad.float() != 0).sum()
+
+
+def test_model_grads_with_mmu_1x1_match_miopen(dev, monkeypatch):
+    """Whole small MMBT (bf16 trunk, the bench precision) at batch 64: every ResNet weight
+    gradient with the 1x1 products on mmu_gemm -- through the parameter store's bf16
+    filter copies and channels-last f32 gradient views (layer3/4 dW at 14x14 and 7x7,
+    dX, the 28x28 forward) -- against the all-MIOpen path, both measured against the fp32 trunk (_no_worse)."""
+    from oracle.weights import SMALL, make_state_dict
+    from src import resnet as R
+    from src.mmbt import MultimodalBertClf
+    from src.testing import small_args, synthetic_batch
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    x, y = synthetic_batch(64, 16, vocab=SMALL.vocab, seed=9)
+    x, y = tuple(t.to(dev) for t in x), y.to(dev)
+    sd = make_state_dict(0, SMALL)
+    assert R._mmu_1x1(1024, 512, 64 * 196, 14) == (False, True, True)
+
+    def grads(precision="bf16"):
+        torch.manual_seed(0)
+        m = MultimodalBertClf(small_args(bert_hidden_dropout=0.0, bert_attn_dropout=0.0, dropout=0.0,
+                                         img_precision=precision))
+        m.load_state_dict(sd, strict=True)
+        m = m.to(dev).train()
+        m.store.zero_grad()
+        loss = m.compute_loss(m(*x), y)
+        loss.backward()
+        return loss.item(), {n: p.grad.float().clone() for n, p in m.named_parameters() if "img_encoder" in n}
+
+    l1, g1 = grads()
+    monkeypatch.setattr(R, "_mmu_1x1", lambda *a: (False, False, False))
+    l0, g0 = grads()
+    lr, gr = grads("fp32")                          # the trunk in fp32: the truth for both
+    assert abs(l1 - lr) <= 1e-2 * abs(lr)
+    for n in g0:
+        if n.endswith("weight") and g0[n].dim() == 4:
+            _no_worse(g1[n], g0[n], gr[n], f"grad {n}")
