@@ -1,3 +1,5 @@
 set -o pipefail
-timeout -k 10 300 python -u -m pytest tests/test_resnet_gpu.py -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/t_resnet.log 2>&1 || { grep -E "Error|FAILED|err|assert" gpurun_out/t_resnet.log | head -30; exit 1; }
-tail -1 gpurun_out/t_resnet.log
+timeout -k 10 400 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/t_gpu.log 2>&1 || { grep -E "Error|FAILED|assert" gpurun_out/t_gpu.log | head -30; exit 1; }
+tail -1 gpurun_out/t_gpu.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+tail -2 gpurun_out/smoke.log
