@@ -65,6 +65,7 @@ class DevicePrefetcher:
     def __init__(self, loader, device, mean=MEAN, std=STD, dtype=torch.float32):
         self.loader, self.device, self.mean, self.std, self.dtype = loader, torch.device(device), mean, std, dtype
         self.dataset = getattr(loader, "dataset", None)
+        self.sampler = getattr(loader, "sampler", None)  # Model_.train_loop sets a DistributedSampler's epoch
 
     def __len__(self):
         return len(self.loader)
@@ -144,8 +145,8 @@ def bert_tokenizer(bert_model):
 def get_vocab(bert_model):
     tok = bert_tokenizer(bert_model)
     vocab = Vocab()
-    vocab.stoi = dict(tok.vocab)
-    vocab.itos = dict(tok.ids_to_tokens)
+    vocab.stoi = dict(tok.get_vocab())  # (transformers 5 has no .ids_to_tokens: invert the map)
+    vocab.itos = {i: w for w, i in vocab.stoi.items()}
     vocab.vocab_sz = len(vocab.itos)
     return vocab
 
@@ -216,7 +217,9 @@ def collate_fn(batch):
 
 
 def get_food101(bert_model="bert-base-uncased", datapath=None, drop_img_percent=0.0, max_seq_len=512,
-                num_image_embeds=3, batch_size=128, n_workers=20, gpu_normalize=False, device=None):
+                num_image_embeds=3, batch_size=128, n_workers=20, gpu_normalize=False, device=None, sampler=None):
+    """``sampler``: optional factory ds -> Sampler for the TRAIN split (data parallel:
+    a DistributedSampler, so every rank draws a disjoint shard; dev/test stay whole)."""
     datapath = datapath or os.environ["DATA_DIR"]
     tokenizer = bert_tokenizer(bert_model).tokenize
     labels, _ = get_labels_and_frequencies(os.path.join(datapath, "train.jsonl"))
@@ -228,12 +231,15 @@ def get_food101(bert_model="bert-base-uncased", datapath=None, drop_img_percent=
         return JsonlDataset(os.path.join(datapath, f"{split}.jsonl"), tokenizer, tf, vocab, n_classes,
                             drop_img_percent, max_seq_len, num_image_embeds, labels)
 
-    def loader(ds, shuffle):
-        dl = torch.utils.data.DataLoader(ds, batch_size=batch_size, shuffle=shuffle, num_workers=n_workers,
-                                         collate_fn=collate_fn, pin_memory=torch.cuda.is_available())
+    def loader(ds, shuffle, smp=None):
+        dl = torch.utils.data.DataLoader(ds, batch_size=batch_size, shuffle=shuffle and smp is None, sampler=smp,
+                                         num_workers=n_workers, collate_fn=collate_fn,
+                                         pin_memory=torch.cuda.is_available())
         return DevicePrefetcher(dl, device) if gpu_normalize else dl
 
-    return loader(make("train"), True), loader(make("dev"), False), loader(make("test"), False), n_classes, vocab
+    train_ds = make("train")
+    train = loader(train_ds, True, sampler(train_ds) if sampler is not None else None)
+    return train, loader(make("dev"), False), loader(make("test"), False), n_classes, vocab
 
 
 class SyntheticFood101(Dataset):

@@ -93,6 +93,38 @@ class GradBucketer:
         self.pending, self.launched, self.done_layers = [], set(), set()
 
 
+def average_buffers(model, group=None):
+    """Average the floating-point buffers (ResNet BatchNorm running_mean / running_var) over
+    the ranks.  Each rank's BatchNorm normalises over its own batch in training, so the
+    running statistics drift apart between ranks; averaging them before evaluation and
+    checkpointing gives every rank (and the rank-0 checkpoint) the same statistics, the
+    mean of what the ranks saw.  num_batches_tracked (integer) is equal on every rank."""
+    world = dist.get_world_size(group)
+    if world == 1:
+        return
+    bufs = [b for b in model.buffers() if b.is_floating_point()]
+    if not bufs:
+        return
+    flat = torch._utils._flatten_dense_tensors(bufs)
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    flat.mul_(1.0 / world)
+    for b, f in zip(bufs, torch._utils._unflatten_dense_tensors(flat, bufs)):
+        b.copy_(f)
+
+
+def sync_buffers_on_eval(model, group=None):
+    """Call average_buffers whenever the model leaves training mode (model.eval() /
+    model.train(False), as Model_.eval_loop does before validation, test and checkpoints)."""
+    train = model.train
+
+    def train_(mode=True):
+        if not mode and model.training:
+            average_buffers(model, group)
+        return train(mode)
+    model.train = train_
+    return model
+
+
 def broadcast_parameters(model, src=0, group=None):
     """Start every rank from rank 0's weights (flat buffer + BN running stats)."""
     dist.broadcast(model.store.flat, src, group=group)

@@ -38,6 +38,28 @@ def cycle(iterable):
         yield from iterable
 
 
+def _set_sampler_epoch(generator, epoch):
+    """Reshuffle a DistributedSampler per epoch (the reference's single-process DataLoader
+    reshuffles every epoch by itself; a DistributedSampler only does when told the epoch)."""
+    sampler = getattr(generator, "sampler", None)
+    if isinstance(sampler, torch.utils.data.DistributedSampler):
+        sampler.set_epoch(epoch)
+
+
+def _all_ranks_any(flag, device=None):
+    """True on every rank when any rank's flag is True (no-op without torch.distributed)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return bool(flag)
+    if dist.get_backend() != "nccl":
+        dev = torch.device("cpu")
+    else:
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return bool(t.item())
+
+
 def _get_step_iterator(steps, generator):
     if steps is None:
         return zip(itertools.count(1), generator)
@@ -196,6 +218,7 @@ class Model_:
                 freeze_img = epoch < kwargs["freeze_img"]
                 freeze_txt = epoch < kwargs["freeze_txt"]
             cbs.on_epoch_begin(epoch, {})
+            _set_sampler_epoch(train_generator, epoch)
             t_epoch = timeit.default_timer()
             it = StepIterator(train_generator, steps_per_epoch, cbs, self.metrics_names)
             self.model.train(True)
@@ -247,6 +270,11 @@ class Model_:
                 counter += 1
             if counter >= patience:
                 stopped_epoch, stop_training = epoch, True
+            # under DP each rank trains on its own shard: stop together or a rank that broke
+            # out would leave the others blocked in the next gradient all-reduce
+            stop_training = _all_ranks_any(stop_training, self.device)
+            if stop_training and stopped_epoch == 0 and counter >= patience:
+                stopped_epoch = epoch
             if stop_training:
                 break
         cbs.on_train_end({})

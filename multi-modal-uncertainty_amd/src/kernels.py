@@ -252,15 +252,30 @@ def maxpool_fwd(x, y, argmax):
     """MaxPool2d(3, 2, 1) of a channels-last bf16 [B, C, H, W] map -> y [B, C, OH, OW]
     (channels-last) and the uint8 argmax in y's NHWC layout; see mmu_maxpool_fwd."""
     _dev_check(x, y, argmax)
-    _want(x, torch.bfloat16, "maxpool x")
     B, C, H, W = x.shape
+    _maxpool_check(x, y, argmax, B, C, H, W, "x", "y")
     N.call("mmu_maxpool_fwd", _ptr(x), B, H, W, C, _ptr(y), _ptr(argmax), _stream(x))
 
 
 def maxpool_bwd(dy, argmax, dx):
     _dev_check(dy, argmax, dx)
     B, C, H, W = dx.shape
+    _maxpool_check(dx, dy, argmax, B, C, H, W, "dx", "dy")
     N.call("mmu_maxpool_bwd", _ptr(dy), _ptr(argmax), B, H, W, C, _ptr(dx), _stream(dx))
+
+
+def _maxpool_check(full, pooled, argmax, B, C, H, W, nf, np_):
+    """The kernels index raw NHWC pointers: refuse any layout / size they do not assume."""
+    oshape = (B, C, (H - 1) // 2 + 1, (W - 1) // 2 + 1)
+    for t, nm in ((full, nf), (pooled, np_)):
+        _want(t, torch.bfloat16, f"maxpool {nm}")
+        if t.dim() != 4 or not t.is_contiguous(memory_format=torch.channels_last):
+            raise N.NativeError(f"maxpool: {nm} must be a channels-last [B, C, H, W] bf16 map")
+    if tuple(pooled.shape) != oshape:
+        raise N.NativeError(f"maxpool: {np_} is {tuple(pooled.shape)}, MaxPool2d(3, 2, 1) of "
+                            f"{(B, C, H, W)} is {oshape}")
+    if argmax.dtype != torch.uint8 or argmax.numel() != pooled.numel() or not argmax.is_contiguous():
+        raise N.NativeError("maxpool: argmax must be a contiguous uint8 tensor with one entry per pooled element")
 
 
 def row_pool_fwd(fmap_nhwc, n, out):

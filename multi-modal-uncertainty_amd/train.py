@@ -183,16 +183,22 @@ def food101_data(args, rank=0, world=1):
             collate_fn=dataset.collate_fn, pin_memory=True)
         return mk(tr, True, sampler), mk(va, False), mk(te, False), 101, _Vocab()
     gpu = bool(args.gpu_normalize) and torch.cuda.is_available()
+    # data parallel: every rank draws a disjoint shard of the train split (reshuffled per
+    # epoch by Model_.train_loop); dev / test are evaluated whole on every rank
+    sampler = (lambda ds: torch.utils.data.DistributedSampler(ds, world, rank, shuffle=True, seed=args.seed)) \
+        if world > 1 else None
     return dataset.get_food101(datapath=args.datapath, batch_size=args.batch_size,
                                drop_img_percent=args.drop_img_percent, max_seq_len=args.max_seq_len,
                                num_image_embeds=args.num_image_embeds, n_workers=args.n_workers,
-                               gpu_normalize=gpu, device=torch.device("cuda", args.device) if gpu else None)
+                               gpu_normalize=gpu, device=torch.device("cuda", args.device) if gpu else None,
+                               sampler=sampler)
 
 
 def _dp_wrap(model, optimizer, accum):
     """Hook the RCCL bucketer between backward and BertAdam; all-reduce only on update micro-batches."""
-    from src.dp import GradBucketer, broadcast_parameters
+    from src.dp import GradBucketer, broadcast_parameters, sync_buffers_on_eval
     broadcast_parameters(model)
+    sync_buffers_on_eval(model)  # BatchNorm running stats averaged over ranks before eval / checkpoints
     bucketer = GradBucketer(model)
     state = {"micro": 0}
 
