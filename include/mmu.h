@@ -91,6 +91,15 @@ int mmu_colsum_reduce(const float* partial, int64_t parts, int64_t N, float* out
 int mmu_colsum_bf16(const void* X, int64_t M, int64_t N, int64_t ldx, float* partial,
                     float* out, int accumulate, mmu_stream_t stream);
 
+/* Batched bf16 transpose: for each of n_jobs jobs (a device table of 4 int64 per job:
+ * src pointer, dst pointer, rows, cols), dst[c*rows + r] = src[r*cols + c].  Keeps the
+ * K-major (transposed) bf16 copies of the BERT layer weights that the data-gradient
+ * products dX = dY.W read as their B operand (the backward of the nn.Linear layers inside
+ * pytorch_pretrained_bert BertLayer, src/mmbt.py:124-126); max_rows / max_cols bound the
+ * jobs' shapes (grid size). */
+int mmu_transpose_bf16_batched(const int64_t* jobs, int n_jobs, int64_t max_rows, int64_t max_cols,
+                               mmu_stream_t stream);
+
 /* ------------------------------------------------------------------ attention
  * softmax(Q K^T / sqrt(64) + keymask) (dropout) V for 12 x 64 heads, Q/K/V read from
  * the token-major fused projection QKV[rows, ld_qkv] (q at col h*64, k at 768+h*64,

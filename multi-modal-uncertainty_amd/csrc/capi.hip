@@ -244,6 +244,14 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
   return check_launch("mmu_gemm");
 }
 
+int mmu_transpose_bf16_batched(const int64_t* jobs, int n_jobs, int64_t max_rows, int64_t max_cols,
+                               mmu_stream_t stream) {
+  if (!jobs || n_jobs <= 0 || n_jobs > 65535 || max_rows <= 0 || max_cols <= 0)
+    return fail("mmu_transpose_bf16_batched: bad args");
+  transpose_bf16_batched_launch(jobs, n_jobs, max_rows, max_cols, (hipStream_t)stream);
+  return check_launch("mmu_transpose_bf16_batched");
+}
+
 int mmu_colsum_reduce(const float* partial, int64_t parts, int64_t N, float* out, int accumulate,
                       mmu_stream_t stream) {
   if (!partial || !out || parts <= 0 || N <= 0) return fail("mmu_colsum_reduce: bad args");

@@ -27,6 +27,24 @@ namespace mmu {
 
 constexpr int BKT = 64;
 
+// Diagnostic build only (make EXTRA=-DMMU_GEMM_STAMPS OUT=../../ab/stamps.so): wave 0 of every
+// big-kernel workgroup records s_memtime at start, after the first K-tile landed, after the
+// K loop and after the epilogue (tools/gemm_stamps.py reads them back).
+#ifdef MMU_GEMM_STAMPS
+__device__ uint64_t g_gemm_stamps[1 << 16][4];
+#define GEMM_STAMP(i)                                                                       \
+  do {                                                                                      \
+    if (threadIdx.x == 0) {                                                                 \
+      const int lin_ = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)); \
+      if (lin_ < (1 << 16)) g_gemm_stamps[lin_][i] = __builtin_amdgcn_s_memtime();          \
+    }                                                                                       \
+  } while (0)
+#else
+#define GEMM_STAMP(i) \
+  do {                \
+  } while (0)
+#endif
+
 static __device__ __forceinline__ int sw_mn(int r) { return (r & 7) ^ (((r >> 3) & 1) << 2); }
 
 // ---------------------------------------------------------------- tile order
@@ -156,10 +174,10 @@ static __device__ __forceinline__ void epi_oct(const GemmParams& p, int64_t z, i
   }
 }
 
-// the epilogue of a wave's 64*NJ/4-row x 64-col block acc[4][NJ] (n-subtile i, m-subtile j)
-// through the wave-private LDS region ws (16 KiB; the caller has passed a barrier that
-// retires every staging read of it)
-template <int EPI, bool OUT_F32, int NJ>
+// the epilogue of a wave's 16*NJ-row x 64-col block acc[4][NJ] (n-subtile i, m-subtile j)
+// through the wave-private LDS region ws (PJ * 4 KiB: passes of 16*PJ rows; the caller has
+// passed a barrier that retires every staging read of it)
+template <int EPI, bool OUT_F32, int NJ, int PJ = 4>
 static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64_t z, int slice, int64_t mw,
                                                       int64_t nw, f32x4 (&acc)[4][NJ], int l, char* ws) {
   if (nw >= p.N) return;  // (N % 128 == 0: a 64-column wave block is all in or all out)
@@ -187,28 +205,28 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
   const bf16* src = EPI == MMU_EPI_DGELU ? (const bf16*)aux : res;
   const int64_t lds_ = EPI == MMU_EPI_DGELU ? p.ldx : p.ldr;
 #pragma unroll
-  for (int pass = 0; pass < NJ / 4; ++pass) {
+  for (int pass = 0; pass < NJ / PJ; ++pass) {
     // the pass's residual / aux rows are requested up front: one memory latency per pass
-    bf16x8 in[8];
+    bf16x8 in[2 * PJ];
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
-      const int64_t m = mw + 64 * pass + rr + 8 * it;
+    for (int it = 0; it < 2 * PJ; ++it) {
+      const int64_t m = mw + 16 * PJ * pass + rr + 8 * it;
       if (LOADS && !slab && m < p.M) in[it] = *(const bf16x8*)(src + m * lds_ + n);
       else in[it] = bf16x8{};
     }
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
+    for (int jj = 0; jj < PJ; ++jj) {
       const int r = 16 * jj + (l & 15);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ch = 4 * i + (l >> 4);
-        *(f32x4*)(ws + r * 256 + ((ch ^ (r & 15)) << 4)) = acc[i][4 * pass + jj];
+        *(f32x4*)(ws + r * 256 + ((ch ^ (r & 15)) << 4)) = acc[i][PJ * pass + jj];
       }
     }
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
+    for (int it = 0; it < 2 * PJ; ++it) {
       const int r = rr + 8 * it;
-      const int64_t m = mw + 64 * pass + r;
+      const int64_t m = mw + 16 * PJ * pass + r;
       const float4 lo = *(const float4*)(ws + r * 256 + (((2 * q) ^ (r & 15)) << 4));
       const float4 hi = *(const float4*)(ws + r * 256 + (((2 * q + 1) ^ (r & 15)) << 4));
       if (m >= p.M) continue;
@@ -372,6 +390,7 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p) {
   const int wm = w >> 2, wn = w & 3;
   int tm, tn, slice;
   int64_t z;
+  GEMM_STAMP(0);
   block_tile(p, z, slice, tm, tn);
   const int64_t m0 = (int64_t)tm * BBM, n0 = (int64_t)tn * BBN;
   // operand byte ranges: rows (K-major) or k-rows (M/N-major) beyond the operand read as zero
@@ -396,6 +415,7 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p) {
   dma_tile<BKM>(smem + B_TILE, rb, p.ldb, n0, kb, w, l);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  GEMM_STAMP(1);
   for (int kt = 0; kt < nk; ++kt) {
     const char* sa = smem + (kt & 1) * B_STAGE;
     const char* sb = sa + B_TILE;
@@ -421,7 +441,139 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+  GEMM_STAMP(2);
   epilogue_block<EPI, OUT_F32, 8>(p, z, slice, m0 + 128 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
+#ifdef MMU_GEMM_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  GEMM_STAMP(3);
+}
+
+// ================================================================ persistent 256x256
+// gemm_big_kernel's tile, wave split, LDS images and K loop, but one workgroup per CU that
+// walks a list of tiles, with the 2-stage LDS-DMA pipeline running ACROSS tile boundaries:
+// the last K-step of a tile issues the first K-tile of the next one, so that tile's
+// operands are in LDS when the epilogue ends (a fresh workgroup instead waits a full
+// HBM / Infinity-Cache latency before its first MFMA), and the epilogue's stores drain
+// while the next tile's first K-step computes.  The epilogue turns its accumulators around
+// in the stage the last K-step just released (8 KiB per wave: 32-row passes); a barrier
+// after it retires those reads before the next DMA writes that stage.
+// Work list: the XCD that runs workgroup lin (lin % 8) owns a contiguous range of pids in
+// the same bijective partition xcd_remap uses, and its workgroups take that range's pids
+// round-robin, so an XCD works through consecutive (grouped) tiles as gemm_big_kernel's
+// dispatch order does.
+template <bool AK, bool BKM, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(512) void gemm_persist_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * B_STAGE];
+  const int t = threadIdx.x, l_ = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int per_z = ntiles * p.splitk;
+  const int total = per_z * p.batch;
+  const int G = (int)gridDim.x;
+  const int lin = (int)blockIdx.x, xcd = lin & 7;
+  // this XCD's pid range [xs, xe) (xcd_remap's partition of `total`) and its workgroup count
+  const int q8 = total >> 3, r8 = total & 7;
+  const int xs = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int xe = xs + (xcd < r8 ? q8 + 1 : q8);
+  const int gx = (G - xcd + 7) >> 3;
+  int pid = xs + (lin >> 3);
+  if (pid >= xe) return;
+  if (p.stagger > 0 && ((lin >> 3) & 1)) {  // A/B: half of each XCD's CUs start later (de-phase epilogues)
+    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
+  }
+
+  const int64_t a_bytes = (AK ? p.M * p.lda : p.K * p.lda) * 2;
+  const int64_t b_bytes = (BKM ? p.N * p.ldb : p.K * p.ldb) * 2;
+  struct Item {
+    int64_t z, m0, n0, kb;
+    int slice, nk;
+  };
+  auto decode = [&](int id) {
+    Item it;
+    it.z = id / per_z;
+    const int r = id - (int)it.z * per_z;
+    it.slice = r / ntiles;
+    int tm, tn;
+    tile_of(r - it.slice * ntiles, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
+    it.m0 = (int64_t)tm * BBM;
+    it.n0 = (int64_t)tn * BBN;
+    it.kb = (int64_t)it.slice * p.kchunk;
+    const int64_t ke = it.kb + p.kchunk < p.K ? it.kb + p.kchunk : p.K;
+    it.nk = (int)((ke - it.kb + BKT - 1) / BKT);
+    return it;
+  };
+  auto rsrc_a = [&](int64_t z) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + z * p.sA), 0, (int)(uint32_t)a_bytes, 0x00020000);
+  };
+  auto rsrc_b = [&](int64_t z) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(p.B + z * p.sB), 0, (int)(uint32_t)b_bytes, 0x00020000);
+  };
+
+  Item cur = decode(pid);
+  {
+    const int l = l_;
+    const __amdgpu_buffer_rsrc_t ra = rsrc_a(cur.z), rb = rsrc_b(cur.z);
+    dma_tile<AK>(smem, ra, p.lda, cur.m0, cur.kb, w, l);
+    dma_tile<BKM>(smem + B_TILE, rb, p.ldb, cur.n0, cur.kb, w, l);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int stage = 0;
+  f32x4 acc[4][8];
+  while (true) {
+    // lane-derived addresses are re-derived per tile rather than kept live across the
+    // epilogue and the loop (hoisted, they cost ~40 VGPRs and spill the M-major variants)
+    int l = l_;
+    asm volatile("" : "+v"(l));
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool has_next = pid + gx < xe;
+    for (int kt = 0; kt < cur.nk; ++kt) {
+      const char* sa = smem + stage * B_STAGE;
+      const char* sb = sa + B_TILE;
+      char* d = smem + (stage ^ 1) * B_STAGE;
+      if (kt + 1 < cur.nk) {
+        const int64_t k1 = cur.kb + (int64_t)(kt + 1) * BKT;
+        dma_tile<AK>(d, rsrc_a(cur.z), p.lda, cur.m0, k1, w, l);
+        dma_tile<BKM>(d + B_TILE, rsrc_b(cur.z), p.ldb, cur.n0, k1, w, l);
+      } else if (has_next) {  // the next tile's first K-tile
+        const Item nx = decode(pid + gx);
+        dma_tile<AK>(d, rsrc_a(nx.z), p.lda, nx.m0, nx.kb, w, l);
+        dma_tile<BKM>(d + B_TILE, rsrc_b(nx.z), p.ldb, nx.n0, nx.kb, w, l);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 fb[4], fa[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fb[i] = s_frag<BKM, 512>(sb, 64 * wn + 16 * i, ks, l);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fa[j] = s_frag<AK, 512>(sa, 128 * wm + 16 * j, ks, l);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      stage ^= 1;
+    }
+    // the stage the last K-step read is free: 8 KiB of it per wave as epilogue scratch
+    epilogue_block<EPI, OUT_F32, 8, 2>(p, cur.z, cur.slice, cur.m0 + 128 * wm, cur.n0 + 64 * wn, acc, l,
+                                       smem + (stage ^ 1) * B_STAGE + w * 8192);
+    if (!has_next) break;
+    // every wave's scratch reads are done before the next DMA into that stage (raw barrier:
+    // the epilogue's global stores need not drain here)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    pid += gx;
+    cur = decode(pid);
+  }
 }
 
 // ================================================================ pipelined 256x256 (8 phases / 2 K-tiles)
@@ -705,10 +857,36 @@ static bool use_duo() {
   return e && e[0] == '1';
 }
 
+// MMU_GEMM_PERSIST=1 selects the persistent kernel (A/B while it is evaluated)
+static bool use_persist() {
+  const char* e = getenv("MMU_GEMM_PERSIST");
+  return e && e[0] == '1';
+}
+
+static int gemm_cus() {
+  static int cache[64] = {};
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return 256;
+  if (!cache[d]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || n <= 0) n = 256;
+    cache[d] = n;
+  }
+  return cache[d];
+}
+
 template <bool AK, bool BKM, int EPI, bool F32>
 static void launch_t(const GemmParams& p, bool big, int batch, hipStream_t s) {
   dim3 grid(p.tiles_m * p.tiles_n, p.splitk, batch);
-  if (big && use_duo()) {
+  if (big && use_persist()) {
+    GemmParams q = p;
+    q.batch = batch;
+    const char* st = getenv("MMU_GEMM_STAGGER");
+    q.stagger = st ? atoi(st) : 0;
+    const int total = p.tiles_m * p.tiles_n * p.splitk * batch;
+    const int cus = gemm_cus();
+    hipLaunchKernelGGL((gemm_persist_kernel<AK, BKM, EPI, F32>), dim3(total < cus ? total : cus), dim3(512), 0, s, q);
+  } else if (big && use_duo()) {
     GemmParams q = p;
     const char* st = getenv("MMU_GEMM_STAGGER");
     q.stagger = st ? atoi(st) : 0;
@@ -918,4 +1096,60 @@ void colsum_bf16_launch(const bf16* X, int64_t M, int64_t N, int64_t ld, float* 
                      dim3(256), 0, s, X, M, N, ld, out);
 }
 
+// ------------------------------------------------------------------ batched transpose
+// one 64 x 64 tile per workgroup through LDS (row pitch 65 elements: conflict-free column
+// reads), 16-B global reads and 8-B writes; blockIdx.z = job, tiles outside a job's shape exit
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const int64_t* __restrict__ jobs) {
+  const int64_t* j = jobs + 4 * blockIdx.z;
+  const bf16* __restrict__ src = (const bf16*)j[0];
+  bf16* __restrict__ dst = (bf16*)j[1];
+  const int64_t rows = j[2], cols = j[3];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  if (r0 >= rows || c0 >= cols) return;
+  __shared__ bf16 tile[64][65];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // 64 rows x 8 octets = 512 loads of 16 B
+    const int idx = t + 256 * i, r = idx >> 3, c = (idx & 7) * 8;
+    const int64_t gr = r0 + r, gc = c0 + c;
+    if (gr < rows && gc + 8 <= cols) {
+      const bf16x8 v = *(const bf16x8*)(src + gr * cols + gc);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) tile[r][c + e] = v[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) tile[r][c + e] = (gr < rows && gc + e < cols) ? src[gr * cols + gc + e] : bf16(0.f);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // 64 dst rows (= src cols) x 16 quads of 8 B
+    const int idx = t + 256 * i, c = idx >> 4, r = (idx & 15) * 4;
+    const int64_t gc = c0 + c, gr = r0 + r;
+    if (gc >= cols) continue;
+    if (gr + 4 <= rows) {
+      bf16x4 v = {tile[r][c], tile[r + 1][c], tile[r + 2][c], tile[r + 3][c]};
+      *(bf16x4*)(dst + gc * rows + gr) = v;
+    } else {
+      for (int e = 0; e < 4; ++e)
+        if (gr + e < rows) dst[gc * rows + gr + e] = tile[r + e][c];
+    }
+  }
+}
+
+void transpose_bf16_batched_launch(const int64_t* jobs, int n_jobs, int64_t max_rows, int64_t max_cols,
+                                   hipStream_t s) {
+  hipLaunchKernelGGL(transpose_bf16_kernel,
+                     dim3((unsigned)((max_cols + 63) / 64), (unsigned)((max_rows + 63) / 64), (unsigned)n_jobs),
+                     dim3(256), 0, s, jobs);
+}
+
 }  // namespace mmu
+
+#ifdef MMU_GEMM_STAMPS
+extern "C" int mmu_debug_gemm_stamps(uint64_t* host, int blocks) {
+  if (blocks > (1 << 16)) blocks = 1 << 16;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(mmu::g_gemm_stamps), sizeof(uint64_t) * 4 * blocks, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#endif

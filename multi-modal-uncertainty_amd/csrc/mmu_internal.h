@@ -32,11 +32,14 @@ struct GemmParams {
   int64_t kchunk;
   float* ws;
   int stagger;  // duo kernel: s_sleep(127) count for the second block of each CU (A/B experiment)
+  int batch;    // batch items (the persistent kernel's 1-D grid walks tiles x slices x batch)
 };
 
 void splitk_reduce_launch(const GemmParams& p, int batch, hipStream_t s);
 void gemm_tail_launch(const GemmParams& p, bool f32out, int64_t m0, int S, const float* ws, int batch, hipStream_t s);
 void gemm_launch(const GemmParams& p, bool a_kmajor, bool b_kmajor, bool f32out, bool big, int batch, hipStream_t s);
+void transpose_bf16_batched_launch(const int64_t* jobs, int n_jobs, int64_t max_rows, int64_t max_cols,
+                                   hipStream_t s);
 void colsum_reduce_launch(const float* part, int64_t parts, int64_t N, float* out, int acc, hipStream_t s);
 void colsum_bf16_launch(const bf16* X, int64_t M, int64_t N, int64_t ld, float* part, float* out, int acc,
                         hipStream_t s);

@@ -49,6 +49,11 @@ class LayerWeights:
             setattr(self, "g_" + k, s.fused_grad(names, self._shapes[k]))
         for k in ("wqkv", "wo", "w1", "w2"):
             setattr(self, k + "16", s.fused_compute(self._names[k], self._shapes[k]))
+        # K-major copies for the data-gradient products dX = dY W (B = W^T): the GEMM's
+        # K-contiguous B path runs 9-17 % faster than its N-contiguous one on these shapes
+        # (profiles/r2_gemm_bt_ab.txt); dZ = dY2 W2 measured no faster and keeps W2 as is
+        for k in ("wqkv", "wo", "w1"):
+            setattr(self, k + "t16", s.transposed_compute(self._names[k], self._shapes[k]))
         self.anchor = s.params[self._names["wqkv"][0]]
 
     def trainable(self):
@@ -148,7 +153,7 @@ def layer_backward(lw, saved, dY, keymask, B, L, p_attn, p_hid, seeds, wgrad):
     if wgrad:
         side.run(lambda: K.gemm(dZ, FFN, False, A, HID, False, lw.g_w1, HID, FFN, HID, M, epi=acc), dZ, A)
     dA = torch.empty(M, HID, dtype=bf16, device=dev)
-    K.gemm(dZ, FFN, True, lw.w116, HID, False, dA, HID, M, HID, FFN, epi=K.epilogue(K.EPI_ADD_RES, residual=dS2))
+    K.gemm(dZ, FFN, True, lw.w1t16, FFN, True, dA, HID, M, HID, FFN, epi=K.epilogue(K.EPI_ADD_RES, residual=dS2))
     # ---- attention-output LayerNorm + dropout + Wo
     dS1 = torch.empty(M, HID, dtype=bf16, device=dev)
     dAo = torch.empty(M, HID, dtype=bf16, device=dev)
@@ -161,7 +166,7 @@ def layer_backward(lw, saved, dY, keymask, B, L, p_attn, p_hid, seeds, wgrad):
             K.gemm(dAo, HID, False, O, HID, False, lw.g_wo, HID, HID, HID, M, epi=acc)
         side.run(wo, pw1, pb1, pbias1, dAo, O)
     dO = torch.empty(M, HID, dtype=bf16, device=dev)
-    K.gemm(dAo, HID, True, lw.wo16, HID, False, dO, HID, M, HID, HID)
+    K.gemm(dAo, HID, True, lw.wot16, HID, True, dO, HID, M, HID, HID)
     # ---- attention + fused QKV
     dqkv = torch.empty(M, 3 * HID, dtype=bf16, device=dev)
     delta = torch.empty(B * HEADS, L, dtype=torch.float32, device=dev)
@@ -174,7 +179,7 @@ def layer_backward(lw, saved, dY, keymask, B, L, p_attn, p_hid, seeds, wgrad):
             K.gemm(dqkv, 3 * HID, False, X, HID, False, lw.g_wqkv, HID, 3 * HID, HID, M, epi=acc)
         side.run(wqkv, dqkv, X, dbp)
     dX = torch.empty(M, HID, dtype=bf16, device=dev)
-    K.gemm(dqkv, 3 * HID, True, lw.wqkv16, HID, False, dX, HID, M, HID, 3 * HID,
+    K.gemm(dqkv, 3 * HID, True, lw.wqkvt16, 3 * HID, True, dX, HID, M, HID, 3 * HID,
            epi=K.epilogue(K.EPI_ADD_RES, residual=dS1))
     return dX, side
 

@@ -169,6 +169,7 @@ class BertAdam(torch.optim.Optimizer):
         K.bertadam_step(st.flat, st.grad, f["m"], f["v"], st.compute, f["table"], f["steps"], len(f["names"]),
                         f["n_chunks"], lr_decay, lr_nodecay, wd, g0["warmup"], t_total, g0["b1"], g0["b2"], g0["e"],
                         g0["max_grad_norm"], f["ws"])
+        st.sync_transposed()  # the K-major bf16 weight copies the data-gradient GEMMs read
         self._host_steps_valid = False
 
     def _step_generic(self):

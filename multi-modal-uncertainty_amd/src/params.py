@@ -8,7 +8,10 @@ layer4..stem).  This gives:
   * contiguous reverse-layer gradient buckets for the RCCL all-reduce (src/dp.py);
   * fused views (Q|K|V weight [2304,768], bias [2304]) the kernels read directly;
   * bf16 copies of every GEMM weight, written by the optimizer kernel, resynced
-    only when the f32 masters were changed elsewhere (load_state_dict, .to()).
+    only when the f32 masters were changed elsewhere (load_state_dict, .to());
+  * transposed (K-major) bf16 copies of registered fused weights (the BERT layer
+    matrices: the data-gradient GEMMs read them as a K-major B operand), refreshed by
+    one batched transpose launch after every write of the bf16 copies.
 Module names / shapes are untouched, so state_dict keys stay the reference's.
 """
 import weakref
@@ -28,6 +31,9 @@ class ParamStore:
         self.flat = self.grad = self.compute = None
         self.offsets, self.coffsets = {}, {}
         self._versions = None
+        self._tspecs = {}  # key (tuple of names) -> shape [rows, cols] of the fused compute view
+        self._tcopies = {}
+        self._tjobs = None
         self.build()
         STORES.add(self)
 
@@ -68,6 +74,9 @@ class ParamStore:
         for n in self.compute_names:
             self.coffsets[n] = off
             off += self.params[n].numel()
+        self._tcopies, self._tjobs = {}, None  # re-allocated on the (new) device
+        for key, shape in self._tspecs.items():
+            self._alloc_transposed(key, shape)
         self.sync_compute()
 
     @property
@@ -103,6 +112,41 @@ class ParamStore:
                 raise RuntimeError(f"ParamStore: compute copies of {names} are not contiguous")
             tot += self.params[n].numel()
         return self.compute[c0:c0 + tot].view(shape)
+
+    def transposed_compute(self, names, shape):
+        """bf16 [cols, rows] copy of the fused compute view ``names`` ([rows, cols]), kept in
+        step with the bf16 copies (sync_compute, and sync_transposed after the optimizer)."""
+        key = tuple(names)
+        if key not in self._tspecs:
+            self._tspecs[key] = tuple(shape)
+            self._alloc_transposed(key, shape)
+            self.sync_transposed()
+        return self._tcopies[key]
+
+    def _alloc_transposed(self, key, shape):
+        rows, cols = shape
+        self._tcopies[key] = torch.empty(cols, rows, dtype=torch.bfloat16, device=self.compute.device)
+        self._tjobs = None
+
+    def sync_transposed(self):
+        """Refresh every transposed copy from the bf16 copies: ONE batched HIP launch."""
+        if not self._tcopies:
+            return
+        if self._tjobs is None:
+            rows = []
+            for key, dst in self._tcopies.items():
+                r, c = self._tspecs[key]
+                src = self.fused_compute(list(key), (r, c))
+                rows.append([src.data_ptr(), dst.data_ptr(), r, c])
+            self._tjobs = (torch.tensor(rows, dtype=torch.int64).to(self.compute.device), len(rows),
+                           max(r[2] for r in rows), max(r[3] for r in rows))
+        if self.compute.device.type != "cuda":
+            for key, dst in self._tcopies.items():  # host-side stores (CPU tests): plain copy
+                dst.copy_(self.fused_compute(list(key), self._tspecs[key]).t())
+            return
+        from . import kernels as K
+        jobs, n, mr, mc = self._tjobs
+        K.transpose_bf16_batched(jobs, n, mr, mc, self.compute)
 
     def grad_of(self, name):
         return self._shaped(self.grad, self.offsets[name], self.params[name])
@@ -146,6 +190,7 @@ class ParamStore:
                 c, o, k = self.coffsets[n], self.offsets[n], self.params[n].numel()
                 self.compute[c:c + k].copy_(self.flat[o:o + k])
         self._versions = self._current_versions()
+        self.sync_transposed()
 
     def compute_of(self, name):
         """bf16 copy of one tensor, shaped like the parameter (conv weights channels-last)."""

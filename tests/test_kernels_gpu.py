@@ -142,6 +142,21 @@ def test_gemm_big_tiles_epilogues(dev):
     assert torch.equal(out, out2)
 
 
+def test_transpose_bf16_batched(dev):
+    """mmu_transpose_bf16_batched: several jobs of different (ragged) shapes in one launch,
+    bit-exact against torch's transpose; bytes outside each destination untouched."""
+    k = K()
+    shapes = [(2304, 768), (768, 3072), (100, 70), (65, 129), (1, 8)]
+    srcs = [rnd(r, c, dev=dev, seed=70 + i) for i, (r, c) in enumerate(shapes)]
+    dsts = [torch.full((c + 1, r), 5.0, dtype=torch.bfloat16, device=dev) for r, c in shapes]  # +1 guard row
+    jobs = torch.tensor([[s_.data_ptr(), d.data_ptr(), r, c] for s_, d, (r, c) in zip(srcs, dsts, shapes)],
+                        dtype=torch.int64).to(dev)
+    k.transpose_bf16_batched(jobs, len(shapes), max(r for r, _ in shapes), max(c for _, c in shapes), srcs[0])
+    for s_, d, (r, c) in zip(srcs, dsts, shapes):
+        assert torch.equal(d[:c], s_.t()), (r, c)
+        assert (d[c:] == 5.0).all(), "wrote past the destination"
+
+
 @pytest.mark.parametrize("Kd", [256, 768])
 def test_gemm_split_k_tail(dev, Kd, monkeypatch):
     """M = 257 tile rows x 3 column tiles = 771 tiles: the partial last wave (3 tiles) runs as a

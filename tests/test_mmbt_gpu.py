@@ -145,6 +145,10 @@ def test_bertadam_fused_matches_restatement_on_model(dev, small):
     assert set(next(iter(sd_opt["state"].values())).keys()) == {"step", "next_m", "next_v"}
     for n, p in named:
         torch.testing.assert_close(opt.state[p]["next_m"].cpu(), ref_m[n], rtol=1e-4, atol=1e-7)
+    # the K-major bf16 weight copies the data-gradient GEMMs read follow the optimizer's bf16 copies
+    for lw in model.enc._lw:
+        for k in ("wqkv", "wo", "w1"):
+            assert torch.equal(getattr(lw, k + "t16"), getattr(lw, k + "16").t()), k
 
 
 def test_freeze_skips_weight_grads(dev):

@@ -66,6 +66,7 @@ def main():
     Hh = rnd(M, FFN)
     dY, dqkv, dZ = rnd(M, HID), rnd(M, 3 * HID), rnd(M, FFN)
     Wqkv, Wo, W1, W2 = rnd(3 * HID, HID), rnd(HID, HID), rnd(FFN, HID), rnd(HID, FFN)
+    Wqkvt, Wot, W1t, W2t = (w.t().contiguous() for w in (Wqkv, Wo, W1, W2))
     bqkv, bo, b1 = (torch.randn(n, device=dev) for n in (3 * HID, HID, FFN))
     out768, out2304, out3072 = (torch.empty(M, n, dtype=bf, device=dev) for n in (HID, 3 * HID, FFN))
     Zs = rnd(M, FFN)
@@ -102,6 +103,22 @@ def main():
          lambda: torch.matmul(dqkv, Wqkv)),
         ("bwd dO   store", M, HID, HID,
          lambda: K.gemm(dY, HID, True, Wo, HID, False, out768, HID, M, HID, HID),
+         lambda: torch.matmul(dY, Wo)),
+        # the same data-grad products with a K-major (transposed) copy of the weight as B
+        ("bwd dZ   B=W2^T kmaj", M, FFN, HID,
+         lambda: K.gemm(dY, HID, True, W2t, HID, True, out3072, FFN, M, FFN, HID,
+                        epi=K.epilogue(K.EPI_DGELU, aux=Zs, colsum=cs)),
+         lambda: torch.matmul(dY, W2)),
+        ("bwd dA   B=W1^T kmaj", M, HID, FFN,
+         lambda: K.gemm(dZ, FFN, True, W1t, FFN, True, out768, HID, M, HID, FFN,
+                        epi=K.epilogue(K.EPI_ADD_RES, residual=dY)),
+         lambda: torch.matmul(dZ, W1)),
+        ("bwd dX   B=Wqkv^T kmaj", M, HID, 3 * HID,
+         lambda: K.gemm(dqkv, 3 * HID, True, Wqkvt, 3 * HID, True, out768, HID, M, HID, 3 * HID,
+                        epi=K.epilogue(K.EPI_ADD_RES, residual=dY)),
+         lambda: torch.matmul(dqkv, Wqkv)),
+        ("bwd dO   B=Wo^T kmaj", M, HID, HID,
+         lambda: K.gemm(dY, HID, True, Wot, HID, True, out768, HID, M, HID, HID),
          lambda: torch.matmul(dY, Wo)),
         ("wgrad W1 dZ^T.A f32acc", FFN, HID, M,
          lambda: K.gemm(dZ, FFN, False, A, HID, False, gW, HID, FFN, HID, M,
