@@ -235,6 +235,8 @@ int mmu_row_pool_bwd(const float* dout, int64_t B, int64_t Hh, int64_t Ww, int64
  *   with momentum (unbiased variance), *num_batches_tracked += 1 (each may be NULL),
  *   save_mean / save_invstd [C] f32 written for the backward.
  * eval: running statistics.  weight / bias may be NULL (affine = False).
+ * relu_mask (may be NULL; needs relu): [rows, C/8] u8 written with bit e of byte (r, c/8)
+ *   = Y[r, c+e] > 0, for the backward to read instead of Y (1/16 of its bytes).
  * ws: device scratch of >= mmu_batchnorm_ws_bytes(C) bytes (per-block partial sums +
  * per-channel coefficients, ~8 MiB), 16-B aligned.
  */
@@ -242,12 +244,14 @@ int64_t mmu_batchnorm_ws_bytes(int64_t C);
 int mmu_batchnorm_fwd(const void* X, const void* skip, void* Y, int64_t rows, int64_t C,
                       const float* weight, const float* bias, float* running_mean, float* running_var,
                       int64_t* num_batches_tracked, int training, float momentum, float eps, int relu,
-                      float* save_mean, float* save_invstd, void* ws, int64_t ws_bytes, mmu_stream_t stream);
-/* Training-mode backward.  g = dY * [Y > 0] when relu (Y = the forward's output), else dY;
+                      float* save_mean, float* save_invstd, void* relu_mask, void* ws, int64_t ws_bytes,
+                      mmu_stream_t stream);
+/* Training-mode backward.  g = dY * [Y > 0] when relu, from relu_mask when given (the
+ * forward's mask), else from Y (the forward's output); g = dY without relu;
  * dX [rows, C] bf16; dSkip (may be NULL) = g, the gradient of the residual input;
  * dweight / dbias (may be NULL) f32 [C] are ACCUMULATED (+=). */
-int mmu_batchnorm_bwd(const void* dY, const void* Y, const void* X, int64_t rows, int64_t C,
-                      const float* weight, const float* save_mean, const float* save_invstd, int relu,
+int mmu_batchnorm_bwd(const void* dY, const void* Y, const void* relu_mask, const void* X, int64_t rows,
+                      int64_t C, const float* weight, const float* save_mean, const float* save_invstd, int relu,
                       void* dX, void* dSkip, float* dweight, float* dbias, void* ws, int64_t ws_bytes,
                       mmu_stream_t stream);
 

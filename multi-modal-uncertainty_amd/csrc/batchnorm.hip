@@ -7,10 +7,14 @@
 //   forward  (train): stats pass (read X)            -> per-block f32 sum / sum of squares
 //                     finalize (per channel, f64)    -> scale, shift, running stats, mean/invstd
 //                     apply pass (read X [+skip])    -> Y = act(X*scale + shift [+ skip])
+//                                                       [+ ReLU mask: one bit per element, Y > 0]
 //   forward  (eval):  finalize from running stats    -> apply pass
-//   backward:         reduce pass (read dY, Y, X)    -> per-block sum(g), sum(g*(x-mean)), g = dY*[Y>0]
+//   backward:         reduce pass (read dY, M, X)    -> per-block sum(g), sum(g*(x-mean)), g = dY*[Y>0]
 //                     finalize                       -> dgamma, dbeta (accumulated), dx coefficients
-//                     apply pass (read dY, Y, X)     -> dX = k1*g + k2*x + k0  [, dSkip = g]
+//                     apply pass (read dY, M, X)     -> dX = k1*g + k2*x + k0  [, dSkip = g]
+// The ReLU mask M ([rows][C/8] bytes, bit e of byte (r, c/8) = Y[r][c+e] > 0) replaces the
+// backward's two reads of Y (2 B per element each) by two 1/8-B reads: the backward moves
+// 10.25 instead of 14 B per element (without a mask it reads Y itself).
 // Semantics of torch.nn.BatchNorm2d in training mode: biased variance normalises, the
 // running variance is updated with the unbiased one, momentum-weighted.
 //
@@ -157,10 +161,11 @@ __global__ __launch_bounds__(BN_THREADS) void bn_fwd_finalize_kernel(
   }
 }
 
-template <bool SKIP, bool RELU>
+template <bool SKIP, bool RELU, bool MASK>
 __global__ __launch_bounds__(BN_THREADS) void bn_apply_kernel(const bf16* __restrict__ X, const bf16* __restrict__ S,
                                                                bf16* __restrict__ Y, int64_t rows, int C, int CH,
-                                                               int64_t rows_per_blk, const float* __restrict__ coef) {
+                                                               int64_t rows_per_blk, const float* __restrict__ coef,
+                                                               uint8_t* __restrict__ M) {
   const BnGeom g = bn_geom(CH, rows, rows_per_blk);
   if (g.rs >= g.rpi) return;
   float sc[8], sh[8];
@@ -177,21 +182,44 @@ __global__ __launch_bounds__(BN_THREADS) void bn_apply_kernel(const bf16* __rest
     bf16x8 sk;
     if (SKIP) sk = *(const bf16x8*)(S + o);
     bf16x8 y;
+    uint32_t bits = 0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float v = fmaf(bf2f(x[e]), sc[e], sh[e]);
       if (SKIP) v += bf2f(sk[e]);
       if (RELU) v = fmaxf(v, 0.f);
       y[e] = f2bf(v);
+      if (MASK) bits |= (bf2f(y[e]) > 0.f ? 1u : 0u) << e;
     }
     *(bf16x8*)(Y + o) = y;
+    if (MASK) M[o >> 3] = (uint8_t)bits;
+  }
+}
+
+// g = dY * [Y > 0] from the ReLU mask byte (MASK), from Y (RELU only), or dY
+template <bool RELU, bool MASK>
+static __device__ __forceinline__ void bn_relu_grad(const bf16* __restrict__ dY, const bf16* __restrict__ Y,
+                                                    const uint8_t* __restrict__ M, int64_t o, float (&gv)[8]) {
+  const bf16x8 dy = *(const bf16x8*)(dY + o);
+  if (RELU && MASK) {
+    const uint32_t bits = M[o >> 3];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gv[e] = ((bits >> e) & 1u) ? bf2f(dy[e]) : 0.f;
+  } else if (RELU) {
+    const bf16x8 y = *(const bf16x8*)(Y + o);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gv[e] = bf2f(y[e]) > 0.f ? bf2f(dy[e]) : 0.f;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gv[e] = bf2f(dy[e]);
   }
 }
 
 // backward reduce: part = {sum g, sum g*(x-mean)},  g = dY * [Y > 0] (RELU)
-template <bool RELU>
+template <bool RELU, bool MASK>
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_reduce_kernel(const bf16* __restrict__ dY,
                                                                     const bf16* __restrict__ Y,
+                                                                    const uint8_t* __restrict__ M,
                                                                     const bf16* __restrict__ X, int64_t rows, int C,
                                                                     int CH, int64_t rows_per_blk,
                                                                     const float* __restrict__ smean,
@@ -206,15 +234,13 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_reduce_kernel(const bf16* _
 #pragma unroll 4
     for (int64_t r = g.r0 + g.rs; r < g.r1; r += g.rpi) {
       const int64_t o = r * C + g.c0;
-      const bf16x8 dy = *(const bf16x8*)(dY + o), x = *(const bf16x8*)(X + o);
-      bf16x8 y;
-      if (RELU) y = *(const bf16x8*)(Y + o);
+      const bf16x8 x = *(const bf16x8*)(X + o);
+      float gv[8];
+      bn_relu_grad<RELU, MASK>(dY, Y, M, o, gv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float gv = bf2f(dy[e]);
-        if (RELU && !(bf2f(y[e]) > 0.f)) gv = 0.f;
-        s[e] += gv;
-        q[e] = fmaf(gv, bf2f(x[e]) - mu[e], q[e]);
+        s[e] += gv[e];
+        q[e] = fmaf(gv[e], bf2f(x[e]) - mu[e], q[e]);
       }
     }
   }
@@ -241,9 +267,10 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_finalize_kernel(const float
   if (db) db[c] += (float)dbeta;
 }
 
-template <bool RELU, bool DSKIP>
+template <bool RELU, bool MASK, bool DSKIP>
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_kernel(const bf16* __restrict__ dY,
                                                                    const bf16* __restrict__ Y,
+                                                                   const uint8_t* __restrict__ M,
                                                                    const bf16* __restrict__ X, int64_t rows, int C,
                                                                    int CH, int64_t rows_per_blk,
                                                                    const float* __restrict__ coef,
@@ -260,16 +287,14 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_kernel(const bf16* __
 #pragma unroll 4
   for (int64_t r = g.r0 + g.rs; r < g.r1; r += g.rpi) {
     const int64_t o = r * C + g.c0;
-    const bf16x8 dy = *(const bf16x8*)(dY + o), x = *(const bf16x8*)(X + o);
-    bf16x8 y;
-    if (RELU) y = *(const bf16x8*)(Y + o);
+    const bf16x8 x = *(const bf16x8*)(X + o);
+    float gv[8];
+    bn_relu_grad<RELU, MASK>(dY, Y, M, o, gv);
     bf16x8 dx, gs;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float gv = bf2f(dy[e]);
-      if (RELU && !(bf2f(y[e]) > 0.f)) gv = 0.f;
-      dx[e] = f2bf(fmaf(k1[e], gv, fmaf(k2[e], bf2f(x[e]), k0[e])));
-      gs[e] = f2bf(gv);
+      dx[e] = f2bf(fmaf(k1[e], gv[e], fmaf(k2[e], bf2f(x[e]), k0[e])));
+      gs[e] = f2bf(gv[e]);
     }
     *(bf16x8*)(dX + o) = dx;
     if (DSKIP) *(bf16x8*)(dS + o) = gs;
@@ -320,14 +345,16 @@ void batchnorm_fwd_launch(const BnFwdParams& q, hipStream_t s) {
     hipLaunchKernelGGL(bn_stats_kernel, G.grid, dim3(BN_THREADS), 0, s, q.X, q.rows, q.C, G.CH, G.rpb, part);
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((q.C + BN_FIN_CH - 1) / BN_FIN_CH), dim3(BN_THREADS), 0, s, part, nparts, q.rows, q.C,
                      q.w, q.b, q.rmean, q.rvar, q.training, q.momentum, q.eps, q.smean, q.sinvstd, q.nbt, coef);
-  const bool sk = q.skip != nullptr;
-#define BN_APPLY(SK, RL)                                                                                    \
-  hipLaunchKernelGGL((bn_apply_kernel<SK, RL>), G.grid, dim3(BN_THREADS), 0, s, q.X, q.skip, q.Y, q.rows, q.C, \
-                     G.CH, G.rpb, coef)
-  if (sk && q.relu) BN_APPLY(true, true);
-  else if (sk) BN_APPLY(true, false);
-  else if (q.relu) BN_APPLY(false, true);
-  else BN_APPLY(false, false);
+  const bool sk = q.skip != nullptr, mk = q.relu && q.mask != nullptr;
+#define BN_APPLY(SK, RL, MK)                                                                                    \
+  hipLaunchKernelGGL((bn_apply_kernel<SK, RL, MK>), G.grid, dim3(BN_THREADS), 0, s, q.X, q.skip, q.Y, q.rows, q.C, \
+                     G.CH, G.rpb, coef, q.mask)
+  if (sk && mk) BN_APPLY(true, true, true);
+  else if (sk && q.relu) BN_APPLY(true, true, false);
+  else if (sk) BN_APPLY(true, false, false);
+  else if (mk) BN_APPLY(false, true, true);
+  else if (q.relu) BN_APPLY(false, true, false);
+  else BN_APPLY(false, false, false);
 #undef BN_APPLY
 }
 
@@ -336,22 +363,26 @@ void batchnorm_bwd_launch(const BnBwdParams& q, hipStream_t s) {
   const int nparts = (int)G.grid.x;
   float* coef = (float*)q.ws;
   float2* part = (float2*)(coef + ((3 * q.C + 3) & ~3));
-  if (q.relu)
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true>), G.grid, dim3(BN_THREADS), 0, s, q.dY, q.Y, q.X, q.rows, q.C, G.CH,
-                       G.rpb, q.smean, part);
-  else
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false>), G.grid, dim3(BN_THREADS), 0, s, q.dY, q.Y, q.X, q.rows, q.C,
-                       G.CH, G.rpb, q.smean, part);
+  const bool mk = q.relu && q.mask != nullptr;
+#define BN_BREDUCE(RL, MK)                                                                                   \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<RL, MK>), G.grid, dim3(BN_THREADS), 0, s, q.dY, q.Y, q.mask, q.X, \
+                     q.rows, q.C, G.CH, G.rpb, q.smean, part)
+  if (mk) BN_BREDUCE(true, true);
+  else if (q.relu) BN_BREDUCE(true, false);
+  else BN_BREDUCE(false, false);
+#undef BN_BREDUCE
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((q.C + BN_FIN_CH - 1) / BN_FIN_CH), dim3(BN_THREADS), 0, s, part, nparts, q.rows, q.C,
                      q.w, q.smean, q.sinvstd, q.dw, q.db, coef);
   const bool ds = q.dS != nullptr;
-#define BN_BAPPLY(RL, DS)                                                                                     \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<RL, DS>), G.grid, dim3(BN_THREADS), 0, s, q.dY, q.Y, q.X, q.rows, q.C, \
-                     G.CH, G.rpb, coef, q.dX, q.dS)
-  if (q.relu && ds) BN_BAPPLY(true, true);
-  else if (q.relu) BN_BAPPLY(true, false);
-  else if (ds) BN_BAPPLY(false, true);
-  else BN_BAPPLY(false, false);
+#define BN_BAPPLY(RL, MK, DS)                                                                                     \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<RL, MK, DS>), G.grid, dim3(BN_THREADS), 0, s, q.dY, q.Y, q.mask, q.X,  \
+                     q.rows, q.C, G.CH, G.rpb, coef, q.dX, q.dS)
+  if (mk && ds) BN_BAPPLY(true, true, true);
+  else if (mk) BN_BAPPLY(true, true, false);
+  else if (q.relu && ds) BN_BAPPLY(true, false, true);
+  else if (q.relu) BN_BAPPLY(true, false, false);
+  else if (ds) BN_BAPPLY(false, false, true);
+  else BN_BAPPLY(false, false, false);
 #undef BN_BAPPLY
 }
 

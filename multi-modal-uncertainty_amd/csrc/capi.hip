@@ -479,8 +479,9 @@ static int bn_common(int64_t rows, int64_t C, void* ws, int64_t ws_bytes, const 
 int mmu_batchnorm_fwd(const void* X, const void* skip, void* Y, int64_t rows, int64_t C, const float* weight,
                       const float* bias, float* running_mean, float* running_var, int64_t* num_batches_tracked,
                       int training, float momentum, float eps, int relu, float* save_mean, float* save_invstd,
-                      void* ws, int64_t ws_bytes, mmu_stream_t stream) {
+                      void* relu_mask, void* ws, int64_t ws_bytes, mmu_stream_t stream) {
   if (!X || !Y) return fail("mmu_batchnorm_fwd: null pointer");
+  if (relu_mask && !relu) return fail("mmu_batchnorm_fwd: relu_mask needs relu");
   if (bn_common(rows, C, ws, ws_bytes, "mmu_batchnorm_fwd")) return 1;
   if ((running_mean == nullptr) != (running_var == nullptr))
     return fail("mmu_batchnorm_fwd: running_mean / running_var must both be given or NULL");
@@ -492,21 +493,21 @@ int mmu_batchnorm_fwd(const void* X, const void* skip, void* Y, int64_t rows, in
   q.X = (const bf16*)X; q.skip = (const bf16*)skip; q.Y = (bf16*)Y; q.rows = rows; q.C = (int)C;
   q.w = weight; q.b = bias; q.rmean = running_mean; q.rvar = running_var; q.nbt = num_batches_tracked;
   q.training = training; q.relu = relu; q.momentum = momentum; q.eps = eps;
-  q.smean = save_mean; q.sinvstd = save_invstd; q.ws = ws;
+  q.smean = save_mean; q.sinvstd = save_invstd; q.ws = ws; q.mask = (uint8_t*)relu_mask;
   batchnorm_fwd_launch(q, (hipStream_t)stream);
   return check_launch("mmu_batchnorm_fwd");
 }
 
-int mmu_batchnorm_bwd(const void* dY, const void* Y, const void* X, int64_t rows, int64_t C, const float* weight,
-                      const float* save_mean, const float* save_invstd, int relu, void* dX, void* dSkip,
-                      float* dweight, float* dbias, void* ws, int64_t ws_bytes, mmu_stream_t stream) {
+int mmu_batchnorm_bwd(const void* dY, const void* Y, const void* relu_mask, const void* X, int64_t rows, int64_t C,
+                      const float* weight, const float* save_mean, const float* save_invstd, int relu, void* dX,
+                      void* dSkip, float* dweight, float* dbias, void* ws, int64_t ws_bytes, mmu_stream_t stream) {
   if (!dY || !X || !dX || !save_mean || !save_invstd) return fail("mmu_batchnorm_bwd: null pointer");
-  if (relu && !Y) return fail("mmu_batchnorm_bwd: relu needs the forward output Y");
+  if (relu && !Y && !relu_mask) return fail("mmu_batchnorm_bwd: relu needs the forward output Y or its relu_mask");
   if (bn_common(rows, C, ws, ws_bytes, "mmu_batchnorm_bwd")) return 1;
   BnBwdParams q{};
   q.dY = (const bf16*)dY; q.Y = (const bf16*)Y; q.X = (const bf16*)X; q.rows = rows; q.C = (int)C; q.w = weight;
   q.smean = save_mean; q.sinvstd = save_invstd; q.relu = relu; q.dX = (bf16*)dX; q.dS = (bf16*)dSkip;
-  q.dw = dweight; q.db = dbias; q.ws = ws;
+  q.dw = dweight; q.db = dbias; q.ws = ws; q.mask = (const uint8_t*)relu_mask;
   batchnorm_bwd_launch(q, (hipStream_t)stream);
   return check_launch("mmu_batchnorm_bwd");
 }

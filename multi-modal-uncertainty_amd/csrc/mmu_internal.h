@@ -146,6 +146,7 @@ struct BnFwdParams {
   float *smean, *sinvstd;
   int64_t* nbt;
   void* ws;
+  uint8_t* mask;  // optional ReLU mask out ([rows][C/8] bytes, bit = Y > 0)
 };
 void batchnorm_fwd_launch(const BnFwdParams& q, hipStream_t s);
 struct BnBwdParams {
@@ -157,6 +158,7 @@ struct BnBwdParams {
   bf16 *dX, *dS;
   float *dw, *db;
   void* ws;
+  const uint8_t* mask;  // optional ReLU mask (read instead of Y)
 };
 void batchnorm_bwd_launch(const BnBwdParams& q, hipStream_t s);
 int64_t batchnorm_ws_bytes(int64_t C);

@@ -60,9 +60,9 @@ SIGNATURES = {
     "mmu_row_pool_bwd": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "mmu_batchnorm_ws_bytes": (c_i64, [c_i64]),
     "mmu_batchnorm_fwd": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_f32,
-                                  c_f32, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp]),
-    "mmu_batchnorm_bwd": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp,
-                                  c_vp, c_vp, c_i64, c_vp]),
+                                  c_f32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "mmu_batchnorm_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp,
+                                  c_vp, c_vp, c_vp, c_i64, c_vp]),
     "mmu_bertadam_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32,
                                   c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_i64, c_vp]),
     "mmu_uncertainty": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),

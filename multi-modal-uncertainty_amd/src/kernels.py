@@ -312,25 +312,41 @@ def _bn_workspace(dev):
     return t
 
 
+def _bn_mask_check(mask, X, what):
+    if mask is None:
+        return
+    C = X.shape[1]
+    if mask.dtype != torch.uint8 or not mask.is_contiguous() or mask.numel() != X.numel() // 8 or C % 8:
+        raise N.NativeError(f"{what}: relu_mask must be contiguous uint8 with numel = X.numel() / 8 "
+                            f"(got {tuple(mask.shape)} {mask.dtype} for X {tuple(X.shape)})")
+    _dev_check(mask, X)
+
+
 def batchnorm_fwd(X, Y, weight, bias, running_mean, running_var, training, momentum, eps, relu=False, skip=None,
-                  num_batches_tracked=None, save_mean=None, save_invstd=None):
-    """X, Y, skip: channels-last bf16 [N, C, H, W] (contiguous as [N*H*W, C])."""
+                  num_batches_tracked=None, save_mean=None, save_invstd=None, relu_mask=None):
+    """X, Y, skip: channels-last bf16 [N, C, H, W] (contiguous as [N*H*W, C]).  relu_mask
+    (optional, relu only): uint8 [N*H*W*C/8] written with the bits Y > 0 for batchnorm_bwd."""
     _dev_check(X, Y)
     _want(X, torch.bfloat16, "batchnorm X")
+    _bn_mask_check(relu_mask, X, "batchnorm_fwd")
     C = X.shape[1]
     rows = X.numel() // C
     ws = _bn_workspace(X.device)
     N.call("mmu_batchnorm_fwd", _ptr(X), _ptr(skip), _ptr(Y), rows, C, _ptr(weight), _ptr(bias), _ptr(running_mean),
            _ptr(running_var), _ptr(num_batches_tracked), int(bool(training)), float(momentum), float(eps),
-           int(bool(relu)), _ptr(save_mean), _ptr(save_invstd), _ptr(ws), ws.numel() * 4, _stream(X))
+           int(bool(relu)), _ptr(save_mean), _ptr(save_invstd), _ptr(relu_mask), _ptr(ws), ws.numel() * 4,
+           _stream(X))
 
 
-def batchnorm_bwd(dY, Y, X, weight, save_mean, save_invstd, relu, dX, dSkip=None, dweight=None, dbias=None):
+def batchnorm_bwd(dY, Y, X, weight, save_mean, save_invstd, relu, dX, dSkip=None, dweight=None, dbias=None,
+                  relu_mask=None):
+    """relu: g = dY * [Y > 0] from relu_mask (batchnorm_fwd's) when given, else from Y."""
     _dev_check(dY, X, dX)
+    _bn_mask_check(relu_mask, X, "batchnorm_bwd")
     C = X.shape[1]
     rows = X.numel() // C
     ws = _bn_workspace(X.device)
-    N.call("mmu_batchnorm_bwd", _ptr(dY), _ptr(Y), _ptr(X), rows, C, _ptr(weight), _ptr(save_mean),
+    N.call("mmu_batchnorm_bwd", _ptr(dY), _ptr(Y), _ptr(relu_mask), _ptr(X), rows, C, _ptr(weight), _ptr(save_mean),
            _ptr(save_invstd), int(bool(relu)), _ptr(dX), _ptr(dSkip), _ptr(dweight), _ptr(dbias), _ptr(ws),
            ws.numel() * 4, _stream(X))
 

@@ -28,15 +28,18 @@ class _BatchNormAct(torch.autograd.Function):
         C = x.shape[1]
         smean = torch.empty(C, dtype=torch.float32, device=x.device)
         sinv = torch.empty_like(smean)
+        # the backward reads the ReLU mask (1 bit per element) instead of Y (16 bits)
+        mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device) if relu else None
         K.batchnorm_fwd(x, Y, weight, bias, bn.running_mean, bn.running_var, True, bn.momentum, bn.eps, relu=relu,
-                        skip=skip, num_batches_tracked=bn.num_batches_tracked, save_mean=smean, save_invstd=sinv)
-        ctx.save_for_backward(x, Y, weight, smean, sinv)
+                        skip=skip, num_batches_tracked=bn.num_batches_tracked, save_mean=smean, save_invstd=sinv,
+                        relu_mask=mask)
+        ctx.save_for_backward(x, mask, weight, smean, sinv)
         ctx.relu, ctx.has_skip = relu, skip is not None
         return Y
 
     @staticmethod
     def backward(ctx, dY):
-        x, Y, weight, smean, sinv = ctx.saved_tensors
+        x, mask, weight, smean, sinv = ctx.saved_tensors
         dY = dY.contiguous(memory_format=torch.channels_last)
         dX = torch.empty_like(x)
         dS = torch.empty_like(x) if ctx.has_skip and ctx.needs_input_grad[3] else None
@@ -47,7 +50,7 @@ class _BatchNormAct(torch.autograd.Function):
         if want_b:
             bias = ctx.bias_ref
             db = bias.grad if bias.grad is not None else torch.zeros_like(bias)
-        K.batchnorm_bwd(dY, Y if ctx.relu else None, x, weight, smean, sinv, ctx.relu, dX, dS, dw, db)
+        K.batchnorm_bwd(dY, None, x, weight, smean, sinv, ctx.relu, dX, dS, dw, db, relu_mask=mask)
         rw = dw if (want_w and weight.grad is None) else None
         rb = db if (want_b and ctx.bias_ref.grad is None) else None
         if ctx.sink is not None and dS is not None:  # conv1's dX GEMM adds it (EPI_ADD_RES)

@@ -542,6 +542,22 @@ def test_batchnorm_train_fwd_bwd(dev, N, C, H, W, skip, relu):
     dw = torch.full((C,), 0.25, device=dev)  # accumulated into
     db = torch.full((C,), -0.5, device=dev)
     k.batchnorm_bwd(dY, Y if relu else None, x, w, sm, si, relu, dX, dS, dw, db)
+    if relu:  # the ReLU-mask path: the forward's bit mask instead of Y, bit-identical results
+        mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=dev)
+        Y2 = torch.empty_like(x)
+        rm2, rv2 = rm0.clone(), rv0.clone()
+        k.batchnorm_fwd(x, Y2, w, b, rm2, rv2, True, 0.1, 1e-5, relu=relu, skip=s, relu_mask=mask,
+                        save_mean=torch.empty_like(sm), save_invstd=torch.empty_like(si))
+        assert torch.equal(Y2, Y)
+        bits = ((Y.permute(0, 2, 3, 1).reshape(-1, 8).float() > 0).to(torch.int32)
+                << torch.arange(8, device=dev, dtype=torch.int32)).sum(1)
+        assert torch.equal(mask.to(torch.int32), bits)
+        dX2, dS2 = torch.empty_like(x), torch.empty_like(x) if skip else None
+        dw2, db2 = torch.full((C,), 0.25, device=dev), torch.full((C,), -0.5, device=dev)
+        k.batchnorm_bwd(dY, None, x, w, sm, si, relu, dX2, dS2, dw2, db2, relu_mask=mask)
+        assert torch.equal(dX2, dX) and torch.equal(dw2, dw) and torch.equal(db2, db)
+        if skip:
+            assert torch.equal(dS2, dS)
     grads = torch.autograd.grad(ref, [xf, wf, bf_] + ([sf] if skip else []), dY.float())
     close(dX, grads[0], atol_frac=2e-2)
     torch.testing.assert_close(dw - 0.25, grads[1], rtol=2e-2, atol=2e-2 * grads[1].abs().max().item() + 1e-3)

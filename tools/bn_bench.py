@@ -33,11 +33,16 @@ def main():
         tf = timed(lambda: K.batchnorm_fwd(x, Y, w, b, rm, rv, True, 0.1, 1e-5, relu=True, skip=s,
                                            save_mean=sm, save_invstd=si), 10)
         tb = timed(lambda: K.batchnorm_bwd(x, Y, x, w, sm, si, True, dX, dS, dw, db), 10)
+        mk = torch.empty(x.numel() // 8, dtype=torch.uint8, device=dev)
+        tfm = timed(lambda: K.batchnorm_fwd(x, Y, w, b, rm, rv, True, 0.1, 1e-5, relu=True, skip=s,
+                                            save_mean=sm, save_invstd=si, relu_mask=mk), 10)
+        tbm = timed(lambda: K.batchnorm_bwd(x, None, x, w, sm, si, True, dX, dS, dw, db, relu_mask=mk), 10)
         nb = x.numel() * 2
         bf = (3 + (1 if skip else 0)) * nb
         bb = (6 + 1 + (1 if skip else 0)) * nb
         print(f"N{N} C{C:5d} {H:3d}x{W:<3d} skip={int(skip)}  fwd {tf * 1e3:7.1f} us ({bf / tf / 1e9:6.2f} TB/s)"
-              f"   bwd {tb * 1e3:7.1f} us ({bb / tb / 1e9:6.2f} TB/s)", flush=True)
+              f"   bwd {tb * 1e3:7.1f} us ({bb / tb / 1e9:6.2f} TB/s)"
+              f"   | relu mask: fwd {tfm * 1e3:7.1f} us  bwd {tbm * 1e3:7.1f} us", flush=True)
 
 
 if __name__ == "__main__":
