@@ -22,14 +22,25 @@ GEMM = re.compile(r"mmu::gemm_(big|small|pipe)_kernel")
 
 
 def per_dispatch(path, counter):
+    """per-dispatch counter sums of the BERT-layer GEMM launches: big-tile mmu_gemm kernels
+    dispatched between an embedding forward and the next embedding backward (the encoder
+    of one step: the ResNet trunk runs before the one and after the other)"""
     vals = defaultdict(float)
     names = {}
-    for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter:
+    rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    inside = False
+    for r in rows:
+        n = r["Kernel_Name"]
+        if "embed_fwd" in n:
+            inside = True
+        elif "embed_bwd" in n:
+            inside = False
+        if not inside or not GEMM.search(n) or "gemm_small" in n:
             continue
         d = r["Dispatch_Id"]
         vals[d] += float(r["Counter_Value"])
-        names[d] = r["Kernel_Name"]
+        names[d] = n
     return vals, names
 
 
