@@ -85,6 +85,22 @@ def main():
          lambda: K.gemm(A, HID, True, W1, HID, True, out3072, FFN, M, FFN, HID,
                         epi=K.epilogue(K.EPI_BIAS_GELU, bias=b1, aux=Zs)),
          lambda: torch.matmul(A, W1.t())),
+        ("fwd ffn1 gelu, no aux", M, FFN, HID,
+         lambda: K.gemm(A, HID, True, W1, HID, True, out3072, FFN, M, FFN, HID,
+                        epi=K.epilogue(K.EPI_BIAS_GELU, bias=b1)),
+         lambda: torch.matmul(A, W1.t())),
+        ("fwd ffn1 bias only", M, FFN, HID,
+         lambda: K.gemm(A, HID, True, W1, HID, True, out3072, FFN, M, FFN, HID,
+                        epi=K.epilogue(K.EPI_STORE, bias=b1)),
+         lambda: torch.matmul(A, W1.t())),
+        ("fwd o    bias only", M, HID, HID,
+         lambda: K.gemm(O, HID, True, Wo, HID, True, out768, HID, M, HID, HID,
+                        epi=K.epilogue(K.EPI_STORE, bias=bo)),
+         lambda: torch.matmul(O, Wo.t())),
+        ("fwd o    res, no dropout", M, HID, HID,
+         lambda: K.gemm(O, HID, True, Wo, HID, True, out768, HID, M, HID, HID,
+                        epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=bo, residual=X, drop_p=0.0, seed=1)),
+         lambda: torch.matmul(O, Wo.t())),
         ("fwd ffn2 drop_res", M, HID, FFN,
          lambda: K.gemm(Hh, FFN, True, W2, FFN, True, out768, HID, M, HID, FFN,
                         epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=bo, residual=A, drop_p=0.1, seed=2)),
