@@ -115,10 +115,9 @@ class ProjFunction(torch.autograd.Function):
         B = X.shape[0]
         E, Ein = wshape
         dY = dout[:, off:off + Li].contiguous().to(bf16).view(B * Li, E)
-        gw = torch.zeros(wshape, dtype=torch.float32, device=X.device)
-        K.gemm(dY, E, False, X.view(B * Li, Ein), Ein, False, gw, Ein, E, Ein, B * Li,
-               epi=K.epilogue(K.EPI_STORE, accumulate=True))
-        gb = torch.zeros(E, dtype=torch.float32, device=X.device)
+        gw = torch.empty(wshape, dtype=torch.float32, device=X.device)
+        K.gemm(dY, E, False, X.view(B * Li, Ein), Ein, False, gw, Ein, E, Ein, B * Li, epi=K.epilogue(K.EPI_STORE))
+        gb = torch.empty(E, dtype=torch.float32, device=X.device)
         K.colsum_bf16(dY, gb)
         return None, gw, gb, dout, None
 
@@ -143,6 +142,10 @@ class BlockFunction(torch.autograd.Function):
         m1, r1 = torch.empty(M, dtype=f32, device=dev), torch.empty(M, dtype=f32, device=dev)
         K.layernorm_fwd(X, l1w, l1b, h1, m1, r1, LN_EPS)
         Win, Wo, W1, W2 = (t.to(bf16) for t in (win, wo, w1, w2))
+        # K-major copies for the data-gradient products dX = dY W (B = W^T K-contiguous: the
+        # GEMM's faster B path, as the BERT layers' transposed copies); dZ = dT W2
+        # keeps W2 as is (no faster K-major on the BERT shapes)
+        Wint, Wot, W1t = (t.t().contiguous() for t in (Win, Wo, W1))
         qkv = torch.empty(M, 3 * E, dtype=bf16, device=dev)
         K.gemm(h1, E, True, Win, E, True, qkv, 3 * E, M, 3 * E, E, epi=K.epilogue(K.EPI_STORE, bias=bin_))
         O = torch.empty(M, E, dtype=bf16, device=dev)
@@ -160,7 +163,7 @@ class BlockFunction(torch.autograd.Function):
         y = torch.empty(M, E, dtype=bf16, device=dev)
         K.gemm(Hh, 4 * E, True, W2, 4 * E, True, y, E, M, E, 4 * E,
                epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=b2, residual=x1))
-        ctx.save_for_backward(X, h1, m1, r1, qkv, O, lse2, x1, h2, m2, r2, Hh, Zd, Win, Wo, W1, W2, l1w, l2w)
+        ctx.save_for_backward(X, h1, m1, r1, qkv, O, lse2, x1, h2, m2, r2, Hh, Zd, Wint, Wot, W1t, W2, l1w, l2w)
         ctx.meta = (B, L, E, heads)
         if e0 is not None:
             _enc._block_events.append((e0, _enc._mark()))
@@ -168,55 +171,55 @@ class BlockFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        (X, h1, m1, r1, qkv, O, lse2, x1, h2, m2, r2, Hh, Zd, Win, Wo, W1, W2, l1w, l2w) = ctx.saved_tensors
+        (X, h1, m1, r1, qkv, O, lse2, x1, h2, m2, r2, Hh, Zd, Wint, Wot, W1t, W2, l1w, l2w) = ctx.saved_tensors
         B, L, E, heads = ctx.meta
         e0 = _enc._mark()
         M, dev, f32 = B * L, X.device, torch.float32
         dY = _rows(dy.contiguous()).to(bf16)
-        acc = K.epilogue(K.EPI_STORE, accumulate=True)
+        st = K.epilogue(K.EPI_STORE)  # weight gradients: f32 C written (no zero fill + accumulate)
         g = {k: None for k in ("win", "bin", "wo", "bo", "l1w", "l1b", "w1", "b1", "w2", "b2", "l2w", "l2b")}
         # ---- c_proj (its input gradient is dy: no trailing dropout)
         dT = dY
-        g["b2"] = torch.zeros(E, dtype=f32, device=dev)
+        g["b2"] = torch.empty(E, dtype=f32, device=dev)
         K.colsum_bf16(dT, g["b2"])
-        g["w2"] = torch.zeros(E, 4 * E, dtype=f32, device=dev)
-        K.gemm(dT, E, False, Hh, 4 * E, False, g["w2"], 4 * E, E, 4 * E, M, epi=acc)
+        g["w2"] = torch.empty(E, 4 * E, dtype=f32, device=dev)
+        K.gemm(dT, E, False, Hh, 4 * E, False, g["w2"], 4 * E, E, 4 * E, M, epi=st)
         dZ = torch.empty(M, 4 * E, dtype=bf16, device=dev)
         g["b1"] = torch.zeros(4 * E, dtype=f32, device=dev)
         K.gemm(dT, E, True, W2, 4 * E, False, dZ, 4 * E, M, 4 * E, E,
                epi=K.epilogue(K.EPI_DGELU, aux=Zd, colsum=g["b1"]))
-        g["w1"] = torch.zeros(4 * E, E, dtype=f32, device=dev)
-        K.gemm(dZ, 4 * E, False, h2, E, False, g["w1"], E, 4 * E, E, M, epi=acc)
+        g["w1"] = torch.empty(4 * E, E, dtype=f32, device=dev)
+        K.gemm(dZ, 4 * E, False, h2, E, False, g["w1"], E, 4 * E, E, M, epi=st)
         dh2 = torch.empty(M, E, dtype=bf16, device=dev)
-        K.gemm(dZ, 4 * E, True, W1, E, False, dh2, E, M, E, 4 * E)
+        K.gemm(dZ, 4 * E, True, W1t, 4 * E, True, dh2, E, M, E, 4 * E)
         # ---- ln_2 (+ the residual stream): dx1 = LN2'(dh2) + dy; its column sums = d out_proj.bias
         P = K.ln_parts(M)
         pw, pb, pbias = (torch.empty(P, E, dtype=f32, device=dev) for _ in range(3))
         dx1 = torch.empty(M, E, dtype=bf16, device=dev)
         K.layernorm_bwd_res(dh2, x1, m2, r2, l2w, dY, dx1, pw, pb, pbias)
         for k, part in (("l2w", pw), ("l2b", pb), ("bo", pbias)):
-            g[k] = torch.zeros(E, dtype=f32, device=dev)
+            g[k] = torch.empty(E, dtype=f32, device=dev)
             K.colsum_reduce(part, g[k])
-        g["wo"] = torch.zeros(E, E, dtype=f32, device=dev)
-        K.gemm(dx1, E, False, O, E, False, g["wo"], E, E, E, M, epi=acc)
+        g["wo"] = torch.empty(E, E, dtype=f32, device=dev)
+        K.gemm(dx1, E, False, O, E, False, g["wo"], E, E, E, M, epi=st)
         dO = torch.empty(M, E, dtype=bf16, device=dev)
-        K.gemm(dx1, E, True, Wo, E, False, dO, E, M, E, E)
+        K.gemm(dx1, E, True, Wot, E, True, dO, E, M, E, E)
         # ---- attention over the sample axis + in_proj
         dqkv = torch.empty(M, 3 * E, dtype=bf16, device=dev)
         delta = torch.empty(L * heads, B, dtype=f32, device=dev)
         K.seqattn_bwd(qkv, O, dO, lse2, delta, dqkv, B, L, heads)
-        g["bin"] = torch.zeros(3 * E, dtype=f32, device=dev)
+        g["bin"] = torch.empty(3 * E, dtype=f32, device=dev)
         K.colsum_bf16(dqkv, g["bin"])
-        g["win"] = torch.zeros(3 * E, E, dtype=f32, device=dev)
-        K.gemm(dqkv, 3 * E, False, h1, E, False, g["win"], E, 3 * E, E, M, epi=acc)
+        g["win"] = torch.empty(3 * E, E, dtype=f32, device=dev)
+        K.gemm(dqkv, 3 * E, False, h1, E, False, g["win"], E, 3 * E, E, M, epi=st)
         dh1 = torch.empty(M, E, dtype=bf16, device=dev)
-        K.gemm(dqkv, 3 * E, True, Win, E, False, dh1, E, M, E, 3 * E)
+        K.gemm(dqkv, 3 * E, True, Wint, 3 * E, True, dh1, E, M, E, 3 * E)
         # ---- ln_1 (+ the residual stream)
         dx = torch.empty(M, E, dtype=bf16, device=dev)
         pw1, pb1 = (torch.empty(P, E, dtype=f32, device=dev) for _ in range(2))
         K.layernorm_bwd_res(dh1, X, m1, r1, l1w, dx1, dx, pw1, pb1, None)
         for k, part in (("l1w", pw1), ("l1b", pb1)):
-            g[k] = torch.zeros(E, dtype=f32, device=dev)
+            g[k] = torch.empty(E, dtype=f32, device=dev)
             K.colsum_reduce(part, g[k])
         if e0 is not None:
             _enc._block_events.append((e0, _enc._mark()))
