@@ -722,6 +722,18 @@ static __device__ __forceinline__ int kperm(int i) {  // LDS row i of a 32-key h
 // keep decisions of key pair (2i, 2i+1) from one 32-bit hash (low half -> even key):
 // zero the dropped P values and shift the two keep bits into w (odd key first, so that a
 // descending walk leaves bit k of w = element k)
+// the same decisions without the keep bits (inference: no backward reads them)
+static __device__ __forceinline__ void drop_pair_zero(uint32_t hsh, uint32_t thr, uint32_t thr_hi, float& e0,
+                                                      float& e1) {
+  asm("v_cmp_le_u32 vcc, %[th], %[h]\n\t"
+      "v_cndmask_b32 %[d1], 0, %[d1], vcc\n\t"
+      "v_cmp_le_u16 vcc, %[t], %[h]\n\t"
+      "v_cndmask_b32 %[d0], 0, %[d0], vcc"
+      : [d0] "+v"(e0), [d1] "+v"(e1)
+      : [h] "v"(hsh), [t] "s"(thr), [th] "s"(thr_hi)
+      : "vcc");
+}
+
 static __device__ __forceinline__ void drop_pair_apply(uint32_t hsh, uint32_t thr, uint32_t thr_hi, float& e0,
                                                        float& e1, uint32_t& w) {
   asm("v_cmp_le_u32 vcc, %[th], %[h]\n\t"
@@ -735,7 +747,9 @@ static __device__ __forceinline__ void drop_pair_apply(uint32_t hsh, uint32_t th
       : "vcc");
 }
 
-template <bool DROP, int WPE, bool NOHOIST>
+// STORE = false: dropout without the keep-bit words (p.dropmask ignored): MC-dropout
+// inference, where no backward reads them; fewer live registers -> 3 waves / SIMD
+template <bool DROP, int WPE, bool NOHOIST, bool STORE = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void attn_fwd_v2_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) char smem[FWD_NS * FWD_STAGE + 4 * 32 * FWD_MAX_NKV * 8];
   uint64_t* kbuf_all = (uint64_t*)(smem + FWD_NS * FWD_STAGE);
@@ -749,7 +763,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const uint32_t thr = drop_thr(p.drop_p), thr_hi = thr << 16;
   const int nkv = (L + 63) / 64;
   uint64_t* kbuf = kbuf_all + w * 32 * nkv;
-  const bool store_bits = DROP && p.dropmask != nullptr;
+  const bool store_bits = STORE && DROP && p.dropmask != nullptr;
   // dropout counter base of row q: seed_bh + 4 (q nkv) + 2h  (+ 4j + s2 per tile half)
   const uint32_t ctr = seed_for(p.seed, bh) + 4u * (uint32_t)q * (uint32_t)nkv + 2u * (uint32_t)h;
 
@@ -871,7 +885,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           uint32_t hsh = hb * kDropMul[i];
           hsh ^= hsh >> 16;
           float e0 = sc[s2][2 * i], e1 = sc[s2][2 * i + 1];
-          drop_pair_apply(hsh, thr, thr_hi, e0, e1, wb[s2]);
+          if (STORE) drop_pair_apply(hsh, thr, thr_hi, e0, e1, wb[s2]);
+          else drop_pair_zero(hsh, thr, thr_hi, e0, e1);
           sc[s2][2 * i] = e0;
           sc[s2][2 * i + 1] = e1;
         }
@@ -948,7 +963,10 @@ void attention_fwd_launch(const AttnParams& p, hipStream_t s) {
     // Dropout variant at 2 waves / SIMD (at the 3-wave register cap it spills lane-constant
     // LDS addresses around the loop: 0.89 vs 0.59 ms at B = 256, L = 513, p = 0.1).
     // A/B (MMU_ATTN_FWD): 3 = 3 waves/SIMD, 4 = 3 waves + per-tile re-derived addresses
-    if (drop_thr(p.drop_p)) {
+    if (drop_thr(p.drop_p) && !p.dropmask && ver != 5) {
+      // inference dropout (MC-dropout passes): no keep bits to store (MMU_ATTN_FWD=5: the storing kernel)
+      hipLaunchKernelGGL((attn_fwd_v2_kernel<true, 3, true, false>), grid, dim3(256), 0, s, p);
+    } else if (drop_thr(p.drop_p)) {
       if (ver == 3) hipLaunchKernelGGL((attn_fwd_v2_kernel<true, 3, false>), grid, dim3(256), 0, s, p);
       else if (ver == 4) hipLaunchKernelGGL((attn_fwd_v2_kernel<true, 3, true>), grid, dim3(256), 0, s, p);
       else hipLaunchKernelGGL((attn_fwd_v2_kernel<true, 2, false>), grid, dim3(256), 0, s, p);

@@ -377,6 +377,36 @@ def test_attention_dropout_multiword(dev, B, L):
         close(dqkv[:, 768 * part:768 * (part + 1)], g[:, 768 * part:768 * (part + 1)], atol_frac=3e-2)
 
 
+@pytest.mark.parametrize("B,L", [(2, 200), (1, 513)])
+def test_attention_dropout_inference_matches_training_forward(dev, B, L):
+    """MC-dropout inference (no dropmask: the forward kernel that stores no keep bits) drops
+    exactly the elements the training forward drops: its dropped-P matrix, recovered 64
+    keys at a time with one-hot V rows, has the zeros the training kernel's keep bits say;
+    O on the real V and LSE agree with the training forward to float-ordering tolerance."""
+    k = K()
+    p, seed = 0.1, 77
+    qkv, km = make_attn_inputs(dev, B, L, pad=False, seed=5, scale=1.0)
+    O1 = torch.empty(B * L, 768, dtype=torch.bfloat16, device=dev)
+    lse1, lse2 = torch.empty(B * 12, L, device=dev), torch.empty(B * 12, L, device=dev)
+    dm = k.dropmask_empty(B, L, 12, dev)
+    k.attention_fwd(qkv, km, O1, lse1, B, L, drop_p=p, seed=seed, dropmask=dm)
+    keep = k.dropmask_dense(dm, L).view(B, 12, L, L)
+    seen = torch.zeros(B, 12, L, L, device=dev)
+    for c in range(0, L, 64):  # one-hot V on keys [c, c+64): O[q, d] = P[q, c+d] * keep / (1-p)
+        w = min(64, L - c)
+        probe = qkv.clone().view(B, L, 3, 12, 64)
+        probe[:, :, 2] = 0
+        probe[:, c + torch.arange(w, device=dev), 2, :, torch.arange(w, device=dev)] = 1.0
+        O = torch.empty(B * L, 768, dtype=torch.bfloat16, device=dev)
+        k.attention_fwd(probe.view(B * L, 2304), km, O, lse2, B, L, drop_p=p, seed=seed)
+        seen[..., c:c + w] = (O.float().view(B, L, 12, 64).permute(0, 2, 1, 3)[..., :w] > 0).float()
+    assert torch.equal(seen, keep)
+    O2 = torch.empty_like(O1)
+    k.attention_fwd(qkv, km, O2, lse2, B, L, drop_p=p, seed=seed)
+    close(O2, O1.float(), atol_frac=1e-2)
+    torch.testing.assert_close(lse2, lse1, rtol=1e-5, atol=1e-5)
+
+
 # ----------------------------------------------------------------------------- layernorm
 def test_layernorm_fwd_bwd(dev):
     k = K()

@@ -20,6 +20,19 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(scope="module", autouse=True)
+def deterministic_convs():
+    """MIOpen's default fp32 conv solvers are not run-to-run deterministic (last-bit
+    differences of the trunk output, ~2e-7), which the random-init eval-mode trunk and the
+    bf16 encoder amplify to ~2e-3 of the logits between two calls on the same input.  These
+    tests compare separate calls (T = 1 vs T passes, two seeded MC runs), so they pin MIOpen
+    to its deterministic solvers (bit-identical repeated forwards, measured on MI355X)."""
+    old = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    yield
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = old
+
+
 def tol_check(got, ref, rel=2e-2, abs_=2e-3, what=""):
     got, ref = np.asarray(got, dtype=np.float64), np.asarray(ref, dtype=np.float64)
     err = np.abs(got - ref).max()
