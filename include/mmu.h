@@ -226,6 +226,17 @@ int mmu_row_pool_fwd(const void* fmap, int64_t B, int64_t Hh, int64_t Ww, int64_
 int mmu_row_pool_bwd(const float* dout, int64_t B, int64_t Hh, int64_t Ww, int64_t C, int64_t n,
                      void* dfmap, mmu_stream_t stream);
 
+/* ------------------------------------------------------------------ 3x3 conv weight gradient
+ * dW (+)= dConv2d(3x3, stride 1, pad 1)/dW of the ResNet-152 bottleneck conv2 (torchvision
+ * Bottleneck.conv2, src/mmbt.py:19-21) on channels-last bf16 maps: X [n_img*H*W, Cin] (the
+ * conv input), dY [n_img*H*W, Cout] (its output gradient); dW f32 [Cout][3][3][Cin] (the
+ * channels-last filter), += when accumulate.  One implicit-im2col MFMA GEMM (M = Cout,
+ * N = 9 Cin, K = pixels; the B operand gathered per tap with zero padding), split-K over
+ * the pixels into ws (f32, may be NULL: no split).  Cin % 256 == 0, Cout % 128 == 0. */
+int mmu_conv3x3_wgrad(const void* dY, const void* X, float* dW, int64_t n_img, int64_t H, int64_t W,
+                      int64_t Cin, int64_t Cout, int accumulate, float* ws, int64_t ws_floats,
+                      mmu_stream_t stream);
+
 /* ------------------------------------------------------------------ BatchNorm (image trunk)
  * BatchNorm2d [+ residual add] [+ ReLU] of the ResNet-152 trunk (torchvision
  * Bottleneck bn1/bn2/bn3 + downsample, src/mmbt.py:19-21) on channels-last bf16

@@ -467,6 +467,43 @@ int mmu_row_pool_bwd(const float* dout, int64_t B, int64_t Hh, int64_t Ww, int64
   return check_launch("mmu_row_pool_bwd");
 }
 
+int mmu_conv3x3_wgrad(const void* dY, const void* X, float* dW, int64_t n_img, int64_t H, int64_t W, int64_t Cin,
+                      int64_t Cout, int accumulate, float* ws, int64_t ws_floats, mmu_stream_t stream) {
+  if (!dY || !X || !dW) return fail("mmu_conv3x3_wgrad: null pointer");
+  if (n_img <= 0 || H <= 0 || W <= 0 || Cin % 256 || Cout % 128 || Cin <= 0 || Cout <= 0)
+    return fail("mmu_conv3x3_wgrad: needs Cin %% 256 == 0, Cout %% 128 == 0 (Cin=%ld Cout=%ld)", Cin, Cout);
+  const int64_t K = n_img * H * W;
+  if (K >= (1 << 24) || 2 * (K + 64) * Cin >= (1ll << 31) || 2 * (K + 64) * Cout >= (1ll << 31))
+    return fail("mmu_conv3x3_wgrad: map too large for 32-bit buffer offsets");
+  GemmParams p{};
+  p.A = (const bf16*)dY; p.lda = Cout;  // A = dY^T: M-major [K pixels][Cout]
+  p.B = (const bf16*)X; p.ldb = Cin;    // B gathered: [K pixels][9 Cin]
+  p.C = dW; p.ldc = 9 * Cin;            // dW [Cout][3][3][Cin] f32 (channels-last filter)
+  p.M = Cout; p.N = 9 * Cin; p.K = K;
+  p.conv_h = (int)H; p.conv_w = (int)W; p.conv_c = (int)Cin;
+  p.tiles_m = (int)((Cout + 255) / 256);
+  p.tiles_n = (int)(9 * Cin / 256);
+  p.group_m = 1;
+  p.kind = MMU_EPI_STORE;
+  p.accumulate = accumulate;
+  // split-K over the pixels (few output tiles): ~640 blocks, >= 1024 pixels per slice
+  const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
+  int64_t want = (640 + tiles - 1) / tiles;
+  if (want > K / 1024) want = K / 1024;
+  if (want > 32) want = 32;
+  if (ws && want > ws_floats / (p.M * p.N)) want = ws_floats / (p.M * p.N);
+  p.splitk = 1;
+  p.kchunk = K;
+  if (ws && want >= 2) {
+    int64_t chunk = ((K + want - 1) / want + 63) / 64 * 64;
+    p.kchunk = chunk;
+    p.splitk = (int)((K + chunk - 1) / chunk);
+    p.ws = ws;
+  }
+  conv3x3_wgrad_launch(p, (hipStream_t)stream);
+  return check_launch("mmu_conv3x3_wgrad");
+}
+
 int64_t mmu_batchnorm_ws_bytes(int64_t C) { return batchnorm_ws_bytes(C); }
 
 static int bn_common(int64_t rows, int64_t C, void* ws, int64_t ws_bytes, const char* who) {

@@ -382,8 +382,39 @@ static __device__ __forceinline__ void dma_tile(char* s, __amdgpu_buffer_rsrc_t 
   }
 }
 
-template <bool AK, bool BKM, int EPI, bool OUT_F32>
-__global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p) {
+// B tile (64 k-rows = pixels x 256 n = one tap's channels ci0..ci0+255) of the 3x3 conv
+// weight gradient, gathered from the NHWC map (rsrc): pixel (img, h, w) reads the input
+// pixel (h + dh, w + dw) of the block's tap; padding (and pixels >= K) read as zero through
+// an offset past the buffer's range.  Same lane-linear LDS image as dma_tile<false>.
+static __device__ __forceinline__ void dma_tile_convb(char* s, __amdgpu_buffer_rsrc_t rsrc, const GemmParams& p,
+                                                      int dh, int dw, int64_t ci0, int64_t k0, int w, int l) {
+  const int H = p.conv_h, W = p.conv_w, HW = H * W, C = p.conv_c;
+  const float rhw = 1.0f / (float)HW, rw = 1.0f / (float)W;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = w * 4 + i;
+    const int kr = piece * 2 + (l >> 5), j = l & 31;
+    const int b = (j >> 1) ^ sw_mn(kr);
+    const int pix = (int)k0 + kr;
+    // pix / HW and rem / W by float reciprocal + one correction (exact for pix < 2^24)
+    int img = (int)((float)pix * rhw);
+    int rem = pix - img * HW;
+    if (rem < 0) { --img; rem += HW; } else if (rem >= HW) { ++img; rem -= HW; }
+    int hh = (int)((float)rem * rw);
+    int ww = rem - hh * W;
+    if (ww < 0) { --hh; ww += W; } else if (ww >= W) { ++hh; ww -= W; }
+    hh += dh;
+    ww += dw;
+    const bool ok = pix < p.K && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
+    const uint32_t src = ok ? (uint32_t)(((((int64_t)img * H + hh) * W + ww) * C + ci0 + 16 * b + 8 * (j & 1)) * 2)
+                            : 0x7FFFFFF0u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (MMU_LDS(void)*)(s + piece * 1024), 16, src, 0, 0, 0);
+  }
+}
+
+// GATHER = 1: the 3x3 conv weight-gradient product (B gathered by dma_tile_convb)
+template <bool AK, bool BKM, int EPI, bool OUT_F32, int GATHER>
+static __device__ __forceinline__ void gemm_big_body(const GemmParams& p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * B_STAGE];
   const int t = threadIdx.x, l = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -411,8 +442,16 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p) {
   const int64_t kb = (int64_t)slice * p.kchunk;
   const int64_t ke = kb + p.kchunk < p.K ? kb + p.kchunk : p.K;
   const int nk = (int)((ke - kb + BKT - 1) / BKT);
+  // conv gather: the block's tap (n0 / C: a 256-column tile lies in one tap) and channels
+  const int tap = GATHER ? (int)(n0 / p.conv_c) : 0;
+  const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+  const int64_t ci0 = GATHER ? n0 - (int64_t)tap * p.conv_c : 0;
+  auto dma_b = [&](char* d, int64_t k) {
+    if (GATHER) dma_tile_convb(d, rb, p, dh, dw, ci0, k, w, l);
+    else dma_tile<BKM>(d, rb, p.ldb, n0, k, w, l);
+  };
   dma_tile<AK>(smem, ra, p.lda, m0, kb, w, l);
-  dma_tile<BKM>(smem + B_TILE, rb, p.ldb, n0, kb, w, l);
+  dma_b(smem + B_TILE, kb);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   GEMM_STAMP(1);
@@ -423,7 +462,7 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p) {
       char* d = smem + ((kt + 1) & 1) * B_STAGE;
       const int64_t k1 = kb + (int64_t)(kt + 1) * BKT;
       dma_tile<AK>(d, ra, p.lda, m0, k1, w, l);
-      dma_tile<BKM>(d + B_TILE, rb, p.ldb, n0, k1, w, l);
+      dma_b(d + B_TILE, k1);
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -447,6 +486,21 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
   GEMM_STAMP(3);
+}
+
+template <bool AK, bool BKM, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p) {
+  gemm_big_body<AK, BKM, EPI, OUT_F32, 0>(p);
+}
+
+// dW[co][tap][ci] (+)= sum over pixels dY[pixel][co] * X[pixel shifted by tap][ci]
+__global__ __launch_bounds__(512) void gemm_convw_kernel(GemmParams p) {
+  gemm_big_body<false, false, MMU_EPI_STORE, true, 1>(p);
+}
+
+void conv3x3_wgrad_launch(const GemmParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(gemm_convw_kernel, dim3(p.tiles_m * p.tiles_n, p.splitk, 1), dim3(512), 0, s, p);
+  if (p.splitk > 1) splitk_reduce_launch(p, 1, s);
 }
 
 // ================================================================ persistent 256x256

@@ -300,6 +300,25 @@ def row_pool_bwd(dout, n, dfmap_nhwc):
     N.call("mmu_row_pool_bwd", _ptr(dout), B, Hh, Ww, C, n, _ptr(dfmap_nhwc), _stream(dout))
 
 
+def conv3x3_wgrad(dY, X, dW, accumulate=False):
+    """dW (+)= weight gradient of a 3x3 / stride 1 / pad 1 conv: X [N, Cin, H, W] and dY
+    [N, Cout, H, W] channels-last bf16, dW f32 [Cout, Cin, 3, 3] channels-last (memory
+    [Cout][3][3][Cin]).  Cin % 256 == 0, Cout % 128 == 0."""
+    _dev_check(dY, X, dW)
+    _want(X, torch.bfloat16, "conv3x3_wgrad X")
+    _want(dY, torch.bfloat16, "conv3x3_wgrad dY")
+    n, cin, h, w = X.shape
+    cout = dY.shape[1]
+    cl = torch.channels_last
+    if (dY.shape != (n, cout, h, w) or dW.shape != (cout, cin, 3, 3) or dW.dtype != torch.float32
+            or not X.is_contiguous(memory_format=cl) or not dY.is_contiguous(memory_format=cl)
+            or not dW.is_contiguous(memory_format=cl)):
+        raise N.NativeError("conv3x3_wgrad: X / dY channels-last bf16 [N, C, H, W], dW f32 channels-last [Cout, Cin, 3, 3]")
+    ws = _splitk_workspace(X.device)
+    N.call("mmu_conv3x3_wgrad", _ptr(dY), _ptr(X), _ptr(dW), n, h, w, cin, cout, int(bool(accumulate)), _ptr(ws),
+           ws.numel(), _stream(X))
+
+
 _bn_ws = {}
 
 

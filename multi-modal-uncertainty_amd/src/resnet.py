@@ -11,6 +11,8 @@ Bottleneck the block input feeds both conv1 and bn3's residual: bn3's backward h
 skip gradient to conv1's backward (_SkipGrad), whose dX GEMM adds it in the epilogue
 (EPI_ADD_RES) instead of autograd summing the two in a separate pass.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -115,10 +117,27 @@ class _ConvBF16(torch.autograd.Function):
         stride, padding = ctx.conf
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         dy = dy.contiguous(memory_format=torch.channels_last)
-        dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w16, None, stride, padding, (1, 1), False, (0, 0), 1,
-                                                       (need_x, need_w, False))
+        cl = torch.channels_last
+        # 3x3 stride-1 filter gradients: one implicit-im2col MFMA GEMM straight into the f32
+        # gradient (mmu_conv3x3_wgrad) instead of MIOpen's wrw + a zero fill + an add pass
+        mmu_w = (need_w and tuple(w16.shape[2:]) == (3, 3) and tuple(stride) == (1, 1) and tuple(padding) == (1, 1)
+                 and _mmu_3x3_wgrad(x.shape[1], w16.shape[0], x.shape[0] * x.shape[2] * x.shape[3]))
+        dx = dw = None
+        if need_x or (need_w and not mmu_w):
+            dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w16, None, stride, padding, (1, 1), False, (0, 0),
+                                                           1, (need_x, need_w and not mmu_w, False))
         rw = None
-        if need_w:
+        if mmu_w:
+            g = ctx.w.grad
+            if g is not None and g.dtype == torch.float32 and g.is_contiguous(memory_format=cl):
+                K.conv3x3_wgrad(dy, x, g, accumulate=True)
+            else:
+                rw = torch.empty(w16.shape, dtype=torch.float32, device=x.device, memory_format=cl)
+                K.conv3x3_wgrad(dy, x, rw, accumulate=False)
+                if g is not None:
+                    g.add_(rw)
+                    rw = None
+        elif need_w:
             if ctx.w.grad is not None:
                 ctx.w.grad.add_(dw)
             else:
@@ -138,6 +157,16 @@ class _SkipGrad:
 def _rows(t):
     """[N, C, H, W] channels-last -> its [N*H*W, C] row-major view."""
     return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
+
+
+_CONV3_WGRAD = os.environ.get("MMU_CONV3_WGRAD", "1") != "0"
+
+
+def _mmu_3x3_wgrad(cin, cout, M):
+    """3x3 / stride-1 filter gradients on mmu_conv3x3_wgrad (the MFMA GEMM with the im2col
+    gather in its B-operand DMA) instead of MIOpen: needs Cin % 256 == 0 and Cout % 128 == 0
+    (layer3 / layer4 conv2 of ResNet-152; MMU_CONV3_WGRAD=0 keeps MIOpen for A/B runs)."""
+    return _CONV3_WGRAD and cin % 256 == 0 and cout % 128 == 0 and M >= 1024
 
 
 def _mmu_1x1(cin, cout, M, H):

@@ -56,6 +56,26 @@ def _close(a, b, what, frac=2e-2):
     assert err <= frac * scale, f"{what}: |err| {err:.3e} vs |ref| {scale:.3e}"
 
 
+@pytest.mark.parametrize("n,cin,cout,h,w", [(2, 256, 256, 14, 14), (3, 512, 128, 7, 5), (1, 256, 384, 9, 11),
+                                             (16, 256, 256, 14, 14)])
+def test_conv3x3_wgrad_matches_torch(dev, n, cin, cout, h, w):
+    """mmu_conv3x3_wgrad (implicit im2col in the GEMM's B-operand DMA, split-K over pixels)
+    against torch's fp32 conv weight gradient on the same bf16 inputs; accumulate and store."""
+    from src import kernels as K
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(cin + h)
+    x = torch.randn(n, cin, h, w, generator=g, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    dy = torch.randn(n, cout, h, w, generator=g, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, 3, 3), dy.float(), stride=1, padding=1)
+    dw = torch.full((cout, cin, 3, 3), 0.5, device=dev).contiguous(memory_format=cl)
+    K.conv3x3_wgrad(dy, x, dw, accumulate=True)
+    _close(dw - 0.5, ref, "dW accumulate", frac=1e-4)
+    dw2 = torch.empty((cout, cin, 3, 3), device=dev).contiguous(memory_format=cl)
+    K.conv3x3_wgrad(dy, x, dw2)
+    _close(dw2, ref, "dW", frac=1e-4)
+    assert (dw2 - ref).abs().max().item() <= 1e-3 * ref.abs().max().item()
+
+
 @pytest.mark.parametrize("cin,width,hw,batch", [(1024, 256, 14, 128), (256, 64, 56, 4)])
 def test_bottleneck_mmu_1x1_matches_miopen(dev, monkeypatch, cin, width, hw, batch):
     from src import resnet as R
@@ -140,6 +160,7 @@ def test_model_grads_with_mmu_1x1_match_miopen(dev, monkeypatch):
 
     l1, g1 = grads()
     monkeypatch.setattr(R, "_mmu_1x1", lambda *a: (False, False, False))
+    monkeypatch.setattr(R, "_mmu_3x3_wgrad", lambda *a: False)
     l0, g0 = grads()
     lr, gr = grads("fp32")                          # the trunk in fp32: the truth for both
     assert abs(l1 - lr) <= 1e-2 * abs(lr)
