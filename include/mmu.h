@@ -237,6 +237,16 @@ int mmu_conv3x3_wgrad(const void* dY, const void* X, float* dW, int64_t n_img, i
                       int64_t Cin, int64_t Cout, int accumulate, float* ws, int64_t ws_floats,
                       mmu_stream_t stream);
 
+/* 3x3 / stride-1 / pad-1 convolution as one implicit-im2col MFMA GEMM (the A operand
+ * gathered per tap, padding read as zero): Y[pixel][n] = sum over taps t = 3 kh + kw and
+ * channels c of X[pixel + (kh - 1, kw - 1)][c] * Wk[n][t * C + c], bf16 in / out,
+ * f32 accumulate; X [n_img*H*W, C] and Y [n_img*H*W, N] NHWC rows.  The forward of
+ * Bottleneck.conv2 is (X = x, Wk = the channels-last filter [Cout][3][3][Cin]); its data
+ * gradient is (X = dY, Wk = the flipped filter transposed to [Cin][3][3][Cout]).
+ * C % 64 == 0, N % 128 == 0, N >= 256. */
+int mmu_conv3x3_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W,
+                         int64_t C, int64_t N, mmu_stream_t stream);
+
 /* ------------------------------------------------------------------ BatchNorm (image trunk)
  * BatchNorm2d [+ residual add] [+ ReLU] of the ResNet-152 trunk (torchvision
  * Bottleneck bn1/bn2/bn3 + downsample, src/mmbt.py:19-21) on channels-last bf16

@@ -504,6 +504,30 @@ int mmu_conv3x3_wgrad(const void* dY, const void* X, float* dW, int64_t n_img, i
   return check_launch("mmu_conv3x3_wgrad");
 }
 
+int mmu_conv3x3_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
+                         int64_t N, mmu_stream_t stream) {
+  if (!X || !Wk || !Y) return fail("mmu_conv3x3_implicit: null pointer");
+  if (n_img <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 64 || N % 128 || N < 256)
+    return fail("mmu_conv3x3_implicit: needs C %% 64 == 0, N %% 128 == 0, N >= 256 (C=%ld N=%ld)", C, N);
+  const int64_t M = n_img * H * W;
+  if (M < 256 || 2 * (M + 256) * C >= (1ll << 31) || 2 * (N + 256) * 9 * C >= (1ll << 31))
+    return fail("mmu_conv3x3_implicit: map size out of range");
+  GemmParams p{};
+  p.A = (const bf16*)X; p.lda = C;       // A gathered: [M pixels][9 C]
+  p.B = (const bf16*)Wk; p.ldb = 9 * C;  // B K-major [N][9 C]
+  p.C = Y; p.ldc = N;                    // Y [M pixels][N] bf16
+  p.M = M; p.N = N; p.K = 9 * C;
+  p.conv_h = (int)H; p.conv_w = (int)W; p.conv_c = (int)C;
+  p.tiles_m = (int)((M + 255) / 256);
+  p.tiles_n = (int)((N + 255) / 256);
+  p.group_m = 1;
+  p.kind = MMU_EPI_STORE;
+  p.splitk = 1;
+  p.kchunk = p.K;
+  conv3x3_implicit_launch(p, (hipStream_t)stream);
+  return check_launch("mmu_conv3x3_implicit");
+}
+
 int64_t mmu_batchnorm_ws_bytes(int64_t C) { return batchnorm_ws_bytes(C); }
 
 static int bn_common(int64_t rows, int64_t C, void* ws, int64_t ws_bytes, const char* who) {

@@ -412,7 +412,46 @@ static __device__ __forceinline__ void dma_tile_convb(char* s, __amdgpu_buffer_r
   }
 }
 
-// GATHER = 1: the 3x3 conv weight-gradient product (B gathered by dma_tile_convb)
+// A tile (256 rows = output pixels x 64 k = channels ci0..ci0+63 of one tap) of a 3x3 /
+// stride-1 / pad-1 convolution as an implicit GEMM, gathered from the NHWC map (rsrc): row
+// pixel (img, h, w) reads input pixel (h + dh, w + dw); padding and rows >= M read as zero.
+// Each lane's 4 rows are fixed for the block (pbase / ph / pw, from conv_rows_init); only
+// the tap and channel offset move with k.  Same lane-linear LDS image as dma_tile<true>.
+struct ConvRows {
+  int base[4], h[4], w[4];  // img * H (-1: row past M), h, w of the lane's rows
+};
+static __device__ __forceinline__ ConvRows conv_rows_init(const GemmParams& p, int64_t m0, int w, int l) {
+  ConvRows r;
+  const int H = p.conv_h, W = p.conv_w, HW = H * W;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (w * 4 + i) * 8 + (l >> 3);
+    const int64_t pix = m0 + row;
+    const int img = (int)(pix / HW), rem = (int)(pix - (int64_t)img * HW);
+    r.base[i] = pix < p.M ? img * H : -1;
+    r.h[i] = rem / W;
+    r.w[i] = rem - r.h[i] * W;
+  }
+  return r;
+}
+static __device__ __forceinline__ void dma_tile_conva(char* s, __amdgpu_buffer_rsrc_t rsrc, const GemmParams& p,
+                                                      const ConvRows& r, int64_t k0, int w, int l) {
+  const int H = p.conv_h, W = p.conv_w, C = p.conv_c;
+  const int tap = (int)(k0 / C), ci0 = (int)(k0 - (int64_t)tap * C);
+  const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = w * 4 + i;
+    const int row = piece * 8 + (l >> 3), c = (l & 7) ^ (row & 7);
+    const int hh = r.h[i] + dh, ww = r.w[i] + dw;
+    const bool ok = r.base[i] >= 0 && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W && k0 < p.K;
+    const uint32_t src = ok ? (uint32_t)((((int64_t)(r.base[i] + hh) * W + ww) * C + ci0 + 8 * c) * 2) : 0x7FFFFFF0u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (MMU_LDS(void)*)(s + piece * 1024), 16, src, 0, 0, 0);
+  }
+}
+
+// GATHER = 1: the 3x3 conv weight-gradient product (B gathered by dma_tile_convb);
+// GATHER = 2: the 3x3 conv forward / data-gradient product (A gathered by dma_tile_conva)
 template <bool AK, bool BKM, int EPI, bool OUT_F32, int GATHER>
 static __device__ __forceinline__ void gemm_big_body(const GemmParams& p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * B_STAGE];
@@ -443,14 +482,20 @@ static __device__ __forceinline__ void gemm_big_body(const GemmParams& p) {
   const int64_t ke = kb + p.kchunk < p.K ? kb + p.kchunk : p.K;
   const int nk = (int)((ke - kb + BKT - 1) / BKT);
   // conv gather: the block's tap (n0 / C: a 256-column tile lies in one tap) and channels
-  const int tap = GATHER ? (int)(n0 / p.conv_c) : 0;
+  const int tap = GATHER == 1 ? (int)(n0 / p.conv_c) : 0;
   const int dh = tap / 3 - 1, dw = tap % 3 - 1;
-  const int64_t ci0 = GATHER ? n0 - (int64_t)tap * p.conv_c : 0;
+  const int64_t ci0 = GATHER == 1 ? n0 - (int64_t)tap * p.conv_c : 0;
   auto dma_b = [&](char* d, int64_t k) {
-    if (GATHER) dma_tile_convb(d, rb, p, dh, dw, ci0, k, w, l);
+    if (GATHER == 1) dma_tile_convb(d, rb, p, dh, dw, ci0, k, w, l);
     else dma_tile<BKM>(d, rb, p.ldb, n0, k, w, l);
   };
-  dma_tile<AK>(smem, ra, p.lda, m0, kb, w, l);
+  ConvRows crow;
+  if (GATHER == 2) crow = conv_rows_init(p, m0, w, l);
+  auto dma_a = [&](char* d, int64_t k) {
+    if (GATHER == 2) dma_tile_conva(d, ra, p, crow, k, w, l);
+    else dma_tile<AK>(d, ra, p.lda, m0, k, w, l);
+  };
+  dma_a(smem, kb);
   dma_b(smem + B_TILE, kb);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -461,7 +506,7 @@ static __device__ __forceinline__ void gemm_big_body(const GemmParams& p) {
     if (kt + 1 < nk) {
       char* d = smem + ((kt + 1) & 1) * B_STAGE;
       const int64_t k1 = kb + (int64_t)(kt + 1) * BKT;
-      dma_tile<AK>(d, ra, p.lda, m0, k1, w, l);
+      dma_a(d, k1);
       dma_b(d + B_TILE, k1);
     }
 #pragma unroll
@@ -496,6 +541,15 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p) {
 // dW[co][tap][ci] (+)= sum over pixels dY[pixel][co] * X[pixel shifted by tap][ci]
 __global__ __launch_bounds__(512) void gemm_convw_kernel(GemmParams p) {
   gemm_big_body<false, false, MMU_EPI_STORE, true, 1>(p);
+}
+
+// Y[pixel][n] = sum over (tap, c) of X[pixel shifted by tap][c] * Wk[n][tap * C + c] (bf16 out)
+__global__ __launch_bounds__(512) void gemm_conva_kernel(GemmParams p) {
+  gemm_big_body<true, true, MMU_EPI_STORE, false, 2>(p);
+}
+
+void conv3x3_implicit_launch(const GemmParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(gemm_conva_kernel, dim3(p.tiles_m * p.tiles_n, 1, 1), dim3(512), 0, s, p);
 }
 
 void conv3x3_wgrad_launch(const GemmParams& p, hipStream_t s) {

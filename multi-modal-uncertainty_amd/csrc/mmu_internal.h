@@ -33,11 +33,13 @@ struct GemmParams {
   float* ws;
   int stagger;  // duo kernel: s_sleep(127) count for the second block of each CU (A/B experiment)
   int batch;    // batch items (the persistent kernel's 1-D grid walks tiles x slices x batch)
-  // 3x3 / stride 1 / pad 1 convolution weight gradient (gemm_convw_kernel): B is gathered
-  // from an NHWC map [K = img * conv_h * conv_w pixels][conv_c] as B[pixel][tap * conv_c + ci]
+  // 3x3 / stride 1 / pad 1 convolutions on an NHWC map [img * conv_h * conv_w pixels][conv_c]:
+  // weight gradient (gemm_convw_kernel): B[pixel][tap * conv_c + ci] gathered;
+  // forward / data gradient (gemm_conva_kernel): A[pixel][tap * conv_c + c] gathered
   int conv_h, conv_w, conv_c;
 };
 void conv3x3_wgrad_launch(const GemmParams& p, hipStream_t s);
+void conv3x3_implicit_launch(const GemmParams& p, hipStream_t s);
 
 void splitk_reduce_launch(const GemmParams& p, int batch, hipStream_t s);
 void gemm_tail_launch(const GemmParams& p, bool f32out, int64_t m0, int S, const float* ws, int batch, hipStream_t s);

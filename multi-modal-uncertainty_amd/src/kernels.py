@@ -300,6 +300,23 @@ def row_pool_bwd(dout, n, dfmap_nhwc):
     N.call("mmu_row_pool_bwd", _ptr(dout), B, Hh, Ww, C, n, _ptr(dfmap_nhwc), _stream(dout))
 
 
+def conv3x3_implicit(X, Wk, Y):
+    """Y[p, n] = sum_{tap, c} X[p + tap shift, c] Wk[n, tap * C + c]: X [N, C, H, W] and Y
+    [N, Nout, H, W] channels-last bf16, Wk bf16 contiguous with Wk.numel() == Nout * 9 * C
+    (a channels-last [Nout, C, 3, 3] filter, or the flipped-transposed one for dX)."""
+    _dev_check(X, Wk, Y)
+    _want(X, torch.bfloat16, "conv3x3_implicit X")
+    _want(Wk, torch.bfloat16, "conv3x3_implicit Wk")
+    n, c, h, w = X.shape
+    nout = Y.shape[1]
+    cl = torch.channels_last
+    if (Y.shape != (n, nout, h, w) or Y.dtype != torch.bfloat16 or Wk.numel() != nout * 9 * c
+            or not X.is_contiguous(memory_format=cl) or not Y.is_contiguous(memory_format=cl)
+            or not (Wk.is_contiguous() or Wk.is_contiguous(memory_format=cl))):
+        raise N.NativeError("conv3x3_implicit: X / Y channels-last bf16 [N, C, H, W], Wk [Nout][3][3][C] bf16")
+    N.call("mmu_conv3x3_implicit", _ptr(X), _ptr(Wk), _ptr(Y), n, h, w, c, nout, _stream(X))
+
+
 def conv3x3_wgrad(dY, X, dW, accumulate=False):
     """dW (+)= weight gradient of a 3x3 / stride 1 / pad 1 conv: X [N, Cin, H, W] and dY
     [N, Cout, H, W] channels-last bf16, dW f32 [Cout, Cin, 3, 3] channels-last (memory

@@ -109,6 +109,12 @@ class _ConvBF16(torch.autograd.Function):
     def forward(ctx, x, w, w16, stride, padding):
         ctx.save_for_backward(x, w16)
         ctx.w, ctx.conf = w, (stride, padding)
+        cout = w16.shape[0]
+        if _is_3x3_s1(w16, stride, padding) and _mmu_3x3(x.shape[1], cout, x.shape[0] * x.shape[2] * x.shape[3])[0]:
+            y = torch.empty((x.shape[0], cout, x.shape[2], x.shape[3]), dtype=x.dtype, device=x.device,
+                            memory_format=torch.channels_last)
+            K.conv3x3_implicit(x, w16, y)
+            return y
         return torch.ops.aten.convolution(x, w16, None, stride, padding, (1, 1), False, (0, 0), 1)
 
     @staticmethod
@@ -122,10 +128,16 @@ class _ConvBF16(torch.autograd.Function):
         # gradient (mmu_conv3x3_wgrad) instead of MIOpen's wrw + a zero fill + an add pass
         mmu_w = (need_w and tuple(w16.shape[2:]) == (3, 3) and tuple(stride) == (1, 1) and tuple(padding) == (1, 1)
                  and _mmu_3x3_wgrad(x.shape[1], w16.shape[0], x.shape[0] * x.shape[2] * x.shape[3]))
+        # its data gradient: the same implicit GEMM on dY with the flipped filter, [Cin][3][3][Cout]
+        mmu_x = (need_x and _is_3x3_s1(w16, stride, padding)
+                 and _mmu_3x3(x.shape[1], w16.shape[0], x.shape[0] * x.shape[2] * x.shape[3])[1])
         dx = dw = None
-        if need_x or (need_w and not mmu_w):
+        if (need_x and not mmu_x) or (need_w and not mmu_w):
             dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w16, None, stride, padding, (1, 1), False, (0, 0),
-                                                           1, (need_x, need_w and not mmu_w, False))
+                                                           1, (need_x and not mmu_x, need_w and not mmu_w, False))
+        if mmu_x:
+            dx = torch.empty_like(x, memory_format=cl)
+            K.conv3x3_implicit(dy, w16.flip(2, 3).permute(1, 2, 3, 0).contiguous(), dx)
         rw = None
         if mmu_w:
             g = ctx.w.grad
@@ -160,6 +172,24 @@ def _rows(t):
 
 
 _CONV3_WGRAD = os.environ.get("MMU_CONV3_WGRAD", "1") != "0"
+
+
+_CONV3_FWD = os.environ.get("MMU_CONV3_FWD", "1") != "0"
+_CONV3_DX = os.environ.get("MMU_CONV3_DX", "1") != "0"
+
+
+def _is_3x3_s1(w16, stride, padding):
+    return tuple(w16.shape[2:]) == (3, 3) and tuple(stride) == (1, 1) and tuple(padding) == (1, 1)
+
+
+def _mmu_3x3(cin, cout, M):
+    """(forward, data gradient) of a 3x3 / stride-1 conv on mmu_conv3x3_implicit (the MFMA
+    GEMM with the im2col gather in its A-operand DMA) instead of MIOpen: the output channels
+    (Cout forward, Cin for dX) >= 256 and % 128, the reduced ones % 64 (layer3 / layer4 conv2;
+    MMU_CONV3_FWD=0 / MMU_CONV3_DX=0 keep MIOpen for A/B runs)."""
+    fwd = _CONV3_FWD and cin % 64 == 0 and cout % 128 == 0 and cout >= 256 and M >= 256
+    dx = _CONV3_DX and cout % 64 == 0 and cin % 128 == 0 and cin >= 256 and M >= 256
+    return fwd, dx
 
 
 def _mmu_3x3_wgrad(cin, cout, M):

@@ -76,6 +76,30 @@ def test_conv3x3_wgrad_matches_torch(dev, n, cin, cout, h, w):
     assert (dw2 - ref).abs().max().item() <= 1e-3 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("n,cin,cout,h,w", [(2, 256, 256, 14, 14), (3, 512, 512, 7, 13), (4, 64, 384, 9, 11),
+                                             (16, 256, 256, 14, 14)])
+def test_conv3x3_implicit_matches_torch(dev, n, cin, cout, h, w):
+    """mmu_conv3x3_implicit (im2col gathered in the A-operand DMA) as the 3x3 conv forward
+    (filter as stored, channels-last) and as its data gradient (flipped filter transposed to
+    [Cin][3][3][Cout]) against torch's fp32 conv on the same bf16 inputs."""
+    from src import kernels as K
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(cin + w)
+    x = torch.randn(n, cin, h, w, generator=g, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    wt = (torch.randn(cout, cin, 3, 3, generator=g, device=dev) * 0.05).to(torch.bfloat16).contiguous(memory_format=cl)
+    y = torch.empty(n, cout, h, w, dtype=torch.bfloat16, device=dev).contiguous(memory_format=cl)
+    K.conv3x3_implicit(x, wt, y)
+    ref = torch.nn.functional.conv2d(x.float(), wt.float(), padding=1)
+    _close(y.float(), ref, "conv fwd", frac=5e-3)
+    assert (y.float() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
+    if cin >= 256:
+        dy = torch.randn(n, cout, h, w, generator=g, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+        dx = torch.empty_like(x)
+        K.conv3x3_implicit(dy, wt.flip(2, 3).permute(1, 2, 3, 0).contiguous(), dx)
+        rdx = torch.nn.grad.conv2d_input(x.shape, wt.float(), dy.float(), padding=1)
+        _close(dx.float(), rdx, "conv dX", frac=5e-3)
+
+
 @pytest.mark.parametrize("cin,width,hw,batch", [(1024, 256, 14, 128), (256, 64, 56, 4)])
 def test_bottleneck_mmu_1x1_matches_miopen(dev, monkeypatch, cin, width, hw, batch):
     from src import resnet as R
@@ -161,6 +185,7 @@ def test_model_grads_with_mmu_1x1_match_miopen(dev, monkeypatch):
     l1, g1 = grads()
     monkeypatch.setattr(R, "_mmu_1x1", lambda *a: (False, False, False))
     monkeypatch.setattr(R, "_mmu_3x3_wgrad", lambda *a: False)
+    monkeypatch.setattr(R, "_mmu_3x3", lambda *a: (False, False))
     l0, g0 = grads()
     lr, gr = grads("fp32")                          # the trunk in fp32: the truth for both
     assert abs(l1 - lr) <= 1e-2 * abs(lr)
