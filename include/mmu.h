@@ -91,11 +91,13 @@ int mmu_colsum_reduce(const float* partial, int64_t parts, int64_t N, float* out
 int mmu_colsum_bf16(const void* X, int64_t M, int64_t N, int64_t ldx, float* partial,
                     float* out, int accumulate, mmu_stream_t stream);
 
-/* Batched bf16 transpose: for each of n_jobs jobs (a device table of 4 int64 per job:
- * src pointer, dst pointer, rows, cols), dst[c*rows + r] = src[r*cols + c].  Keeps the
- * K-major (transposed) bf16 copies of the BERT layer weights that the data-gradient
- * products dX = dY.W read as their B operand (the backward of the nn.Linear layers inside
- * pytorch_pretrained_bert BertLayer, src/mmbt.py:124-126); max_rows / max_cols bound the
+/* Batched bf16 transpose: for each of n_jobs jobs (a device table of 6 int64 per job:
+ * src pointer, dst pointer, rows, cols, src row pitch, dst row pitch; a pitch of 0 means
+ * dense: cols / rows), dst[c*dpitch + r] = src[r*spitch + c].  Keeps the K-major
+ * (transposed) bf16 copies of the BERT layer weights that the data-gradient products
+ * dX = dY.W read as their B operand (the backward of the nn.Linear layers inside
+ * pytorch_pretrained_bert BertLayer, src/mmbt.py:124-126), and the flipped, transposed
+ * 3x3 filters of the conv data gradient (one job per tap); max_rows / max_cols bound the
  * jobs' shapes (grid size). */
 int mmu_transpose_bf16_batched(const int64_t* jobs, int n_jobs, int64_t max_rows, int64_t max_cols,
                                mmu_stream_t stream);

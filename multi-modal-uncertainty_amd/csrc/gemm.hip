@@ -1206,12 +1206,14 @@ void colsum_bf16_launch(const bf16* X, int64_t M, int64_t N, int64_t ld, float* 
 
 // ------------------------------------------------------------------ batched transpose
 // one 64 x 64 tile per workgroup through LDS (row pitch 65 elements: conflict-free column
-// reads), 16-B global reads and 8-B writes; blockIdx.z = job, tiles outside a job's shape exit
+// reads), 16-B global reads and 8-B writes; blockIdx.z = job, tiles outside a job's shape exit.
+// Job = {src, dst, rows, cols, src row pitch, dst row pitch} (pitches 0: dense)
 __global__ __launch_bounds__(256) void transpose_bf16_kernel(const int64_t* __restrict__ jobs) {
-  const int64_t* j = jobs + 4 * blockIdx.z;
+  const int64_t* j = jobs + 6 * blockIdx.z;
   const bf16* __restrict__ src = (const bf16*)j[0];
   bf16* __restrict__ dst = (bf16*)j[1];
   const int64_t rows = j[2], cols = j[3];
+  const int64_t sld = j[4] ? j[4] : cols, dld = j[5] ? j[5] : rows;
   const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
   if (r0 >= rows || c0 >= cols) return;
   __shared__ bf16 tile[64][65];
@@ -1221,12 +1223,12 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const int64_t* __re
     const int idx = t + 256 * i, r = idx >> 3, c = (idx & 7) * 8;
     const int64_t gr = r0 + r, gc = c0 + c;
     if (gr < rows && gc + 8 <= cols) {
-      const bf16x8 v = *(const bf16x8*)(src + gr * cols + gc);
+      const bf16x8 v = *(const bf16x8*)(src + gr * sld + gc);
 #pragma unroll
       for (int e = 0; e < 8; ++e) tile[r][c + e] = v[e];
     } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) tile[r][c + e] = (gr < rows && gc + e < cols) ? src[gr * cols + gc + e] : bf16(0.f);
+      for (int e = 0; e < 8; ++e) tile[r][c + e] = (gr < rows && gc + e < cols) ? src[gr * sld + gc + e] : bf16(0.f);
     }
   }
   __syncthreads();
@@ -1237,10 +1239,10 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const int64_t* __re
     if (gc >= cols) continue;
     if (gr + 4 <= rows) {
       bf16x4 v = {tile[r][c], tile[r + 1][c], tile[r + 2][c], tile[r + 3][c]};
-      *(bf16x4*)(dst + gc * rows + gr) = v;
+      *(bf16x4*)(dst + gc * dld + gr) = v;
     } else {
       for (int e = 0; e < 4; ++e)
-        if (gr + e < rows) dst[gc * rows + gr + e] = tile[r + e][c];
+        if (gr + e < rows) dst[gc * dld + gr + e] = tile[r + e][c];
     }
   }
 }

@@ -100,12 +100,12 @@ def colsum_reduce(partial, out, accumulate=False):
 
 
 def transpose_bf16_batched(jobs, n_jobs, max_rows, max_cols, stream_of):
-    """dst = src^T for every (src ptr, dst ptr, rows, cols) row of the int64 device table
-    ``jobs`` [n_jobs, 4]; see mmu_transpose_bf16_batched.  ``stream_of``: a tensor on the
-    target device (its current stream is used)."""
+    """dst = src^T for every (src ptr, dst ptr, rows, cols, src pitch, dst pitch) row of the
+    int64 device table ``jobs`` [n_jobs, 6] (pitch 0: dense); see mmu_transpose_bf16_batched.
+    ``stream_of``: a tensor on the target device (its current stream is used)."""
     _dev_check(jobs, stream_of)
-    if jobs.dtype != torch.int64 or not jobs.is_contiguous() or jobs.numel() < 4 * n_jobs:
-        raise N.NativeError("transpose_bf16_batched: jobs must be a contiguous int64 [n_jobs, 4] device table")
+    if jobs.dtype != torch.int64 or not jobs.is_contiguous() or jobs.numel() < 6 * n_jobs:
+        raise N.NativeError("transpose_bf16_batched: jobs must be a contiguous int64 [n_jobs, 6] device table")
     N.call("mmu_transpose_bf16_batched", _ptr(jobs), int(n_jobs), int(max_rows), int(max_cols), _stream(stream_of))
 
 

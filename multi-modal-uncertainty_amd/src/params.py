@@ -33,6 +33,7 @@ class ParamStore:
         self._versions = None
         self._tspecs = {}  # key (tuple of names) -> shape [rows, cols] of the fused compute view
         self._tcopies = {}
+        self._fcopies = {}  # conv filter name -> flipped, transposed bf16 copy [Cin, 3, 3, Cout]
         self._tjobs = None
         self.build()
         STORES.add(self)
@@ -128,21 +129,40 @@ class ParamStore:
         self._tcopies[key] = torch.empty(cols, rows, dtype=torch.bfloat16, device=self.compute.device)
         self._tjobs = None
 
+    def flipped_filter(self, name):
+        """bf16 [Cin, 3, 3, Cout] copy of the 3x3 filter ``name`` flipped in both taps (the B
+        operand of the conv data gradient as an implicit GEMM, src/resnet.py), kept in step
+        with the bf16 copies like the transposed ones (9 strided jobs of the same launch)."""
+        if name not in self._fcopies:
+            O, I, kh, kw = self.params[name].shape
+            assert (kh, kw) == (3, 3), name
+            self._fcopies[name] = torch.empty(I, 3, 3, O, dtype=torch.bfloat16, device=self.compute.device)
+            self._tjobs = None
+            self.sync_transposed()
+        return self._fcopies[name]
+
     def sync_transposed(self):
-        """Refresh every transposed copy from the bf16 copies: ONE batched HIP launch."""
-        if not self._tcopies:
+        """Refresh every transposed / flipped copy from the bf16 copies: ONE batched HIP launch."""
+        if not self._tcopies and not self._fcopies:
             return
         if self._tjobs is None:
             rows = []
             for key, dst in self._tcopies.items():
                 r, c = self._tspecs[key]
                 src = self.fused_compute(list(key), (r, c))
-                rows.append([src.data_ptr(), dst.data_ptr(), r, c])
+                rows.append([src.data_ptr(), dst.data_ptr(), r, c, 0, 0])
+            for name, dst in self._fcopies.items():  # src [O][t][I] -> dst[i][8 - t][o], one job per tap
+                O, I = self.params[name].shape[:2]
+                base = self.compute_of(name).data_ptr()
+                for t in range(9):
+                    rows.append([base + 2 * t * I, dst.data_ptr() + 2 * (8 - t) * O, O, I, 9 * I, 9 * O])
             self._tjobs = (torch.tensor(rows, dtype=torch.int64).to(self.compute.device), len(rows),
                            max(r[2] for r in rows), max(r[3] for r in rows))
         if self.compute.device.type != "cuda":
             for key, dst in self._tcopies.items():  # host-side stores (CPU tests): plain copy
                 dst.copy_(self.fused_compute(list(key), self._tspecs[key]).t())
+            for name, dst in self._fcopies.items():
+                dst.copy_(self.compute_of(name).flip(2, 3).permute(1, 2, 3, 0))
             return
         from . import kernels as K
         jobs, n, mr, mc = self._tjobs

@@ -106,9 +106,9 @@ class _ConvBF16(torch.autograd.Function):
     plus an AccumulateGrad add)."""
 
     @staticmethod
-    def forward(ctx, x, w, w16, stride, padding):
+    def forward(ctx, x, w, w16, stride, padding, flipped=None):
         ctx.save_for_backward(x, w16)
-        ctx.w, ctx.conf = w, (stride, padding)
+        ctx.w, ctx.conf, ctx.flipped = w, (stride, padding), flipped
         cout = w16.shape[0]
         if _is_3x3_s1(w16, stride, padding) and _mmu_3x3(x.shape[1], cout, x.shape[0] * x.shape[2] * x.shape[3])[0]:
             y = torch.empty((x.shape[0], cout, x.shape[2], x.shape[3]), dtype=x.dtype, device=x.device,
@@ -137,7 +137,9 @@ class _ConvBF16(torch.autograd.Function):
                                                            1, (need_x and not mmu_x, need_w and not mmu_w, False))
         if mmu_x:
             dx = torch.empty_like(x, memory_format=cl)
-            K.conv3x3_implicit(dy, w16.flip(2, 3).permute(1, 2, 3, 0).contiguous(), dx)
+            # the store's flipped copy (refreshed with the bf16 filters), else one made here
+            wf = ctx.flipped() if ctx.flipped is not None else w16.flip(2, 3).permute(1, 2, 3, 0).contiguous()
+            K.conv3x3_implicit(dy, wf, dx)
         rw = None
         if mmu_w:
             g = ctx.w.grad
@@ -154,7 +156,7 @@ class _ConvBF16(torch.autograd.Function):
                 ctx.w.grad.add_(dw)
             else:
                 rw = dw.float()
-        return dx, rw, None, None, None
+        return dx, rw, None, None, None, None
 
 
 class _SkipGrad:
@@ -294,6 +296,17 @@ class StoreConv2d(nn.Conv2d):
                 return store.compute_of(src[1])
         return None
 
+    def _flipped_getter(self):
+        """() -> the store's flipped [Cin, 3, 3, Cout] copy of this 3x3 filter (created on the
+        first data-gradient call), or None"""
+        src = self._src
+        if src is None or self.kernel_size != (3, 3):
+            return None
+        store, name = src[0](), src[1]
+        if store is None or not hasattr(store, "flipped_filter"):
+            return None
+        return lambda: store.flipped_filter(name)
+
     def _is_1x1(self):
         return self.kernel_size == (1, 1) and self.stride == (1, 1) and self.padding == (0, 0)
 
@@ -312,7 +325,7 @@ class StoreConv2d(nn.Conv2d):
             x = x.contiguous(memory_format=torch.channels_last)
             if self._is_1x1():
                 return _Conv1x1.apply(x, self.weight, w16, sink)
-            return _ConvBF16.apply(x, self.weight, w16, self.stride, self.padding)
+            return _ConvBF16.apply(x, self.weight, w16, self.stride, self.padding, self._flipped_getter())
         if sink is not None:
             raise RuntimeError("StoreConv2d: a skip-gradient sink needs the bf16 1x1 path")
         return super().forward(x)

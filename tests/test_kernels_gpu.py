@@ -149,12 +149,25 @@ def test_transpose_bf16_batched(dev):
     shapes = [(2304, 768), (768, 3072), (100, 70), (65, 129), (1, 8)]
     srcs = [rnd(r, c, dev=dev, seed=70 + i) for i, (r, c) in enumerate(shapes)]
     dsts = [torch.full((c + 1, r), 5.0, dtype=torch.bfloat16, device=dev) for r, c in shapes]  # +1 guard row
-    jobs = torch.tensor([[s_.data_ptr(), d.data_ptr(), r, c] for s_, d, (r, c) in zip(srcs, dsts, shapes)],
+    jobs = torch.tensor([[s_.data_ptr(), d.data_ptr(), r, c, 0, 0] for s_, d, (r, c) in zip(srcs, dsts, shapes)],
                         dtype=torch.int64).to(dev)
     k.transpose_bf16_batched(jobs, len(shapes), max(r for r, _ in shapes), max(c for _, c in shapes), srcs[0])
     for s_, d, (r, c) in zip(srcs, dsts, shapes):
         assert torch.equal(d[:c], s_.t()), (r, c)
         assert (d[c:] == 5.0).all(), "wrote past the destination"
+
+
+def test_transpose_bf16_strided_flipped_filter(dev):
+    """strided jobs (row pitches): the 9 per-tap jobs the parameter store uses for the flipped
+    [Cin][3][3][Cout] copy of a channels-last 3x3 filter, bit-exact vs flip + permute."""
+    k = K()
+    O, I = 384, 256
+    w = rnd(O, I, 3, 3, dev=dev, seed=3).contiguous(memory_format=torch.channels_last)
+    dst = torch.full((I, 3, 3, O), 7.0, dtype=torch.bfloat16, device=dev)
+    rows = [[w.data_ptr() + 2 * t * I, dst.data_ptr() + 2 * (8 - t) * O, O, I, 9 * I, 9 * O] for t in range(9)]
+    jobs = torch.tensor(rows, dtype=torch.int64).to(dev)
+    k.transpose_bf16_batched(jobs, 9, O, I, w)
+    assert torch.equal(dst, w.flip(2, 3).permute(1, 2, 3, 0))
 
 
 @pytest.mark.parametrize("Kd", [256, 768])
