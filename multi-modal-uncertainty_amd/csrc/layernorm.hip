@@ -7,6 +7,7 @@
 // (MMU_EPI_BIAS_DROP_RES: same (seed, m*H+n) quad stream) and emits per-block
 // partial column sums for dgamma / dbeta / dbias, so the LN-affine and the Linear
 // bias gradients cost no extra pass over the activations.
+#include <cstdlib>
 #include "mmu_common.h"
 #include "mmu_internal.h"
 
@@ -62,6 +63,92 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16* __restrict__ X,
     if (two) load(row + 4, xb);
     process(row, xa);
     if (two) process(row + 4, xb);
+  }
+}
+
+// forward, 16-B accesses: a wave owns a PAIR of rows (2 x 32 NV chunks of 8 bf16 = NV slabs
+// of 64 lanes: chunk q = 64 i + l of slab i is row q / (32 NV), columns 8 (q % (32 NV)) ..+7),
+// two pairs in flight per wave; the rows' sums are two masked wave reductions.  Needs both
+// rows of a pair in one parameter group (group_rows even, or one group).  (The same layout
+// for the backward measured slower than its row-per-wave kernel: 8 f32 column accumulators
+// per chunk x 3 quantities hold it at 2 waves / SIMD.)
+constexpr int LN2_PAIRS = 8;  // pairs per block: 4 waves x 2
+template <int NV>  // H = 256 * NV
+__global__ __launch_bounds__(256) void ln_fwd2_kernel(const bf16* __restrict__ X, const float* __restrict__ w,
+                                                      const float* __restrict__ b, bf16* __restrict__ Y,
+                                                      float* __restrict__ mean, float* __restrict__ rstd,
+                                                      int64_t rows, float eps, int64_t group_rows, int64_t pstride) {
+  constexpr int H = 256 * NV, CPR = 32 * NV;  // chunks per row
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int cc[NV];
+  bool hb[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int q = 64 * i + l;
+    hb[i] = q >= CPR;
+    cc[i] = 8 * (hb[i] ? q - CPR : q);
+  }
+  const int64_t p0 = (int64_t)blockIdx.x * LN2_PAIRS;
+  const int64_t np = (rows + 1) / 2;
+  const int64_t pend = p0 + LN2_PAIRS < np ? p0 + LN2_PAIRS : np;
+  for (int64_t pr = p0 + wv; pr < pend; pr += 8) {
+    bf16x8 xa[NV], xb[NV];
+    const bool two = pr + 4 < pend;
+    auto load = [&](int64_t pp, bf16x8 (&x)[NV]) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int64_t row = 2 * pp + (hb[i] ? 1 : 0);
+        x[i] = row < rows ? *(const bf16x8*)(X + row * H + cc[i]) : bf16x8{};
+      }
+    };
+    auto process = [&](int64_t pp, const bf16x8 (&x)[NV]) {
+      float v[NV][8];
+      float sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        float s = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { v[i][e] = bf2f(x[i][e]); s += v[i][e]; }
+        if (hb[i]) sb += s; else sa += s;
+      }
+      const float mua = wave_sum(sa) / H, mub = wave_sum(sb) / H;
+      float qa = 0.f, qb = 0.f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const float mu = hb[i] ? mub : mua;
+        float q = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { const float d = v[i][e] - mu; q += d * d; }
+        if (hb[i]) qb += q; else qa += q;
+      }
+      const float rsa = rsqrtf(wave_sum(qa) / H + eps), rsb = rsqrtf(wave_sum(qb) / H + eps);
+      const int64_t ra = 2 * pp;
+      const float* wr = w + (ra / group_rows) * pstride;
+      const float* br = b + (ra / group_rows) * pstride;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int64_t row = ra + (hb[i] ? 1 : 0);
+        if (row >= rows) continue;
+        const float mu = hb[i] ? mub : mua, rs = hb[i] ? rsb : rsa;
+        const float4 w0 = *(const float4*)(wr + cc[i]), w1 = *(const float4*)(wr + cc[i] + 4);
+        const float4 b0 = *(const float4*)(br + cc[i]), b1 = *(const float4*)(br + cc[i] + 4);
+        const float ww[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        bf16x8 y;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) y[e] = f2bf((v[i][e] - mu) * rs * ww[e] + bb[e]);
+        *(bf16x8*)(Y + row * H + cc[i]) = y;
+      }
+      if (mean && l == 0) {
+        mean[ra] = mua;
+        rstd[ra] = rsa;
+        if (ra + 1 < rows) { mean[ra + 1] = mub; rstd[ra + 1] = rsb; }
+      }
+    };
+    load(pr, xa);
+    if (two) load(pr + 4, xb);
+    process(pr, xa);
+    if (two) process(pr + 4, xb);
   }
 }
 
@@ -172,8 +259,26 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dY
   }
 }
 
+static bool ln_v2() {
+  const char* e = getenv("MMU_LN_V2");  // 0 = the 8-B row-per-wave forward (A/B)
+  return !(e && e[0] == '0');
+}
+
 void layernorm_fwd_launch(const bf16* X, const float* w, const float* b, bf16* Y, float* mean, float* rstd,
                           int64_t rows, int64_t H, float eps, int64_t group_rows, int64_t pstride, hipStream_t s) {
+  if (ln_v2() && (group_rows % 2 == 0 || group_rows >= rows || pstride == 0) && H % 256 == 0 && H <= 1024) {
+    const dim3 g2((unsigned)(((rows + 1) / 2 + LN2_PAIRS - 1) / LN2_PAIRS));
+#define LNF2(NV) hipLaunchKernelGGL(ln_fwd2_kernel<NV>, g2, dim3(256), 0, s, X, w, b, Y, mean, rstd, rows, eps, \
+                                    group_rows, pstride)
+    switch (H / 256) {
+      case 1: LNF2(1); break;
+      case 2: LNF2(2); break;
+      case 3: LNF2(3); break;
+      default: LNF2(4); break;
+    }
+#undef LNF2
+    return;
+  }
   const dim3 g((unsigned)((rows + LN_FWD_ROWS - 1) / LN_FWD_ROWS));
 #define LNF(NV) hipLaunchKernelGGL(ln_fwd_kernel<NV>, g, dim3(256), 0, s, X, w, b, Y, mean, rstd, rows, eps, \
                                    group_rows, pstride)

@@ -421,6 +421,27 @@ def test_attention_dropout_inference_matches_training_forward(dev, B, L):
 
 
 # ----------------------------------------------------------------------------- layernorm
+@pytest.mark.parametrize("H,groups,rows_per", [(768, 3, 130), (768, 2, 77), (256, 1, 9), (1024, 2, 64)])
+def test_layernorm_fwd_grouped(dev, H, groups, rows_per, monkeypatch):
+    """row groups with their own affine parameters (the K ensemble members in one launch):
+    both forward kernels (16-B row pairs when the group size is even, else row per wave)
+    against torch per group; odd total row counts."""
+    k = K()
+    rows = groups * rows_per
+    X = rnd(rows, H, dev=dev, seed=31, scale=2.0)
+    w = torch.randn(groups, H, device=dev) * 0.1 + 1
+    b = torch.randn(groups, H, device=dev) * 0.1
+    ref = torch.cat([torch.nn.functional.layer_norm(X[g * rows_per:(g + 1) * rows_per].float(), (H,), w[g], b[g],
+                                                    eps=1e-12) for g in range(groups)])
+    for v2 in ("1", "0"):
+        monkeypatch.setenv("MMU_LN_V2", v2)
+        Y = torch.empty_like(X)
+        mean, rstd = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+        k.layernorm_fwd(X, w, b, Y, mean, rstd, group_rows=rows_per, param_stride=H)
+        close(Y, ref)
+        torch.testing.assert_close(mean, X.float().mean(1), rtol=1e-4, atol=1e-4)
+
+
 def test_layernorm_fwd_bwd(dev):
     k = K()
     rows, H, p, seed = 333, 768, 0.1, 77

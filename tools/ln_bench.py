@@ -20,7 +20,13 @@ def main():
     dX, dXd = torch.empty_like(X), torch.empty_like(X)
     P = K.ln_parts(M)
     pw, pb, pbias = (torch.empty(P, H, device=dev) for _ in range(3))
+    os.environ["MMU_LN_V2"] = "0"
+    tf0 = timed(lambda: K.layernorm_fwd(X, w, b, Y, mean, rstd), 10)
+    Y0 = Y.clone()
+    os.environ["MMU_LN_V2"] = "1"
     tf = timed(lambda: K.layernorm_fwd(X, w, b, Y, mean, rstd), 10)
+    print(f"LN fwd row-per-wave 8-B {tf0 * 1e3:7.1f} us ({2 * M * H * 2 / tf0 / 1e9:5.2f} TB/s)  identical: "
+          f"{bool(torch.equal(Y0, Y))}", flush=True)
     tb = timed(lambda: K.layernorm_bwd(dY, X, mean, rstd, w, dX, dXd, 0.1, 3, pw, pb, pbias), 10)
     nb = M * H * 2
     print(f"LN fwd {tf * 1e3:7.1f} us ({2 * nb / tf / 1e9:5.2f} TB/s)   bwd {tb * 1e3:7.1f} us "
