@@ -5,8 +5,11 @@ The reference is single-device (train.py:307-310); this is the build's DP layer
 order backward completes them (src/params.py), so buckets are plain contiguous
 slices: [classifier + pooler + layer 11 ...], ..., [layer 0 ...], [embeddings +
 image projection + ResNet].  Each fused BERT layer's backward reports when its
-weight gradients are enqueued; as soon as a bucket's layers are all done its
-all-reduce (torch.distributed backend "nccl" = RCCL) is issued.  The collective
+weight gradients are enqueued, the embedding backward when the embedding tables'
+are, and each ResNet residual block when the gradient of its input is formed (a
+tensor hook on the block input, registered by a forward pre-hook: by then every
+parameter gradient of the block is enqueued); as soon as a bucket's parts are all
+done its all-reduce (torch.distributed backend "nccl" = RCCL) is issued.  The collective
 runs on RCCL's own stream, ordered after the producing kernels by an event, so it
 overlaps the backward of the layers below.  ``finish()`` issues what is left and
 makes the compute stream wait before the optimizer step.  Mean = sum / world size
@@ -28,7 +31,9 @@ class GradBucketer:
         self.enc._grad_ready_hook = self._on_ready
         self.pending = []
         self.launched = set()
+        self.done_segs = set()
         self.enabled = True
+        self._hooks = [m.register_forward_pre_hook(self._block_pre_hook(k)) for k, m in self._blocks.items()]
 
     def _plan(self):
         st = self.store
@@ -56,12 +61,73 @@ class GradBucketer:
         assert head_end == 0 or buckets[0]["start"] == 0
         tail_start = buckets[-1]["end"]
         total = st.numel()
-        step = max(self.bucket_bytes // 4, 1)
-        for s in range(tail_start, total, step):  # embeddings + projection + ResNet: issued at finish()
-            buckets.append({"start": s, "end": min(total, s + step), "layers": set()})
+        # tail: embeddings + image projection ("emb"), then the ResNet residual blocks in
+        # backward order (layer4 last block ... layer1 first block), then the stem: buckets of
+        # whole segments, each issued when its segments' gradients are all enqueued (the stem's
+        # at finish())
+        segs = []  # (key, start, end) in flat order
+        for n in st.names:
+            o = st.offsets[n]
+            if o < tail_start:
+                continue
+            key = self._segment_of(n)
+            if segs and segs[-1][0] == key:
+                segs[-1][2] = max(segs[-1][2], o + st.params[n].numel())
+            else:
+                segs.append([key, o, o + st.params[n].numel()])
+        assert not segs or segs[0][1] == tail_start
+        cur = None
+        for key, o0, o1 in segs:
+            if cur is None:
+                cur = {"start": o0, "end": o1, "layers": set(), "segs": {key}}
+            else:
+                cur["end"] = o1
+                cur["segs"].add(key)
+            if 4 * (cur["end"] - cur["start"]) >= self.bucket_bytes:
+                buckets.append(cur)
+                cur = None
+        if cur is not None:
+            buckets.append(cur)
         self.buckets = buckets
+        self.seg_to_buckets = {}
+        for b, bk in enumerate(buckets):
+            for key in bk.get("segs", ()):
+                self.seg_to_buckets.setdefault(key, []).append(b)
+        prefix = f"{self.enc._prefix}img_encoder."
+        mods = dict(self.enc.img_encoder.named_modules(prefix=prefix[:-1]))
+        self._blocks = {key: mods[key] for key, _, _ in segs if key not in ("emb", "stem") and key in mods}
         self.layer_to_bucket = {i: b for b, bk in enumerate(buckets) for i in bk["layers"]}
         self.done_layers = set()
+
+    def _segment_of(self, name):
+        """tail segment of a parameter: "emb" (text / image embeddings), the ResNet residual
+        block ``<prefix>img_encoder.model.<stage>.<block>`` (stages 4..7 = layer1..layer4), or
+        "stem"."""
+        prefix = f"{self.enc._prefix}img_encoder."
+        if not name.startswith(prefix):
+            return "emb"
+        parts = name[len(prefix):].split(".")
+        if len(parts) >= 3 and parts[0] == "model" and parts[1] in ("4", "5", "6", "7"):
+            return prefix + ".".join(parts[:3])
+        return "stem"
+
+    def _block_pre_hook(self, key):
+        def pre(module, args):
+            x = args[0] if args else None
+            if (self.enabled and self.world > 1 and torch.is_grad_enabled() and isinstance(x, torch.Tensor)
+                    and x.requires_grad):
+                x.register_hook(lambda g: self._on_segment(key))
+        return pre
+
+    def _on_segment(self, key):
+        """a tail segment's gradients are all enqueued: issue the buckets it completes"""
+        if not self.enabled or self.world == 1:
+            return
+        self.done_segs.add(key)
+        for b in self.seg_to_buckets.get(key, ()):
+            segs = self.buckets[b]["segs"]
+            if "stem" not in segs and segs <= self.done_segs:
+                self._issue(b)
 
     def _issue(self, b):
         if b in self.launched:
@@ -73,6 +139,9 @@ class GradBucketer:
         self.launched.add(b)
 
     def _on_ready(self, lw):
+        if lw == "embeddings":
+            self._on_segment("emb")
+            return
         if not self.enabled or self.world == 1 or not hasattr(lw, "module"):
             return
         i = self.enc._lw.index(lw)
@@ -90,7 +159,7 @@ class GradBucketer:
         for w in self.pending:
             w.wait()
         self.store.grad.mul_(1.0 / self.world)
-        self.pending, self.launched, self.done_layers = [], set(), set()
+        self.pending, self.launched, self.done_layers, self.done_segs = [], set(), set(), set()
 
 
 def average_buffers(model, group=None):

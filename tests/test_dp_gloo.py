@@ -39,9 +39,14 @@ def _worker(rank, world, port, q):
         for lw in reversed(model.enc._lw):  # backward order: top layer first
             bk._on_ready(lw)
             launched.append(len(bk.launched))
+        n_enc = len(bk.launched)
+        bk._on_ready("embeddings")  # then the embeddings, then the trunk's blocks (backward order)
+        for key in bk._blocks:
+            bk._on_segment(key)
+        tail = len(bk.launched) - n_enc
         bk.finish()
         q.put((rank, w_sum, model.store.grad.double().sum().item(), model.store.grad[:1000].tolist(), launched,
-               len(bk.buckets)))
+               len(bk.buckets), tail))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover - reported to the parent
         import traceback
@@ -69,10 +74,11 @@ def test_bucketed_allreduce_matches_mean():
     from src.testing import small_args
     n = MultimodalBertClf(small_args()).store.numel()
     mean = sum(torch.randn(n, generator=g).double() for g in gens) / world
-    for rank, w_sum, gsum, head, launched, nb in res:
+    for rank, w_sum, gsum, head, launched, nb, tail in res:
         assert abs(gsum - float(mean.sum())) < 1e-3 * abs(float(mean.sum())) + 1e-2
         torch.testing.assert_close(torch.tensor(head, dtype=torch.float64), mean[:1000], rtol=1e-5, atol=1e-6)
         assert launched[-1] >= 1, "no bucket launched during backward"
+        assert tail >= 1, "no embedding / trunk bucket launched before finish()"
     assert res[0][1] == res[1][1], "ranks start from different weights"
 
 
