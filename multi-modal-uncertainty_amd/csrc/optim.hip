@@ -36,7 +36,16 @@ __global__ __launch_bounds__(256) void adam_sqnorm_kernel(AdamDev a) {
   }
   const float* g = a.grads + a.table[7 * tid] + start;
   float s = 0.f;
-  for (int64_t i = threadIdx.x; i < len; i += 256) { float x = g[i]; s += x * x; }
+  // 16-B loads over the aligned body, scalar head (to 16-B alignment) and tail
+  const int64_t head = ((16 - ((uintptr_t)g & 15)) & 15) / 4 < len ? ((16 - ((uintptr_t)g & 15)) & 15) / 4 : len;
+  for (int64_t i = threadIdx.x; i < head; i += 256) { const float x = g[i]; s += x * x; }
+  const int64_t nv = (len - head) / 4;
+  const float4* g4 = (const float4*)(g + head);
+  for (int64_t i = threadIdx.x; i < nv; i += 256) {
+    const float4 x = g4[i];
+    s += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
+  }
+  for (int64_t i = head + 4 * nv + threadIdx.x; i < len; i += 256) { const float x = g[i]; s += x * x; }
   __shared__ float red[4];
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
@@ -83,18 +92,39 @@ __global__ __launch_bounds__(256) void adam_update_kernel(AdamDev a) {
   float* v = a.v + off;
   const float* g = a.grads + off;
   bf16* cp = T[3] >= 0 ? a.bf16_copy + T[3] + start : nullptr;
-  const float b1 = a.b1, b2 = a.b2, c1 = 1.f - a.b1, c2 = 1.f - a.b2;
-  for (int64_t i = threadIdx.x; i < len; i += 256) {
-    const float gr = g[i] * coef;
-    const float mm = b1 * m[i] + c1 * gr;
-    const float vv = b2 * v[i] + c2 * gr * gr;
-    m[i] = mm;
-    v[i] = vv;
-    float u = mm / (sqrtf(vv) + a.eps);
-    if (wd > 0.f) u += wd * p[i];
-    const float np = p[i] - lr * u;
-    p[i] = np;
-    if (cp) cp[i] = f2bf(np);
+  const float b1 = a.b1, b2 = a.b2, c1 = 1.f - a.b1, c2 = 1.f - a.b2, eps = a.eps;
+  auto one = [&](float pi, float gi, float mi, float vi, float& po, float& mo, float& vo) {
+    const float gr = gi * coef;
+    mo = b1 * mi + c1 * gr;
+    vo = b2 * vi + c2 * gr * gr;
+    float u = mo / (sqrtf(vo) + eps);
+    if (wd > 0.f) u += wd * pi;
+    po = pi - lr * u;
+  };
+  // 16-B accesses (8-B bf16 stores) when the chunk's f32 offset and its bf16 copy offset are
+  // multiples of 4 elements (every tensor but a few odd-sized biases), else scalar
+  const bool vec = (off & 3) == 0 && (!cp || ((T[3] + start) & 3) == 0);
+  const int64_t nv = vec ? len / 4 : 0;
+  for (int64_t i = threadIdx.x; i < nv; i += 256) {
+    const float4 pv = ((const float4*)p)[i], gv = ((const float4*)g)[i];
+    const float4 mv = ((const float4*)m)[i], vv = ((const float4*)v)[i];
+    float4 po, mo, vo;
+    one(pv.x, gv.x, mv.x, vv.x, po.x, mo.x, vo.x);
+    one(pv.y, gv.y, mv.y, vv.y, po.y, mo.y, vo.y);
+    one(pv.z, gv.z, mv.z, vv.z, po.z, mo.z, vo.z);
+    one(pv.w, gv.w, mv.w, vv.w, po.w, mo.w, vo.w);
+    ((float4*)m)[i] = mo;
+    ((float4*)v)[i] = vo;
+    ((float4*)p)[i] = po;
+    if (cp) ((bf16x4*)cp)[i] = bf16x4{f2bf(po.x), f2bf(po.y), f2bf(po.z), f2bf(po.w)};
+  }
+  for (int64_t i = 4 * nv + threadIdx.x; i < len; i += 256) {
+    float po, mo, vo;
+    one(p[i], g[i], m[i], v[i], po, mo, vo);
+    m[i] = mo;
+    v[i] = vo;
+    p[i] = po;
+    if (cp) cp[i] = f2bf(po);
   }
 }
 
