@@ -13,9 +13,9 @@ import re
 from collections import defaultdict
 
 CATS = [
-    ("mmu GEMM (BERT layers + ResNet 1x1 convs)", r"mmu::gemm_|gemm_(small|big)_kernel|mmu::splitk"),
+    ("mmu GEMM (BERT layers + ResNet 1x1 / 3x3 convs)", r"mmu::gemm_|gemm_(small|big)_kernel|mmu::splitk"),
     ("mmu attention", r"mmu::attn_|mmu::seqattn_"),
-    ("mmu LayerNorm", r"mmu::ln_|ln_fwd_kernel|ln_bwd_kernel"),
+    ("mmu LayerNorm", r"mmu::ln_|ln_fwd_kernel|ln_fwd2_kernel|ln_bwd_kernel"),
     ("mmu embed / pool", r"mmu::embed|mmu::row_pool|embed_fwd_kernel|embed_bwd"),
     ("mmu BertAdam", r"mmu::adam"),
     ("mmu BatchNorm (ResNet)", r"mmu::bn_|bn_(stats|apply|bwd)"),
