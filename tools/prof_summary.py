@@ -72,6 +72,21 @@ def main():
              f"dispatches {len(win)}", "", "| category | launches | ms | % of kernel time |", "|---|---|---|---|"]
     for c, (n, ms) in sorted(per_cat.items(), key=lambda kv: -kv[1][1]):
         lines.append(f"| {c} | {n} | {ms:.2f} | {100 * ms / busy:.1f} |")
+    # the launches bench.py's roofline times with HIP events: the big-tile GEMMs between the
+    # embedding forward and the embedding backward (the encoder of the step)
+    inside, bert = False, []
+    for r in win:
+        k = r["Kernel_Name"]
+        if "embed_fwd" in k:
+            inside = True
+        elif "embed_bwd" in k:
+            inside = False
+        elif inside and re.search(r"gemm_big_kernel", k):
+            bert.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    if bert:
+        lines += ["", f"BERT-layer GEMM launches (big-tile `mmu_gemm` between embed_fwd and embed_bwd; what "
+                      f"bench.py's roofline times with HIP events): {len(bert)} launches, mean "
+                      f"{sum(bert) / len(bert):.1f} us, total {sum(bert) / 1e3:.2f} ms"]
     lines += ["", "| kernel | launches | total ms | avg us |", "|---|---|---|---|"]
     for k, (n, ms) in sorted(per_kernel.items(), key=lambda kv: -kv[1][1])[:40]:
         lines.append(f"| `{k[:120]}` | {n} | {ms:.2f} | {1000 * ms / n:.1f} |")
