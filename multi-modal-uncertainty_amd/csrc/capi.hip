@@ -131,9 +131,12 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
   // tile-order group height, measured on the BERT shapes (tools/gemm_bench.py --var
   // MMU_GEMM_GROUP): row-major for <= 3 column tiles, 2 with an N-major B (dY.W2), 8 for the
   // wide forward products (QKV 0.496 -> 0.457 ms, W1+GELU 0.888 -> 0.832 ms)
-  p.group_m = p.tiles_n <= 3 ? 1 : (b_kmajor ? 8 : 2);
-  if (const char* g = getenv("MMU_GEMM_GROUP")) p.group_m = atoi(g) > 0 ? atoi(g) : p.group_m;
   int kind = MMU_EPI_STORE;
+  if (epi) kind = epi->kind;
+  // (and 2 for the dGELU product dY2.W2, whose epilogue streams the [M, 3072] gelu' rows:
+  // 0.888 -> 0.756 ms with a K-major B, profiles/r2_gemm_group_dz.txt)
+  p.group_m = p.tiles_n <= 3 ? 1 : ((b_kmajor && kind != MMU_EPI_DGELU) ? 8 : 2);
+  if (const char* g = getenv("MMU_GEMM_GROUP")) p.group_m = atoi(g) > 0 ? atoi(g) : p.group_m;
   if (epi) {
     kind = epi->kind;
     p.accumulate = epi->accumulate;

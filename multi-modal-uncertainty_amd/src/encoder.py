@@ -51,8 +51,9 @@ class LayerWeights:
             setattr(self, k + "16", s.fused_compute(self._names[k], self._shapes[k]))
         # K-major copies for the data-gradient products dX = dY W (B = W^T): the GEMM's
         # K-contiguous B path runs 9-17 % faster than its N-contiguous one on these shapes
-        # (profiles/r2_gemm_bt_ab.txt); dZ = dY2 W2 measured no faster and keeps W2 as is
-        for k in ("wqkv", "wo", "w1"):
+        # (profiles/r2_gemm_bt_ab.txt); dZ = dY2 W2 too, with 2-row tile groups (0.848 ->
+        # 0.756 ms, profiles/r2_gemm_group_dz.txt)
+        for k in ("wqkv", "wo", "w1", "w2"):
             setattr(self, k + "t16", s.transposed_compute(self._names[k], self._shapes[k]))
         self.anchor = s.params[self._names["wqkv"][0]]
 
@@ -148,7 +149,7 @@ def layer_backward(lw, saved, dY, keymask, B, L, p_attn, p_hid, seeds, wgrad):
         side.run(w2, pw, pb, pbias, dY2, Hh)
     dZ = torch.empty(M, FFN, dtype=bf16, device=dev)
     # dgelu epilogue also accumulates the intermediate-bias gradient (column sums of dZ) in place
-    K.gemm(dY2, HID, True, lw.w216, FFN, False, dZ, FFN, M, FFN, HID,
+    K.gemm(dY2, HID, True, lw.w2t16, HID, True, dZ, FFN, M, FFN, HID,
            epi=K.epilogue(K.EPI_DGELU, aux=Z, colsum=lw.g_b1 if wgrad else None))
     if wgrad:
         side.run(lambda: K.gemm(dZ, FFN, False, A, HID, False, lw.g_w1, HID, FFN, HID, M, epi=acc), dZ, A)

@@ -142,10 +142,10 @@ class BlockFunction(torch.autograd.Function):
         m1, r1 = torch.empty(M, dtype=f32, device=dev), torch.empty(M, dtype=f32, device=dev)
         K.layernorm_fwd(X, l1w, l1b, h1, m1, r1, LN_EPS)
         Win, Wo, W1, W2 = (t.to(bf16) for t in (win, wo, w1, w2))
-        # K-major copies for the data-gradient products dX = dY W (B = W^T K-contiguous: the
-        # GEMM's faster B path, as the BERT layers' transposed copies); dZ = dT W2
-        # keeps W2 as is (no faster K-major on the BERT shapes)
-        Wint, Wot, W1t = (t.t().contiguous() for t in (Win, Wo, W1))
+        # K-major copies for the data-gradient products dX = dY W and dZ = dT W2 (B = W^T
+        # K-contiguous: the GEMM's faster B path, as the BERT layers' transposed copies,
+        # DESIGN.md §2)
+        Wint, Wot, W1t, W2t = (t.t().contiguous() for t in (Win, Wo, W1, W2))
         qkv = torch.empty(M, 3 * E, dtype=bf16, device=dev)
         K.gemm(h1, E, True, Win, E, True, qkv, 3 * E, M, 3 * E, E, epi=K.epilogue(K.EPI_STORE, bias=bin_))
         O = torch.empty(M, E, dtype=bf16, device=dev)
@@ -163,7 +163,7 @@ class BlockFunction(torch.autograd.Function):
         y = torch.empty(M, E, dtype=bf16, device=dev)
         K.gemm(Hh, 4 * E, True, W2, 4 * E, True, y, E, M, E, 4 * E,
                epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=b2, residual=x1))
-        ctx.save_for_backward(X, h1, m1, r1, qkv, O, lse2, x1, h2, m2, r2, Hh, Zd, Wint, Wot, W1t, W2, l1w, l2w)
+        ctx.save_for_backward(X, h1, m1, r1, qkv, O, lse2, x1, h2, m2, r2, Hh, Zd, Wint, Wot, W1t, W2t, l1w, l2w)
         ctx.meta = (B, L, E, heads)
         if e0 is not None:
             _enc._block_events.append((e0, _enc._mark()))
@@ -171,7 +171,7 @@ class BlockFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        (X, h1, m1, r1, qkv, O, lse2, x1, h2, m2, r2, Hh, Zd, Wint, Wot, W1t, W2, l1w, l2w) = ctx.saved_tensors
+        (X, h1, m1, r1, qkv, O, lse2, x1, h2, m2, r2, Hh, Zd, Wint, Wot, W1t, W2t, l1w, l2w) = ctx.saved_tensors
         B, L, E, heads = ctx.meta
         e0 = _enc._mark()
         M, dev, f32 = B * L, X.device, torch.float32
@@ -186,7 +186,7 @@ class BlockFunction(torch.autograd.Function):
         K.gemm(dT, E, False, Hh, 4 * E, False, g["w2"], 4 * E, E, 4 * E, M, epi=st)
         dZ = torch.empty(M, 4 * E, dtype=bf16, device=dev)
         g["b1"] = torch.zeros(4 * E, dtype=f32, device=dev)
-        K.gemm(dT, E, True, W2, 4 * E, False, dZ, 4 * E, M, 4 * E, E,
+        K.gemm(dT, E, True, W2t, E, True, dZ, 4 * E, M, 4 * E, E,
                epi=K.epilogue(K.EPI_DGELU, aux=Zd, colsum=g["b1"]))
         g["w1"] = torch.empty(4 * E, E, dtype=f32, device=dev)
         K.gemm(dZ, 4 * E, False, h2, E, False, g["w1"], E, 4 * E, E, M, epi=st)
