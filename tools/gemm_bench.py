@@ -71,6 +71,7 @@ def main():
     out768, out2304, out3072 = (torch.empty(M, n, dtype=bf, device=dev) for n in (HID, 3 * HID, FFN))
     Zs = rnd(M, FFN)
     gW = torch.zeros(FFN, HID, device=dev)
+    gW2, gWq, gWo = torch.zeros(HID, FFN, device=dev), torch.zeros(3 * HID, HID, device=dev), torch.zeros(HID, HID, device=dev)
     cs = torch.zeros(FFN, device=dev)
     cases = [
         ("fwd qkv  X.Wqkv^T+b", M, 3 * HID, HID,
@@ -140,6 +141,18 @@ def main():
          lambda: K.gemm(dZ, FFN, False, A, HID, False, gW, HID, FFN, HID, M,
                         epi=K.epilogue(K.EPI_STORE, accumulate=True)),
          lambda: torch.matmul(dZ.t(), A)),
+        ("wgrad W2 dY^T.H f32acc", HID, FFN, M,
+         lambda: K.gemm(dY, HID, False, Hh, FFN, False, gW2, FFN, HID, FFN, M,
+                        epi=K.epilogue(K.EPI_STORE, accumulate=True)),
+         lambda: torch.matmul(dY.t(), Hh)),
+        ("wgrad Wqkv dQKV^T.X f32acc", 3 * HID, HID, M,
+         lambda: K.gemm(dqkv, 3 * HID, False, X, HID, False, gWq, HID, 3 * HID, HID, M,
+                        epi=K.epilogue(K.EPI_STORE, accumulate=True)),
+         lambda: torch.matmul(dqkv.t(), X)),
+        ("wgrad Wo dS1^T.O f32acc", HID, HID, M,
+         lambda: K.gemm(dY, HID, False, O, HID, False, gWo, HID, HID, HID, M,
+                        epi=K.epilogue(K.EPI_STORE, accumulate=True)),
+         lambda: torch.matmul(dY.t(), O)),
     ]
     vals = a.vals.split(",")
     print(f"{'gemm':26s} {'M':>7s} {'N':>5s} {'K':>7s} " + " ".join(f"{(a.var[-8:] + '=' + v)[-18:]:>18s}" for v in vals)
