@@ -86,8 +86,11 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor,
 /* Sum `parts` rows of a [parts, N] f32 partial table into out[N] (+= if accumulate). */
 int mmu_colsum_reduce(const float* partial, int64_t parts, int64_t N, float* out,
                       int accumulate, mmu_stream_t stream);
-/* Column sums of a bf16 [M, N] matrix into out[N] f32 (+= if accumulate): the bias grad
- * of the fused QKV projection.  `partial` is unused (kept for ABI stability; may be NULL). */
+/* Column sums of a bf16 [M, N] matrix into out[N] f32 (+= if accumulate): the bias grads
+ * of the FLAVA blocks' projections (src/model.py).  `partial` (may be NULL): f32 scratch
+ * of at least ceil(M / 64) * N floats; with it the row blocks are sized for ~1 K
+ * workgroups and fold through per-block partial rows (mmu_colsum_reduce), without it
+ * 1024-row blocks add into out by float atomics. */
 int mmu_colsum_bf16(const void* X, int64_t M, int64_t N, int64_t ldx, float* partial,
                     float* out, int accumulate, mmu_stream_t stream);
 

@@ -1153,15 +1153,18 @@ void colsum_reduce_launch(const float* part, int64_t parts, int64_t N, float* ou
                      dim3(256), 0, s, part, parts, N, out);
 }
 
-// bf16 [M,N] column sums: each block sums 256 rows x 512 columns, one atomic per column
-// column sums of a bf16 [M, N] matrix: block = 64 octets of columns x COLSUM_BF16_ROWS rows
-// (4 waves, 4 loads in flight each), one float atomic per column per block (~M/1024 atomics
-// per address: 256-row blocks put ~140 same-address atomics in the L2 queue at M = 35 K)
+// column sums of a bf16 [M, N] matrix: block = 64 octets of columns x rpb rows (4 waves, 4
+// loads in flight each).  With a scratch table the blocks write per-block partial rows
+// (no atomics) that colsum_reduce_kernel folds, so the row blocks can be short enough to put
+// ~1 K blocks on the chip; without one, rpb = 1024 rows and one float atomic per column per
+// block (short blocks would pile hundreds of same-address atomics into the L2 queue).
 constexpr int COLSUM_BF16_ROWS = 1024;
+constexpr int COLSUM_BF16_MIN_ROWS = 64;
 __global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16* __restrict__ X, int64_t M, int64_t N,
-                                                          int64_t ld, float* __restrict__ out) {
-  const int64_t r0 = (int64_t)blockIdx.y * COLSUM_BF16_ROWS;
-  const int64_t r1 = r0 + COLSUM_BF16_ROWS < M ? r0 + COLSUM_BF16_ROWS : M;
+                                                          int64_t ld, int64_t rpb, float* __restrict__ part,
+                                                          float* __restrict__ out) {
+  const int64_t r0 = (int64_t)blockIdx.y * rpb;
+  const int64_t r1 = r0 + rpb < M ? r0 + rpb : M;
   const int64_t c = ((int64_t)blockIdx.x * 64 + (threadIdx.x & 63)) * 8;
   const int wv = threadIdx.x >> 6;
   __shared__ float red[4][64 * 8];
@@ -1187,21 +1190,44 @@ __global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16* __restrict
   for (int e = 0; e < 8; ++e) red[wv][(threadIdx.x & 63) * 8 + e] = s[e];
   __syncthreads();
   if (wv == 0 && c < N) {
+    float t[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int q = (threadIdx.x & 63) * 8 + e;
-      atomicAdd(out + c + e, red[0][q] + red[1][q] + red[2][q] + red[3][q]);
+      t[e] = red[0][q] + red[1][q] + red[2][q] + red[3][q];
+    }
+    if (part) {
+      float4* d = (float4*)(part + (int64_t)blockIdx.y * N + c);
+      d[0] = make_float4(t[0], t[1], t[2], t[3]);
+      d[1] = make_float4(t[4], t[5], t[6], t[7]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) atomicAdd(out + c + e, t[e]);
     }
   }
 }
 
 void colsum_bf16_launch(const bf16* X, int64_t M, int64_t N, int64_t ld, float* part, float* out, int acc,
                         hipStream_t s) {
-  (void)part;
+  const int64_t gx = (N / 8 + 63) / 64;
+  static const bool v1 = getenv("MMU_COLSUM_V1") && atoi(getenv("MMU_COLSUM_V1"));  // A/B: the atomic-only path
+  if (v1) part = nullptr;
+  int64_t rpb = COLSUM_BF16_ROWS;
+  if (part) {  // ~1 K blocks: rows per block a multiple of 16 in [64, 1024]
+    rpb = (M * gx + 1023) / 1024;
+    rpb = (rpb + 15) / 16 * 16;
+    rpb = rpb < COLSUM_BF16_MIN_ROWS ? COLSUM_BF16_MIN_ROWS : rpb > COLSUM_BF16_ROWS ? COLSUM_BF16_ROWS : rpb;
+  }
+  const int64_t gy = (M + rpb - 1) / rpb;
+  if (part && gy > 1) {
+    hipLaunchKernelGGL(colsum_bf16_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, s, X, M, N, ld, rpb, part,
+                       (float*)nullptr);
+    colsum_reduce_launch(part, gy, N, out, acc, s);
+    return;
+  }
   if (!acc) (void)hipMemsetAsync(out, 0, sizeof(float) * N, s);
-  hipLaunchKernelGGL(colsum_bf16_kernel, dim3((unsigned)((N / 8 + 63) / 64),
-                                              (unsigned)((M + COLSUM_BF16_ROWS - 1) / COLSUM_BF16_ROWS)),
-                     dim3(256), 0, s, X, M, N, ld, out);
+  hipLaunchKernelGGL(colsum_bf16_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, s, X, M, N, ld, rpb,
+                     (float*)nullptr, out);
 }
 
 // ------------------------------------------------------------------ batched transpose

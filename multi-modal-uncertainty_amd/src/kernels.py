@@ -112,7 +112,9 @@ def transpose_bf16_batched(jobs, n_jobs, max_rows, max_cols, stream_of):
 def colsum_bf16(X, out, accumulate=False):
     _dev_check(X, out)
     M, N_ = X.shape
-    N.call("mmu_colsum_bf16", _ptr(X), M, N_, X.stride(0), None, _ptr(out), int(accumulate), _stream(X))
+    # scratch for the per-block partial rows (>= ceil(M / 64) x N f32, see mmu_colsum_bf16)
+    part = torch.empty(((M + 63) // 64) * N_, dtype=torch.float32, device=X.device)
+    N.call("mmu_colsum_bf16", _ptr(X), M, N_, X.stride(0), _ptr(part), _ptr(out), int(accumulate), _stream(X))
 
 
 def dropmask_empty(batch, L, heads=12, device=None):

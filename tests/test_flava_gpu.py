@@ -181,11 +181,14 @@ def test_train_entry_point_flava_synthetic(dev, tmp_path):
     assert np.isfinite(h["loss"]).all()
 
 
-@pytest.mark.parametrize("M,N", [(37, 768), (5000, 2304), (35072, 768)])
-def test_colsum_bf16(dev, M, N):
+@pytest.mark.parametrize("M,N,acc", [(37, 768, True), (5000, 2304, True), (35072, 768, True), (35072, 2304, False),
+                                     (65, 1024, False), (300000, 768, True)])
+def test_colsum_bf16(dev, M, N, acc):
+    """Both paths of mmu_colsum_bf16: one row block (atomics) and per-block partial rows
+    folded by mmu_colsum_reduce (1-1024 rows per block)."""
     k = K()
     X = rnd(M, N, dev=dev, seed=8)
     out = torch.full((N,), 3.0, device=dev)
-    k.colsum_bf16(X, out, accumulate=True)
-    ref = X.float().sum(0) + 3.0
+    k.colsum_bf16(X, out, accumulate=acc)
+    ref = X.float().sum(0) + (3.0 if acc else 0.0)
     torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-3 * M ** 0.5)
