@@ -10,6 +10,11 @@
 #include <cstdlib>
 #include <cmath>
 
+static int64_t env_i64(const char* name, int64_t dflt) {
+  const char* v = getenv(name);
+  return v && *v && atoll(v) > 0 ? atoll(v) : dflt;
+}
+
 using namespace mmu;
 
 static thread_local std::string g_err;
@@ -159,9 +164,11 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
   p.kchunk = K;
   if (kind == MMU_EPI_STORE && c_dtype == MMU_F32 && !p.bias && !p.colsum && epi && epi->workspace && K >= 4096) {
     const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n * batch;
+    // MMU_SPLITK_MAX / MMU_SPLITK_MINK override the slice cap / minimum slice depth (A/B runs)
+    static const int64_t max_split = env_i64("MMU_SPLITK_MAX", 64), min_k = env_i64("MMU_SPLITK_MINK", 1024);
     int64_t want = (640 + tiles - 1) / tiles;
-    if (want > K / 1024) want = K / 1024;
-    if (want > 32) want = 32;
+    if (want > K / min_k) want = K / min_k;
+    if (want > max_split) want = max_split;
     const int64_t cap = epi->workspace_floats / (batch * M * N);
     if (want > cap) want = cap;
     if (want >= 2) {
