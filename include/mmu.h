@@ -47,7 +47,8 @@ const char* mmu_last_error(void);
 enum {
   MMU_EPI_STORE = 0,        /* C = acc (+bias[n]) (+C if accumulate)                     */
   MMU_EPI_BIAS_GELU = 1,    /* z = acc+bias; C = gelu_erf(z); aux (optional) = gelu'(z)  */
-  MMU_EPI_BIAS_DROP_RES = 2,/* C = residual + dropout(acc+bias)                          */
+  MMU_EPI_BIAS_DROP_RES = 2,/* C = residual + dropout(acc+bias); with c_dtype MMU_F32 the
+                               residual is f32 too (the encoder's f32 hidden stream)    */
   MMU_EPI_DGELU = 3,        /* C = acc * aux   (aux = the forward's gelu'(z))            */
   MMU_EPI_ADD_RES = 4,      /* C = acc + residual                                        */
   MMU_EPI_BIAS_DROP_QGELU = 5 /* u = dropout(acc+bias); C = u*sigmoid(1.702u); aux (optional)
@@ -59,7 +60,7 @@ typedef struct mmu_epilogue {
   int32_t accumulate;       /* STORE only: C += result (f32 C)                         */
   const float* bias;        /* [N] f32 or NULL                                          */
   int64_t bias_bstride;
-  const void* residual;     /* bf16 [M, ldr]                                            */
+  const void* residual;     /* bf16 [M, ldr] (f32 for BIAS_DROP_RES into an f32 C)      */
   int64_t ldr, res_bstride;
   void* aux;                /* bf16 [M, ldx]: GELU derivative (written or read)         */
   int64_t ldx, aux_bstride;
@@ -68,10 +69,8 @@ typedef struct mmu_epilogue {
   float drop_p;             /* BIAS_DROP_RES                                            */
   uint64_t seed;            /* dropout stream: element (z, m, n) uses counter (z*M+m)*N+n */
   float* workspace;         /* optional f32 scratch: lets a STORE/f32/no-bias product split K
-                               over workgroups (weight gradients), and lets any 256x256-tile
-                               product run the M-tile rows of a partial last wave of tiles
-                               as a split-K tail (same epilogue, same dropout counters);
-                               slabs summed in slice order, so results stay deterministic.
+                               over workgroups (weight gradients); slabs summed in slice
+                               order, so results stay deterministic.
                                Stream-ordered: one workspace per stream.                */
   int64_t workspace_floats;
 } mmu_epilogue;
@@ -153,6 +152,20 @@ int mmu_layernorm_bwd(const void* dY, const void* X, const float* mean, const fl
                       float* part_dw, float* part_db, float* part_dbias,
                       int64_t rows, int64_t H, int64_t rows_per_part, mmu_stream_t stream);
 
+/* The encoder's f32 hidden stream (post-LN BertLayer, src/mmbt.py:124-126): the LN input
+ * S = residual + dropout(branch) stays f32 (written by an f32 BIAS_DROP_RES epilogue), so
+ * that the 24 residual adds of the 12 layers are never rounded to bf16.
+ * mmu_layernorm_fwd_f32: X f32 [rows, H] -> Y bf16 (the next GEMM's operand) and, when
+ * Y32 != NULL, Y32 f32 (the next residual); group_rows / param_stride as above.
+ * mmu_layernorm_bwd_f32: mmu_layernorm_bwd with an f32 X. */
+int mmu_layernorm_fwd_f32(const float* X, const float* w, const float* b, void* Y, float* Y32,
+                          float* mean, float* rstd, int64_t rows, int64_t H, float eps,
+                          int64_t group_rows, int64_t param_stride, mmu_stream_t stream);
+int mmu_layernorm_bwd_f32(const void* dY, const float* X, const float* mean, const float* rstd,
+                          const float* w, void* dX, void* dXdrop, float drop_p, uint64_t seed,
+                          float* part_dw, float* part_db, float* part_dbias,
+                          int64_t rows, int64_t H, int64_t rows_per_part, mmu_stream_t stream);
+
 /* Pre-LN block backward (FLAVA ResidualAttentionBlock, src/model.py:210-212: x + f(LN(x))):
  * dX = LN'(dY) + dRes; part_dbias = column sums of that total dX (the bias gradient of the
  * Linear whose output was added to the residual stream).  No dropout output. */
@@ -184,7 +197,8 @@ int mmu_seqattn_bwd(const void* QKV, int64_t ld_qkv, const void* O, int64_t ld_o
  * Source sequence s of length S = n_img+2+T: s=0 [CLS], 1..n_img image proj rows,
  * n_img+1 [SEP] (positions 0..n_img+1, token type 0), then text t at position t,
  * type seg[b,t].  Output row (v,b,j) embeds source position idx[v*Lout + j]
- * (idx == NULL: identity, Lout == S) and is LayerNorm'ed.  X [V*B*Lout, H] bf16;
+ * (idx == NULL: identity, Lout == S) and is LayerNorm'ed.  X [V*B*Lout, H] bf16,
+ * X32 (optional, may be NULL) the same rows in f32 (the encoder's f32 hidden stream);
  * keymask [V*B, Lout] f32 additive; mean/rstd (optional) f32 [V*B*Lout] for backward.
  * Dropout after the LN: drop_img on the image-segment rows (ImageBertEmbeddings.dropout,
  * args.dropout), drop_txt on text rows (BertEmbeddings.dropout 0.1); counter row*768+col.
@@ -196,7 +210,7 @@ int mmu_embed_fwd(const int64_t* ids, const int64_t* seg, const int64_t* txt_mas
                   int64_t cls_id, int64_t sep_id,
                   const int64_t* idx, int64_t V, int64_t B, int64_t T, int64_t n_img, int64_t Lout,
                   int64_t H, float drop_txt, float drop_img, uint64_t seed,
-                  void* X, float* keymask, float* mean, float* rstd, mmu_stream_t stream);
+                  void* X, float* X32, float* keymask, float* mean, float* rstd, mmu_stream_t stream);
 /* Backward of mmu_embed_fwd for the identity variant (training): recomputes the
  * pre-LN sums, LN backward, then scatters: word rows by atomics, position / type
  * / [CLS] / [SEP] by batch reduction, image rows to dproj f32 [B, n_img, H].

@@ -87,29 +87,6 @@ static __device__ __forceinline__ bf16x8 scale_frag(uint4 u, float sc) {
   return v;
 }
 
-// ---- cooperative [ROWS][64] tile loader (register staged), rows >= L zero-filled
-template <int ROWS, int NT>
-struct TileLoader {
-  static constexpr int PER = ROWS * 8 / NT;  // 16-B chunks per thread
-  uint4 r[PER];
-  __device__ __forceinline__ void load(const bf16* base, int64_t ld, int row0, int L, int t) {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      int idx = t + NT * i, row = idx >> 3, c = idx & 7;
-      r[i] = (row0 + row < L) ? *(const uint4*)(base + (int64_t)(row0 + row) * ld + 8 * c) : make_uint4(0, 0, 0, 0);
-    }
-  }
-  __device__ __forceinline__ void store(char* s, int t, float sc = 1.0f) {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      int idx = t + NT * i, row = idx >> 3, c = idx & 7;
-      uint4 v = r[i];
-      if (sc != 1.0f) { bf16x8 f = scale_frag(v, sc); v = *(uint4*)&f; }
-      *(uint4*)(s + tile_off(row, c)) = v;
-    }
-  }
-};
-
 // Buffer descriptor from provably wave-uniform inputs: with the base / size words in
 // VGPRs hipcc wraps EVERY buffer op in a readfirstlane "waterfall" loop (~10 instructions
 // and a branch per DMA; 68 such loops in the dK/dV kernel).  Inputs derived from the
@@ -134,564 +111,12 @@ static __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// =============================================================================== forward
-// grid (ceil(L/128), batch*heads), 256 threads; wave w owns queries [blk*128 + 32w, +32)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_fwd_kernel(AttnParams p) {
-  constexpr int KV = 64, TILE = KV * 128;
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE + 2 * KV * 4];
-  float* maskL = (float*)(smem + 4 * TILE);
-  const int t = threadIdx.x, l = t & 63, w = t >> 6, h = l >> 5;
-  const int bh = blockIdx.y, b = bh / p.heads, hd = bh - b * p.heads;
-  const int L = p.L, HD = p.heads * 64;
-  const int q0w = blockIdx.x * 128 + 32 * w, q = q0w + (l & 31);
-  const bool wave_live = q0w < L;
-  const bf16* base = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64;
-  const bf16* Kb = base + HD;
-  const bf16* Vb = base + 2 * HD;
-  const float* km = p.keymask + (int64_t)b * L;
-  const uint32_t sbh = seed_for(p.seed, bh), Lp = (uint32_t)((L + 1) & ~1);
-  const uint32_t thr = drop_thr(p.drop_p);
+// ---------------------------------------------------------------- forward ring geometry
+constexpr int FWD_NS = 2;                      // K/V ring depth (tiles)
+constexpr int FWD_TILE = 64 * 128;             // 64 keys x 64 d bf16
+constexpr int FWD_STAGE = 2 * FWD_TILE + 256;  // K tile, V tile, key-mask row
+constexpr int FWD_MAX_NKV = 9;                 // L <= 576 (BERT: 512 text + image tokens)
 
-  bf16x8 qf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    uint4 u = q < L ? *(const uint4*)(base + (int64_t)q * p.ld_qkv + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
-    qf[ks] = scale_frag(u, 0.125f);
-  }
-  f32x16 o[2];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
-  float m_run = NEG_INF, l_run = 0.f;
-
-  TileLoader<KV, 256> lk, lv;
-  const int nkv = (L + KV - 1) / KV;
-  lk.load(Kb, p.ld_qkv, 0, L, t);
-  lv.load(Vb, p.ld_qkv, 0, L, t);
-  lk.store(smem, t);
-  lv.store(smem + TILE, t);
-  if (t < KV) maskL[t] = t < L ? km[t] * LOG2E : NEG_INF;
-  __syncthreads();
-
-  for (int j = 0; j < nkv; ++j) {
-    const int stg = j & 1;
-    const char* Ks = smem + stg * 2 * TILE;
-    const char* Vs = Ks + TILE;
-    const float* mk = maskL + stg * KV;
-    const bool more = j + 1 < nkv;
-    float mnext = 0.f;
-    if (more) {
-      lk.load(Kb, p.ld_qkv, (j + 1) * KV, L, t);
-      lv.load(Vb, p.ld_qkv, (j + 1) * KV, L, t);
-      if (t < KV) { int key = (j + 1) * KV + t; mnext = key < L ? km[key] * LOG2E : NEG_INF; }
-    }
-    if (wave_live) {
-      f32x16 sc[2];
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sc[st][i] = 0.f;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-          sc[st] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ks, 32 * st, ks, l), qf[ks], sc[st], 0, 0, 0);
-      }
-      float mx = NEG_INF;
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          int key = 32 * st + (r & 3) + 8 * (r >> 2) + 4 * h;
-          float s = sc[st][r] * LOG2E + mk[key];
-          sc[st][r] = s;
-          mx = fmaxf(mx, s);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m_run, mx);
-      const float alpha = m_run == NEG_INF ? 0.f : __builtin_amdgcn_exp2f(m_run - mnew);
-      float rs = 0.f;
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float e = __builtin_amdgcn_exp2f(sc[st][r] - mnew);
-          sc[st][r] = e;
-          rs += e;
-        }
-      rs += __shfl_xor(rs, 32, 64);
-      l_run = l_run * alpha + rs;
-      m_run = mnew;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
-      if (thr) {
-        uint64_t kbits = 0;  // keep bits of this lane's 32 keys of the tile (bit = key - j*KV)
-#pragma unroll
-        for (int st = 0; st < 2; ++st)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int kl = 32 * st + 8 * g + 4 * h;
-            const uint32_t key = j * KV + kl;
-            uint32_t h0 = drop_pair(sbh, q, key, Lp), h1 = drop_pair(sbh, q, key + 2, Lp);
-            const uint32_t k4 = ((h0 & 0xFFFFu) >= thr ? 1u : 0u) | ((h0 >> 16) >= thr ? 2u : 0u) |
-                                ((h1 & 0xFFFFu) >= thr ? 4u : 0u) | ((h1 >> 16) >= thr ? 8u : 0u);
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (!((k4 >> e) & 1)) sc[st][4 * g + e] = 0.f;
-            kbits |= (uint64_t)k4 << kl;
-          }
-        if (p.dropmask) {  // the backward kernels read these bits instead of re-hashing
-          const uint64_t other = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(kbits >> 32), 32, 64) << 32) |
-                                 (uint32_t)__shfl_xor((int)(uint32_t)kbits, 32, 64);
-          if (h == 0 && q < L) p.dropmask[((int64_t)bh * L + q) * nkv + j] = kbits | other;
-        }
-      }
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          bf16x8 pf = acc_frag(sc[st], s2);
-#pragma unroll
-          for (int dt = 0; dt < 2; ++dt)
-            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Vs, 32 * st + 16 * s2, 32 * dt, l), pf, o[dt], 0, 0, 0);
-        }
-    }
-    if (more) {
-      char* dK = smem + (stg ^ 1) * 2 * TILE;
-      lk.store(dK, t);
-      lv.store(dK + TILE, t);
-      if (t < KV) maskL[(stg ^ 1) * KV + t] = mnext;
-    }
-    __syncthreads();
-  }
-  if (!wave_live || q >= L) return;
-  const float inv = (thr ? 1.0f / (1.0f - p.drop_p) : 1.0f) / l_run;
-  bf16* ob = p.out + ((int64_t)b * L + q) * p.ld_out + hd * 64;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      bf16x4 v = {f2bf(o[dt][4 * g] * inv), f2bf(o[dt][4 * g + 1] * inv), f2bf(o[dt][4 * g + 2] * inv),
-                  f2bf(o[dt][4 * g + 3] * inv)};
-      *(bf16x4*)(ob + 32 * dt + 8 * g + 4 * h) = v;
-    }
-  if (h == 0) p.lse[(int64_t)bh * L + q] = m_run * LN2 + logf(l_run);
-}
-
-// ---------------------------------------------------------------- forward, LDS-DMA ring
-// attn_fwd_kernel with K / V tiles and the key-mask row arriving by buffer_load...lds into
-// a 3-deep ring (2 tiles ahead, one raw barrier per tile).  Keys past L read as zero rows
-// and mask 0, so the partial last tile masks them to -inf explicitly.  The keep bits go
-// to a per-wave LDS buffer and are written out once at the end (stores inside the loop
-// would break the counted vmcnt waits).  Needs ceil(L/64) <= FWD_MAX_NKV.
-constexpr int FWD_NS = 2;
-constexpr int FWD_TILE = 64 * 128;
-constexpr int FWD_STAGE = 2 * FWD_TILE + 256;
-constexpr int FWD_MAX_NKV = 9;  // L <= 576 (BERT: 512 text + image tokens); keeps 3 blocks / CU
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void attn_fwd_dma_kernel(AttnParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[FWD_NS * FWD_STAGE + 4 * 32 * FWD_MAX_NKV * 8];
-  uint64_t* kbuf_all = (uint64_t*)(smem + FWD_NS * FWD_STAGE);
-  const int t = threadIdx.x, l = t & 63, h = l >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int bh = blockIdx.y, b = bh / p.heads, hd = bh - b * p.heads;
-  const int L = p.L, HD = p.heads * 64;
-  const int q0w = blockIdx.x * 128 + 32 * w, q = q0w + (l & 31);
-  const bool wave_live = q0w < L;
-  const bf16* base = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64;
-  const uint32_t sbh = seed_for(p.seed, bh), Lp = (uint32_t)((L + 1) & ~1);
-  const uint32_t thr = drop_thr(p.drop_p);
-  const int nkv = (L + 63) / 64;
-  uint64_t* kbuf = kbuf_all + w * 32 * nkv;  // [32 rows][nkv] keep words of this wave
-
-  const __amdgpu_buffer_rsrc_t rkv = urs((void*)(p.qkv + (int64_t)b * L * p.ld_qkv), (int)(L * p.ld_qkv * 2));
-  const __amdgpu_buffer_rsrc_t rm = urs((void*)(p.keymask + (int64_t)b * L), (int)(L * 4));
-  bf16x8 qf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    uint4 u = q < L ? *(const uint4*)(base + (int64_t)q * p.ld_qkv + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
-    qf[ks] = scale_frag(u, 0.125f);
-  }
-  f32x16 o[2];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
-  float m_run = NEG_INF, l_run = 0.f;
-
-  // per tile: waves 0,1 -> K pieces, waves 2,3 -> V pieces (4 each); wave 0 also the mask row
-  auto issue = [&](int j) {
-    char* st = smem + (j % FWD_NS) * FWD_STAGE;
-    const int k0 = j * 64;
-    const int off_col = (w < 2 ? HD : 2 * HD) + hd * 64;
-    char* dst = st + (w < 2 ? 0 : FWD_TILE);
-#pragma unroll
-    for (int pc = 0; pc < 4; ++pc) {
-      const int piece = 4 * (w & 1) + pc;
-      const int row = 8 * piece + (l >> 3), c = (l & 7) ^ fsw(row);
-      dma16(rkv, dst + piece * 1024, (uint32_t)(((k0 + row) * p.ld_qkv + off_col + 8 * c) * 2));
-    }
-    if (w == 0 && l < 16) dma16(rm, st + 2 * FWD_TILE, (uint32_t)((k0 + 4 * l) * 4));
-  };
-  auto wait_for = [&](int ahead) {
-    if (w == 0) {
-      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  };
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  for (int j = 0; j < FWD_NS - 1 && j < nkv; ++j) issue(j);
-  for (int j = 0; j < nkv; ++j) {
-    const int ahead = nkv - 1 - j < FWD_NS - 2 ? nkv - 1 - j : FWD_NS - 2;
-    wait_for(ahead);
-    raw_barrier();
-    if (j + FWD_NS - 1 < nkv) issue(j + FWD_NS - 1);
-    const char* st = smem + (j % FWD_NS) * FWD_STAGE;
-    const char* Ks = st;
-    const char* Vs = st + FWD_TILE;
-    const float* mk = (const float*)(st + 2 * FWD_TILE);
-    const bool partial = (j + 1) * 64 > L;  // keys >= L live only in the last tile
-    if (wave_live) {
-      f32x16 sc[2];
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sc[s2][i] = 0.f;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-          sc[s2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ks, 32 * s2, ks, l), qf[ks], sc[s2], 0, 0, 0);
-      }
-      float mx = NEG_INF;
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = 32 * s2 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          float s = (sc[s2][r] + mk[key]) * LOG2E;
-          if (partial && j * 64 + key >= L) s = NEG_INF;
-          sc[s2][r] = s;
-          mx = fmaxf(mx, s);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m_run, mx);
-      const float alpha = m_run == NEG_INF ? 0.f : __builtin_amdgcn_exp2f(m_run - mnew);
-      float rs = 0.f;
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float e = __builtin_amdgcn_exp2f(sc[s2][r] - mnew);
-          sc[s2][r] = e;
-          rs += e;
-        }
-      rs += __shfl_xor(rs, 32, 64);
-      l_run = l_run * alpha + rs;
-      m_run = mnew;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
-      if (thr) {
-        uint64_t kbits = 0;  // keep bits of this lane's 32 keys of the tile (bit = key - 64j)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int kl = 32 * s2 + 8 * g + 4 * h;
-            const uint32_t key = j * 64 + kl;
-            uint32_t h0 = drop_pair(sbh, q, key, Lp), h1 = drop_pair(sbh, q, key + 2, Lp);
-            const uint32_t k4 = ((h0 & 0xFFFFu) >= thr ? 1u : 0u) | ((h0 >> 16) >= thr ? 2u : 0u) |
-                                ((h1 & 0xFFFFu) >= thr ? 4u : 0u) | ((h1 >> 16) >= thr ? 8u : 0u);
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (!((k4 >> e) & 1)) sc[s2][4 * g + e] = 0.f;
-            kbits |= (uint64_t)k4 << kl;
-          }
-        const uint64_t other = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(kbits >> 32), 32, 64) << 32) |
-                               (uint32_t)__shfl_xor((int)(uint32_t)kbits, 32, 64);
-        if (h == 0) kbuf[(l & 31) * nkv + j] = kbits | other;
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          bf16x8 pf = acc_frag(sc[s2], u);
-#pragma unroll
-          for (int dt = 0; dt < 2; ++dt)
-            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Vs, 32 * s2 + 16 * u, 32 * dt, l), pf, o[dt], 0, 0,
-                                                            0);
-        }
-    }
-  }
-  if (!wave_live) return;
-  if (thr && p.dropmask) {  // this wave's 32 rows x nkv words are contiguous in the dropmask
-    uint64_t* dst = p.dropmask + ((int64_t)bh * L + q0w) * nkv;
-    const int rows = L - q0w < 32 ? L - q0w : 32;
-    for (int i = l; i < rows * nkv; i += 64) dst[i] = kbuf[i];
-  }
-  if (q >= L) return;
-  const float inv = (thr ? 1.0f / (1.0f - p.drop_p) : 1.0f) / l_run;
-  bf16* ob = p.out + ((int64_t)b * L + q) * p.ld_out + hd * 64;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      bf16x4 v = {f2bf(o[dt][4 * g] * inv), f2bf(o[dt][4 * g + 1] * inv), f2bf(o[dt][4 * g + 2] * inv),
-                  f2bf(o[dt][4 * g + 3] * inv)};
-      *(bf16x4*)(ob + 32 * dt + 8 * g + 4 * h) = v;
-    }
-  if (h == 0) p.lse[(int64_t)bh * L + q] = m_run * LN2 + logf(l_run);
-}
-
-// =============================================================================== backward
-// delta[bh, q] = sum_d dO[q, d] * O[q, d]   (one wave per (bh, 8 rows))
-__global__ __launch_bounds__(256) void attn_delta_kernel(AttnParams p) {
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
-  const int bh = blockIdx.y, b = bh / p.heads, hd = bh - b * p.heads;
-  const int row = blockIdx.x * 32 + w * 8 + (l >> 3);
-  if (row >= p.L) return;
-  const int c = (l & 7) * 8;
-  const int64_t tok = (int64_t)b * p.L + row;
-  bf16x8 a = *(const bf16x8*)(p.o + tok * p.ld_o + hd * 64 + c);
-  bf16x8 d = *(const bf16x8*)(p.dout + tok * p.ld_do + hd * 64 + c);
-  float s = 0.f;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) s += bf2f(a[e]) * bf2f(d[e]);
-  s += __shfl_xor(s, 1, 64);
-  s += __shfl_xor(s, 2, 64);
-  s += __shfl_xor(s, 4, 64);
-  if ((l & 7) == 0) p.delta[(int64_t)bh * p.L + row] = s;
-}
-
-// dQ: grid (ceil(L/128), batch*heads), 256 threads, wave owns 32 queries; loops over 64-key tiles
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_dq_kernel(AttnParams p) {
-  constexpr int KV = 64, TILE = KV * 128;
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE + 2 * KV * 4];
-  float* maskL = (float*)(smem + 4 * TILE);
-  const int t = threadIdx.x, l = t & 63, w = t >> 6, h = l >> 5;
-  const int bh = blockIdx.y, b = bh / p.heads, hd = bh - b * p.heads;
-  const int L = p.L, HD = p.heads * 64;
-  const int q0w = blockIdx.x * 128 + 32 * w, q = q0w + (l & 31);
-  const bool wave_live = q0w < L, qv = q < L;
-  const bf16* base = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64;
-  const bf16* Kb = base + HD;
-  const bf16* Vb = base + 2 * HD;
-  const float* km = p.keymask + (int64_t)b * L;
-  const bool drop = drop_thr(p.drop_p) != 0;  // same test as the forward's
-  const float zs = drop ? 1.0f / (1.0f - p.drop_p) : 1.0f;
-
-  bf16x8 qf[4], df[4];
-  const bf16* dob = p.dout + ((int64_t)b * L + q) * p.ld_do + hd * 64;
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    uint4 u = qv ? *(const uint4*)(base + (int64_t)q * p.ld_qkv + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
-    qf[ks] = scale_frag(u, 0.125f);
-    uint4 v = qv ? *(const uint4*)(dob + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
-    df[ks] = *(bf16x8*)&v;
-  }
-  // row constants as the accumulators' initial values: S - lse and dP - delta/zs, so that
-  // p = exp2(log2e (S - lse) + mask) and dS = p (keep ? (dP - delta/zs) zs : -delta)
-  const float nlse = qv ? -p.lse[(int64_t)bh * L + q] : -__builtin_huge_valf();
-  const float dlt = qv ? p.delta[(int64_t)bh * L + q] : 0.f;
-  const float ndz = -dlt / zs;
-  f32x16 dq[2];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) { dq[0][i] = 0.f; dq[1][i] = 0.f; }
-
-  TileLoader<KV, 256> lk, lv;
-  const int nkv = (L + KV - 1) / KV;
-  // keep bits of this query row (written by the forward), pre-shifted by 4h so the bit
-  // of accumulator register r of sub-tile st sits at the constant 32st + (r&3) + 8(r>>2)
-  const uint64_t* kwp = p.dropmask + ((int64_t)bh * L + q) * nkv;
-  const bool kwl = drop && qv;
-  uint64_t kw = kwl ? kwp[0] : ~0ull;
-  lk.load(Kb, p.ld_qkv, 0, L, t);
-  lv.load(Vb, p.ld_qkv, 0, L, t);
-  lk.store(smem, t);
-  lv.store(smem + TILE, t);
-  if (t < KV) maskL[t] = t < L ? km[t] * LOG2E : NEG_INF;
-  __syncthreads();
-  for (int j = 0; j < nkv; ++j) {
-    const int stg = j & 1;
-    const char* Ks = smem + stg * 2 * TILE;
-    const char* Vs = Ks + TILE;
-    const float* mk = maskL + stg * KV;
-    const bool more = j + 1 < nkv;
-    float mnext = 0.f;
-    uint64_t kwn = ~0ull;
-    if (more) {
-      lk.load(Kb, p.ld_qkv, (j + 1) * KV, L, t);
-      lv.load(Vb, p.ld_qkv, (j + 1) * KV, L, t);
-      if (t < KV) { int key = (j + 1) * KV + t; mnext = key < L ? km[key] * LOG2E : NEG_INF; }
-      if (kwl) kwn = kwp[j + 1];
-    }
-    if (wave_live) {
-      const uint64_t kwh = kw >> (4 * h);
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const uint32_t kw32 = (uint32_t)(kwh >> (32 * st));
-        f32x16 sc, dp;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) { sc[i] = nlse; dp[i] = ndz; }
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ks, 32 * st, ks, l), qf[ks], sc, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Vs, 32 * st, ks, l), df[ks], dp, 0, 0, 0);
-        }
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 4 * g + e;
-            const int kc = (r & 3) + 8 * (r >> 2), kl = 32 * st + kc + 4 * h;
-            const float pr = __builtin_amdgcn_exp2f(fmaf(sc[r], LOG2E, mk[kl]));
-            const float v = (kw32 & (1u << kc)) ? dp[r] * zs : -dlt;
-            sc[r] = pr * v;  // dS^T
-          }
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          bf16x8 sf = acc_frag(sc, s2);
-#pragma unroll
-          for (int dt = 0; dt < 2; ++dt)
-            dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Ks, 32 * st + 16 * s2, 32 * dt, l), sf, dq[dt], 0, 0, 0);
-        }
-      }
-    }
-    if (more) {
-      char* dK = smem + (stg ^ 1) * 2 * TILE;
-      lk.store(dK, t);
-      lv.store(dK + TILE, t);
-      if (t < KV) maskL[(stg ^ 1) * KV + t] = mnext;
-    }
-    kw = kwn;
-    __syncthreads();
-  }
-  if (!qv) return;
-  bf16* ob = p.out + ((int64_t)b * L + q) * p.ld_out + hd * 64;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      bf16x4 v = {f2bf(dq[dt][4 * g] * 0.125f), f2bf(dq[dt][4 * g + 1] * 0.125f), f2bf(dq[dt][4 * g + 2] * 0.125f),
-                  f2bf(dq[dt][4 * g + 3] * 0.125f)};
-      *(bf16x4*)(ob + 32 * dt + 8 * g + 4 * h) = v;
-    }
-}
-
-// dK, dV: grid (ceil(L/64), batch*heads), 128 threads; wave owns 32 keys; loops over 32-query tiles
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void attn_dkdv_kernel(AttnParams p) {
-  constexpr int QT = 32, TILE = QT * 128;
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE + 2 * 2 * QT * 4 + 2 * QT * 8];
-  float* rowL = (float*)(smem + 4 * TILE);  // [stage][2][QT]: -lse, delta
-  uint64_t* rowK = (uint64_t*)(rowL + 4 * QT);  // [stage][QT]: keep bits of this block's 64 keys
-  const int t = threadIdx.x, l = t & 63, w = t >> 6, h = l >> 5;
-  const int bh = blockIdx.y, b = bh / p.heads, hd = bh - b * p.heads;
-  const int L = p.L, HD = p.heads * 64;
-  const int k0w = blockIdx.x * 64 + 32 * w, key = k0w + (l & 31);
-  const bool wave_live = k0w < L, kv = key < L;
-  const bf16* base = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64;
-  const bf16* dob = p.dout + (int64_t)b * L * p.ld_do + hd * 64;
-  const bool drop = drop_thr(p.drop_p) != 0;  // same test as the forward's
-  const float zs = drop ? 1.0f / (1.0f - p.drop_p) : 1.0f;
-  const int nkv = (L + 63) / 64;
-  const float mkey = kv ? p.keymask[(int64_t)b * L + key] * LOG2E : NEG_INF;
-
-  bf16x8 kf[4], vf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    uint4 u = kv ? *(const uint4*)(base + (int64_t)key * p.ld_qkv + HD + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
-    uint4 v = kv ? *(const uint4*)(base + (int64_t)key * p.ld_qkv + 2 * HD + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
-    kf[ks] = *(bf16x8*)&u;
-    vf[ks] = *(bf16x8*)&v;
-  }
-  f32x16 dk[2], dv[2];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) { dk[0][i] = 0.f; dk[1][i] = 0.f; dv[0][i] = 0.f; dv[1][i] = 0.f; }
-
-  TileLoader<QT, 128> lq, ld;
-  const int nq = (L + QT - 1) / QT;
-  auto load_rows = [&](int i0, float& a, float& c, uint64_t& k) {
-    int qq = i0 + (t & 31);
-    a = qq < L ? -p.lse[(int64_t)bh * L + qq] : -__builtin_huge_valf();
-    c = qq < L ? p.delta[(int64_t)bh * L + qq] : 0.f;
-    k = (drop && qq < L) ? p.dropmask[((int64_t)bh * L + qq) * nkv + blockIdx.x] : ~0ull;
-  };
-  float ra = 0.f, rc = 0.f;
-  uint64_t rk = 0;
-  lq.load(base, p.ld_qkv, 0, L, t);
-  ld.load(dob, p.ld_do, 0, L, t);
-  load_rows(0, ra, rc, rk);
-  lq.store(smem, t, 0.125f);
-  ld.store(smem + TILE, t);
-  if (t < QT) { rowL[t] = ra; rowL[QT + t] = rc; rowK[t] = rk; }
-  __syncthreads();
-  for (int i = 0; i < nq; ++i) {
-    const int stg = i & 1;
-    const char* Qs = smem + stg * 2 * TILE;
-    const char* Ds = Qs + TILE;
-    const float* nlse = rowL + stg * 2 * QT;
-    const float* dlt = nlse + QT;
-    const uint32_t* kbit = (const uint32_t*)(rowK + stg * QT);  // [QT][2] halves: this wave's keys = half w
-    const bool more = i + 1 < nq;
-    if (more) {
-      lq.load(base, p.ld_qkv, (i + 1) * QT, L, t);
-      ld.load(dob, p.ld_do, (i + 1) * QT, L, t);
-      load_rows((i + 1) * QT, ra, rc, rk);
-    }
-    if (wave_live) {
-      f32x16 sc, dp;  // S starts at -lse of its query row (row constant as initial accumulator)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { sc[r] = nlse[(r & 3) + 8 * (r >> 2) + 4 * h]; dp[r] = 0.f; }
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Qs, 0, ks, l), kf[ks], sc, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ds, 0, ks, l), vf[ks], dp, 0, 0, 0);
-      }
-      f32x16 pz;  // dropped P (for dV)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ql = (r & 3) + 8 * (r >> 2) + 4 * h;
-        float pr = __builtin_amdgcn_exp2f(fmaf(sc[r], LOG2E, mkey));
-        float z = ((kbit[2 * ql + w] >> (l & 31)) & 1u) ? zs : 0.f;
-        pz[r] = pr * z;
-        sc[r] = pr * (dp[r] * z - dlt[ql]);  // dS
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        bf16x8 pf = acc_frag(pz, s2), sf = acc_frag(sc, s2);
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf, tr_frag(Ds, 16 * s2, 32 * dt, l), dv[dt], 0, 0, 0);
-          dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sf, tr_frag(Qs, 16 * s2, 32 * dt, l), dk[dt], 0, 0, 0);
-        }
-      }
-    }
-    if (more) {
-      char* dQ = smem + (stg ^ 1) * 2 * TILE;
-      lq.store(dQ, t, 0.125f);
-      ld.store(dQ + TILE, t);
-      if (t < QT) {
-        rowL[(stg ^ 1) * 2 * QT + t] = ra;
-        rowL[(stg ^ 1) * 2 * QT + QT + t] = rc;
-        rowK[(stg ^ 1) * QT + t] = rk;
-      }
-    }
-    __syncthreads();
-  }
-  if (!wave_live) return;
-  // dK/dV accumulators: rows = key (registers), cols = d (lanes)
-  bf16* outb = p.out + (int64_t)b * L * p.ld_out + hd * 64;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int kk = k0w + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (kk < L) {
-        const int64_t off = (int64_t)kk * p.ld_out + 32 * dt + (l & 31);
-        outb[off + HD] = f2bf(dk[dt][r]);
-        outb[off + 2 * HD] = f2bf(dv[dt][r]);
-      }
-    }
-}
-
-static bool attn_dma();
 // ---------------------------------------------------------------- forward v2 (lean softmax)
 // attn_fwd_dma_kernel's ring and tiling with the per-element VALU work cut down (the v1
 // forward issued ~750 VALU per 16 MFMAs per tile and measured VALU-busy ~88 %):
@@ -950,34 +375,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
 }
 
-static int attn_fwd_ver() {
-  const char* e = getenv("MMU_ATTN_FWD");  // 1 = v1 LDS-DMA kernel, 0 = register-staged (A/B)
-  return e ? atoi(e) : 2;
-}
-
 void attention_fwd_launch(const AttnParams& p, hipStream_t s) {
   dim3 grid((p.L + 127) / 128, p.batch * p.heads);
-  const int ver = attn_dma() ? attn_fwd_ver() : 0;
-  const bool fits = (p.L + 63) / 64 <= FWD_MAX_NKV;
-  if (ver >= 2 && fits && p.ld_out % 8 == 0) {
-    // Dropout variant at 2 waves / SIMD (at the 3-wave register cap it spills lane-constant
-    // LDS addresses around the loop: 0.89 vs 0.59 ms at B = 256, L = 513, p = 0.1).
-    // A/B (MMU_ATTN_FWD): 3 = 3 waves/SIMD, 4 = 3 waves + per-tile re-derived addresses
-    if (drop_thr(p.drop_p) && !p.dropmask && ver != 5) {
-      // inference dropout (MC-dropout passes): no keep bits to store (MMU_ATTN_FWD=5: the storing kernel)
-      hipLaunchKernelGGL((attn_fwd_v2_kernel<true, 3, true, false>), grid, dim3(256), 0, s, p);
-    } else if (drop_thr(p.drop_p)) {
-      if (ver == 3) hipLaunchKernelGGL((attn_fwd_v2_kernel<true, 3, false>), grid, dim3(256), 0, s, p);
-      else if (ver == 4) hipLaunchKernelGGL((attn_fwd_v2_kernel<true, 3, true>), grid, dim3(256), 0, s, p);
-      else hipLaunchKernelGGL((attn_fwd_v2_kernel<true, 2, false>), grid, dim3(256), 0, s, p);
-    } else {
-      if (ver == 4) hipLaunchKernelGGL((attn_fwd_v2_kernel<false, 3, true>), grid, dim3(256), 0, s, p);
-      else hipLaunchKernelGGL((attn_fwd_v2_kernel<false, 3, false>), grid, dim3(256), 0, s, p);
-    }
-  } else if (ver >= 1 && fits) {
-    hipLaunchKernelGGL(attn_fwd_dma_kernel, grid, dim3(256), 0, s, p);
+  if (drop_thr(p.drop_p) && !p.dropmask) {
+    // inference dropout (MC-dropout passes): no keep bits to store, 3 waves / SIMD
+    hipLaunchKernelGGL((attn_fwd_v2_kernel<true, 3, true, false>), grid, dim3(256), 0, s, p);
+  } else if (drop_thr(p.drop_p)) {
+    // training dropout at 2 waves / SIMD (at the 3-wave register cap it spills lane-constant
+    // LDS addresses around the loop: 0.89 vs 0.59 ms at B = 256, L = 513, p = 0.1)
+    hipLaunchKernelGGL((attn_fwd_v2_kernel<true, 2, false>), grid, dim3(256), 0, s, p);
   } else {
-    hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, s, p);
+    hipLaunchKernelGGL((attn_fwd_v2_kernel<false, 3, false>), grid, dim3(256), 0, s, p);
   }
 }
 
@@ -1334,26 +742,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     }
 }
 
-static bool attn_dma() {
-  const char* e = getenv("MMU_ATTN_DMA");  // 0 = register-staged kernels (A/B comparisons)
-  return !(e && e[0] == '0');
-}
-
-bool attention_bwd_fuses_colsum() { return attn_dma(); }
-
 void attention_bwd_launch(const AttnParams& p, hipStream_t s) {
-  if (attn_dma()) {  // the dQ kernel computes (and stores) delta itself
-    hipLaunchKernelGGL(attn_dq_dma_kernel, dim3((p.L + 127) / 128, p.batch * p.heads), dim3(256), 0, s, p);
-  } else {
-    hipLaunchKernelGGL(attn_delta_kernel, dim3((p.L + 31) / 32, p.batch * p.heads), dim3(256), 0, s, p);
-    hipLaunchKernelGGL(attn_dq_kernel, dim3((p.L + 127) / 128, p.batch * p.heads), dim3(256), 0, s, p);
-  }
-  if (attn_dma() && drop_thr(p.drop_p))
+  // the dQ kernel also computes (and stores) delta = rowsum(dO * O) for the dK/dV kernel
+  hipLaunchKernelGGL(attn_dq_dma_kernel, dim3((p.L + 127) / 128, p.batch * p.heads), dim3(256), 0, s, p);
+  if (drop_thr(p.drop_p))
     hipLaunchKernelGGL(attn_dkdv_dma_kernel<true>, dim3((p.L + 63) / 64, p.batch * p.heads), dim3(128), 0, s, p);
-  else if (attn_dma())
-    hipLaunchKernelGGL(attn_dkdv_dma_kernel<false>, dim3((p.L + 63) / 64, p.batch * p.heads), dim3(128), 0, s, p);
   else
-    hipLaunchKernelGGL(attn_dkdv_kernel, dim3((p.L + 63) / 64, p.batch * p.heads), dim3(128), 0, s, p);
+    hipLaunchKernelGGL(attn_dkdv_dma_kernel<false>, dim3((p.L + 63) / 64, p.batch * p.heads), dim3(128), 0, s, p);
 }
 
 }  // namespace mmu

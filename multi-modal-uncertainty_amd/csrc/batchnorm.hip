@@ -312,13 +312,9 @@ struct BnGrid {
 // multiple of the rows per iteration), and few enough row blocks that blocks x C partial
 // pairs fit BN_MAX_PART_ELEMS.  (A fixed 64 K elements per block left the trunk's small
 // tensors on 24-200 blocks -- e.g. layer3's 256-channel 14x14 maps at batch 32 -- i.e. on
-// a tenth of the CUs, latency-bound.)  MMU_BN_TARGET / MMU_BN_MIN override, for A/B runs.
-static int64_t bn_env(const char* name, int64_t dflt) {
-  const char* v = getenv(name);
-  return v && *v ? atoll(v) : dflt;
-}
+// a tenth of the CUs, latency-bound.)
 static BnGrid bn_grid(int64_t rows, int C) {
-  static const int64_t target = bn_env("MMU_BN_TARGET", 1024), min_elems = bn_env("MMU_BN_MIN", 4096);
+  const int64_t target = 1024, min_elems = 4096;
   BnGrid g;
   g.CH = 512;
   while (C % g.CH) g.CH >>= 1;

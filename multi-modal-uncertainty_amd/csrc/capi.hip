@@ -10,11 +10,6 @@
 #include <cstdlib>
 #include <cmath>
 
-static int64_t env_i64(const char* name, int64_t dflt) {
-  const char* v = getenv(name);
-  return v && *v && atoll(v) > 0 ? atoll(v) : dflt;
-}
-
 using namespace mmu;
 
 static thread_local std::string g_err;
@@ -33,19 +28,6 @@ static int check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail("%s: launch failed: %s", what, hipGetErrorString(e));
   return 0;
-}
-
-// compute units of the current device (the wave size of a launch: gemm tail peeling)
-static int cu_count() {
-  static int cache[64] = {};
-  int d = 0;
-  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return 256;
-  if (!cache[d]) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || n <= 0) n = 256;
-    cache[d] = n;
-  }
-  return cache[d];
 }
 
 // ------------------------------------------------------------------ timing of mmu_gemm
@@ -127,21 +109,18 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
   // 32-bit buffer offsets of those out-of-range reads never wrap back into the operand)
   const int64_t a_span = 2 * (a_kmajor ? (M + 256) * lda : (K + 64) * lda);
   const int64_t b_span = 2 * (b_kmajor ? (N + 256) * ldb : (K + 64) * ldb);
-  const char* force_small = getenv("MMU_GEMM_SMALL");  // A/B experiments: 1 = always the 128x128 kernel
-  const bool big = M >= 256 && N >= 256 && a_span < (1ll << 32) - 4096 && b_span < (1ll << 32) - 4096 &&
-                   !(force_small && force_small[0] == '1');
+  const bool big = M >= 256 && N >= 256 && a_span < (1ll << 32) - 4096 && b_span < (1ll << 32) - 4096;
   const int tile = big ? 256 : 128;
   p.tiles_m = (int)((M + tile - 1) / tile);
   p.tiles_n = (int)((N + tile - 1) / tile);
-  // tile-order group height, measured on the BERT shapes (tools/gemm_bench.py --var
-  // MMU_GEMM_GROUP): row-major for <= 3 column tiles, 2 with an N-major B (dY.W2), 8 for the
+  // tile-order group height, measured on the BERT shapes (tools/gemm_bench.py; group-height
+  // sweeps in profiles/r1_gemm_group_sweep.txt): row-major for <= 3 column tiles, 2 with an N-major B (dY.W2), 8 for the
   // wide forward products (QKV 0.496 -> 0.457 ms, W1+GELU 0.888 -> 0.832 ms)
   int kind = MMU_EPI_STORE;
   if (epi) kind = epi->kind;
   // (and 2 for the dGELU product dY2.W2, whose epilogue streams the [M, 3072] gelu' rows:
   // 0.888 -> 0.756 ms with a K-major B, profiles/r2_gemm_group_dz.txt)
   p.group_m = p.tiles_n <= 3 ? 1 : ((b_kmajor && kind != MMU_EPI_DGELU) ? 8 : 2);
-  if (const char* g = getenv("MMU_GEMM_GROUP")) p.group_m = atoi(g) > 0 ? atoi(g) : p.group_m;
   if (epi) {
     kind = epi->kind;
     p.accumulate = epi->accumulate;
@@ -153,7 +132,10 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
   }
   p.kind = kind;
   if (kind < 0 || kind > MMU_EPI_BIAS_DROP_QGELU) return fail("mmu_gemm: bad epilogue kind %d", kind);
-  if (kind != MMU_EPI_STORE && c_dtype != MMU_BF16) return fail("mmu_gemm: fused epilogues write bf16");
+  if (kind != MMU_EPI_STORE && kind != MMU_EPI_BIAS_DROP_RES && c_dtype != MMU_BF16)
+    return fail("mmu_gemm: fused epilogues other than BIAS_DROP_RES write bf16");
+  if (kind == MMU_EPI_BIAS_DROP_RES && c_dtype == MMU_F32 && (ldc % 4 || (epi && epi->ldr % 4)))
+    return fail("mmu_gemm: f32 hidden-stream epilogue needs 16-B aligned rows");
   if (kind == MMU_EPI_DGELU && !p.aux) return fail("mmu_gemm: DGELU epilogue needs aux");
   if ((kind == MMU_EPI_BIAS_DROP_RES || kind == MMU_EPI_ADD_RES) && !p.residual)
     return fail("mmu_gemm: epilogue needs residual");
@@ -164,8 +146,8 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
   p.kchunk = K;
   if (kind == MMU_EPI_STORE && c_dtype == MMU_F32 && !p.bias && !p.colsum && epi && epi->workspace && K >= 4096) {
     const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n * batch;
-    // MMU_SPLITK_MAX / MMU_SPLITK_MINK override the slice cap / minimum slice depth (A/B runs)
-    static const int64_t max_split = env_i64("MMU_SPLITK_MAX", 64), min_k = env_i64("MMU_SPLITK_MINK", 1024);
+    // slice cap 64 / minimum slice depth 1024 (profiles/r2_splitk_cap_ab.txt)
+    const int64_t max_split = 64, min_k = 1024;
     int64_t want = (640 + tiles - 1) / tiles;
     if (want > K / min_k) want = K / min_k;
     if (want > max_split) want = max_split;
@@ -179,37 +161,6 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
       p.ws = epi->workspace;
     }
   }
-  // split-K tail: peel the M-tile rows of a partial last wave of big tiles (see gemm.hip
-  // gemm_tail_kernel).  Opt-in (MMU_GEMM_TAIL=1): on the BERT shapes it measured no faster
-  // than the plain launch (profiles/r1_gemm_tail_ab.txt): a partial last wave of 3-12 tiles
-  // runs at its uncontended rate and costs about what the extra launches do
-  int64_t tail_m0 = 0;
-  int tail_s = 0;
-  if (big && p.splitk == 1 && epi && epi->workspace) {
-    const char* te = getenv("MMU_GEMM_TAIL");
-    const int cus = cu_count();
-    const int64_t per_row = batch * p.tiles_n;  // tiles per M-tile row (all batch items)
-    const int64_t tiles = per_row * p.tiles_m;
-    const int64_t rem = tiles % cus;
-    if (te && te[0] == '1' && tiles > cus && rem > 0 && rem * 4 <= cus) {
-      const int64_t peel = (rem + per_row - 1) / per_row;
-      const int64_t m0 = (int64_t)(p.tiles_m - peel) * 256;
-      const int64_t mt = M - m0, kit = (K + 63) / 64;
-      // slices: balance the slice's main loop (~1.4 us per 64-deep step) against reading
-      // the slabs back (~5 TB/s): S ~ sqrt(k-steps * 7e6 / slab bytes)
-      const double slab_bytes = 4.0 * (double)mt * (double)N * (double)batch;
-      int64_t S = (int64_t)(sqrt((double)kit * 7.0e6 / slab_bytes) + 0.5);
-      const int64_t max_s = cus / (peel * per_row) > 1 ? cus / (peel * per_row) : 1;
-      if (S > max_s) S = max_s;
-      if (S > kit) S = kit;
-      const int64_t cap = epi->workspace_floats / (batch * mt * N);
-      if (S > cap) S = cap;
-      if (S >= 2 && m0 > 0) {
-        tail_m0 = m0;
-        tail_s = (int)S;
-      }
-    }
-  }
   hipStream_t s = (hipStream_t)stream;
   bool timed;
   std::pair<hipEvent_t, hipEvent_t> ev;
@@ -221,30 +172,8 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
     ev = take_events();
     (void)hipEventRecord(ev.first, s);
   }
-  if (tail_s) {
-    GemmParams t = p;  // the peeled rows as a split-K product into f32 slabs
-    t.A = a_kmajor ? p.A + tail_m0 * lda : p.A + tail_m0;
-    t.M = M - tail_m0;
-    t.tiles_m = (int)((t.M + 255) / 256);
-    t.group_m = 1;
-    t.kind = MMU_EPI_STORE;
-    t.accumulate = 0;
-    t.bias = nullptr;
-    t.colsum = nullptr;
-    t.residual = nullptr;
-    t.aux = nullptr;
-    t.drop_p = 0.f;
-    t.splitk = tail_s;
-    t.kchunk = ((K + tail_s - 1) / tail_s + 63) / 64 * 64;
-    t.splitk = (int)((K + t.kchunk - 1) / t.kchunk);
-    t.ws = epi->workspace;
-    tail_s = t.splitk;
-    gemm_launch(t, a_kmajor != 0, b_kmajor != 0, true, true, (int)batch, s);
-    p.tiles_m -= (int)((M - tail_m0) / 256 + ((M - tail_m0) % 256 ? 1 : 0));
-  }
   gemm_launch(p, a_kmajor != 0, b_kmajor != 0, c_dtype == MMU_F32, big, (int)batch, s);
   if (p.splitk > 1) splitk_reduce_launch(p, (int)batch, s);
-  if (tail_s) gemm_tail_launch(p, c_dtype == MMU_F32, tail_m0, tail_s, epi->workspace, (int)batch, s);
   if (timed) {
     (void)hipEventRecord(ev.second, s);
     std::lock_guard<std::mutex> lk(g_t.mu);
@@ -281,6 +210,7 @@ static int attn_common(int64_t ld_qkv, int64_t batch, int64_t L, int64_t heads, 
   if (ld_qkv < 3 * heads * 64 || ld_qkv % 8) return fail("attention: ld_qkv too small / unaligned");
   if (drop_p < 0.f || drop_p >= 1.f) return fail("attention: drop_p out of range");
   if ((int64_t)batch * heads > 65535 * 64) return fail("attention: batch*heads too large");
+  if (L > 576) return fail("attention: L=%ld > 576 (the kernels stage ceil(L/64) <= 9 key tiles)", L);
   return 0;
 }
 
@@ -289,7 +219,7 @@ int mmu_attention_fwd(const void* QKV, int64_t ld_qkv, const float* keymask, voi
                       mmu_stream_t stream) {
   if (!QKV || !keymask || !O || !LSE) return fail("mmu_attention_fwd: null pointer");
   if (attn_common(ld_qkv, batch, L, heads, drop_p)) return 1;
-  if (ld_o < heads * 64 || ld_o % 4) return fail("mmu_attention_fwd: bad ld_o");
+  if (ld_o < heads * 64 || ld_o % 8) return fail("mmu_attention_fwd: bad ld_o");
   if (batch * heads > 65535) return fail("mmu_attention_fwd: batch*heads > 65535");
   AttnParams p{};
   p.qkv = (const bf16*)QKV; p.ld_qkv = ld_qkv; p.keymask = keymask; p.out = (bf16*)O; p.ld_out = ld_o;
@@ -315,7 +245,6 @@ int mmu_attention_bwd(const void* QKV, int64_t ld_qkv, const float* keymask, con
   p.ld_out = ld_dqkv; p.batch = (int)batch; p.L = (int)L; p.heads = (int)heads; p.drop_p = drop_p; p.seed = seed;
   p.dropmask = (uint64_t*)dropmask;
   p.colsum = dbias_parts;
-  if (dbias_parts && !attention_bwd_fuses_colsum()) return fail("mmu_attention_bwd: dbias_parts need MMU_ATTN_DMA != 0");
   attention_bwd_launch(p, (hipStream_t)stream);
   return check_launch("mmu_attention_bwd");
 }
@@ -338,9 +267,33 @@ int mmu_layernorm_bwd(const void* dY, const void* X, const float* mean, const fl
   if (!dY || !X || !mean || !rstd || !w || !dX) return fail("mmu_layernorm_bwd: null pointer");
   if (rows <= 0 || H <= 0 || H % 256 || H > 1024 || rows_per_part <= 0) return fail("mmu_layernorm_bwd: bad shape");
   if (drop_p < 0.f || drop_p >= 1.f) return fail("mmu_layernorm_bwd: drop_p out of range");
-  layernorm_bwd_launch((const bf16*)dY, (const bf16*)X, mean, rstd, w, (bf16*)dX, (bf16*)dXdrop, nullptr, drop_p, seed,
+  layernorm_bwd_launch((const bf16*)dY, X, false, mean, rstd, w, (bf16*)dX, (bf16*)dXdrop, nullptr, drop_p, seed,
                        part_dw, part_db, part_dbias, rows, H, rows_per_part, (hipStream_t)stream);
   return check_launch("mmu_layernorm_bwd");
+}
+
+int mmu_layernorm_fwd_f32(const float* X, const float* w, const float* b, void* Y, float* Y32, float* mean,
+                          float* rstd, int64_t rows, int64_t H, float eps, int64_t group_rows, int64_t param_stride,
+                          mmu_stream_t stream) {
+  if (!X || !w || !b || !Y) return fail("mmu_layernorm_fwd_f32: null pointer");
+  if ((mean == nullptr) != (rstd == nullptr)) return fail("mmu_layernorm_fwd_f32: mean/rstd must both be given or NULL");
+  if (rows <= 0 || H <= 0 || H % 256 || H > 1024) return fail("mmu_layernorm_fwd_f32: H=%ld must be 256/512/768/1024", H);
+  if (group_rows <= 0) group_rows = rows;
+  if (param_stride < 0) return fail("mmu_layernorm_fwd_f32: bad param_stride");
+  layernorm_fwd32_launch(X, w, b, (bf16*)Y, Y32, mean, rstd, rows, H, eps, group_rows, param_stride,
+                         (hipStream_t)stream);
+  return check_launch("mmu_layernorm_fwd_f32");
+}
+
+int mmu_layernorm_bwd_f32(const void* dY, const float* X, const float* mean, const float* rstd, const float* w,
+                          void* dX, void* dXdrop, float drop_p, uint64_t seed, float* part_dw, float* part_db,
+                          float* part_dbias, int64_t rows, int64_t H, int64_t rows_per_part, mmu_stream_t stream) {
+  if (!dY || !X || !mean || !rstd || !w || !dX) return fail("mmu_layernorm_bwd_f32: null pointer");
+  if (rows <= 0 || H <= 0 || H % 256 || H > 1024 || rows_per_part <= 0) return fail("mmu_layernorm_bwd_f32: bad shape");
+  if (drop_p < 0.f || drop_p >= 1.f) return fail("mmu_layernorm_bwd_f32: drop_p out of range");
+  layernorm_bwd_launch((const bf16*)dY, X, true, mean, rstd, w, (bf16*)dX, (bf16*)dXdrop, nullptr, drop_p, seed,
+                       part_dw, part_db, part_dbias, rows, H, rows_per_part, (hipStream_t)stream);
+  return check_launch("mmu_layernorm_bwd_f32");
 }
 
 int mmu_layernorm_bwd_res(const void* dY, const void* X, const float* mean, const float* rstd, const float* w,
@@ -348,7 +301,7 @@ int mmu_layernorm_bwd_res(const void* dY, const void* X, const float* mean, cons
                           int64_t H, int64_t rows_per_part, mmu_stream_t stream) {
   if (!dY || !X || !mean || !rstd || !w || !dX || !dRes) return fail("mmu_layernorm_bwd_res: null pointer");
   if (rows <= 0 || H <= 0 || H % 256 || H > 1024 || rows_per_part <= 0) return fail("mmu_layernorm_bwd_res: bad shape");
-  layernorm_bwd_launch((const bf16*)dY, (const bf16*)X, mean, rstd, w, (bf16*)dX, nullptr, (const bf16*)dRes, 0.f, 0,
+  layernorm_bwd_launch((const bf16*)dY, X, false, mean, rstd, w, (bf16*)dX, nullptr, (const bf16*)dRes, 0.f, 0,
                        part_dw, part_db, part_dbias, rows, H, rows_per_part, (hipStream_t)stream);
   return check_launch("mmu_layernorm_bwd_res");
 }
@@ -398,8 +351,8 @@ int mmu_seqattn_bwd(const void* QKV, int64_t ld_qkv, const void* O, int64_t ld_o
 int mmu_embed_fwd(const int64_t* ids, const int64_t* seg, const int64_t* txt_mask, const float* proj, const float* word,
                   const float* pos, const float* type, const float* ln_w, const float* ln_b, float eps, int64_t cls_id,
                   int64_t sep_id, const int64_t* idx, int64_t V, int64_t B, int64_t T, int64_t n_img, int64_t Lout,
-                  int64_t H, float drop_txt, float drop_img, uint64_t seed, void* X, float* keymask, float* mean,
-                  float* rstd, mmu_stream_t stream) {
+                  int64_t H, float drop_txt, float drop_img, uint64_t seed, void* X, float* X32, float* keymask,
+                  float* mean, float* rstd, mmu_stream_t stream) {
   if (H != 768) return fail("mmu_embed_fwd: H must be 768");
   if (!word || !pos || !type || !ln_w || !ln_b || !X || !keymask || !proj) return fail("mmu_embed_fwd: null pointer");
   if (T > 0 && (!ids || !seg)) return fail("mmu_embed_fwd: text ids/segments missing");
@@ -408,7 +361,7 @@ int mmu_embed_fwd(const int64_t* ids, const int64_t* seg, const int64_t* txt_mas
   EmbedParams p{};
   p.ids = ids; p.seg = seg; p.txt_mask = txt_mask; p.idx = idx; p.proj = proj; p.word = word; p.pos = pos;
   p.type = type; p.ln_w = ln_w; p.ln_b = ln_b; p.eps = eps; p.cls_id = cls_id; p.sep_id = sep_id; p.V = V; p.B = B;
-  p.T = T; p.n_img = n_img; p.Lout = Lout; p.H = H; p.X = (bf16*)X;
+  p.T = T; p.n_img = n_img; p.Lout = Lout; p.H = H; p.X = (bf16*)X; p.X32 = X32;
   if (drop_txt < 0.f || drop_txt >= 1.f || drop_img < 0.f || drop_img >= 1.f) return fail("mmu_embed_fwd: bad dropout");
   p.drop_txt = drop_txt; p.drop_img = drop_img; p.seed = seed; p.keymask = keymask; p.mean = mean; p.rstd = rstd;
   embed_fwd_launch(p, (hipStream_t)stream);

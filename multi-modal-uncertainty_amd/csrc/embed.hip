@@ -86,6 +86,7 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbedParams p) {
       for (int k = 0; k < 4; ++k) y[k] = ((keep >> k) & 1) ? y[k] * dsc : 0.f;
     }
     *(bf16x4*)(p.X + row * 768 + c) = bf16x4{f2bf(y[0]), f2bf(y[1]), f2bf(y[2]), f2bf(y[3])};
+    if (p.X32) *(float4*)(p.X32 + row * 768 + c) = make_float4(y[0], y[1], y[2], y[3]);  // the f32 hidden stream
   }
   if (l == 0) {
     p.keymask[row] = km;

@@ -108,7 +108,7 @@ static __device__ __forceinline__ bf16x8 s_frag(const char* s, int row0, int ks,
 // one (m, n..n+7) octet: epilogue math + store; v holds acc (+ bias) on entry
 template <int EPI, bool OUT_F32>
 static __device__ __forceinline__ void epi_oct(const GemmParams& p, int64_t z, int64_t m, int64_t n, float (&v)[8],
-                                               const bf16x8& in, bf16* aux, float scale, uint32_t thr) {
+                                               const float (&in)[8], bf16* aux, float scale, uint32_t thr) {
   if (EPI == MMU_EPI_BIAS_GELU) {  // C = gelu(z); aux (optional) = gelu'(z) for the backward
     float d[8];
 #pragma unroll
@@ -127,7 +127,7 @@ static __device__ __forceinline__ void epi_oct(const GemmParams& p, int64_t z, i
       for (int r = 0; r < 8; ++r) v[r] = ((keep >> r) & 1) ? v[r] * scale : 0.f;
     }
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] += bf2f(in[r]);  // residual
+    for (int r = 0; r < 8; ++r) v[r] += in[r];  // residual (f32 when C is f32: the hidden stream)
   } else if (EPI == MMU_EPI_BIAS_DROP_QGELU) {  // FLAVA mlp: u = dropout(z); C = u*sigmoid(1.702u)
     uint32_t keep = 0xFFu;                         // aux (optional) = dC/dz = keep*scale*qgelu'(u)
     if (thr) {
@@ -151,10 +151,10 @@ static __device__ __forceinline__ void epi_oct(const GemmParams& p, int64_t z, i
     }
   } else if (EPI == MMU_EPI_DGELU) {  // in = aux = gelu'(z) saved by the forward epilogue
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] *= bf2f(in[r]);
+    for (int r = 0; r < 8; ++r) v[r] *= in[r];
   } else if (EPI == MMU_EPI_ADD_RES) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] += bf2f(in[r]);  // residual
+    for (int r = 0; r < 8; ++r) v[r] += in[r];  // residual
   }
   if (OUT_F32) {
     float4* C = (float4*)((float*)p.C + z * p.sC + m * p.ldc + n);
@@ -202,17 +202,31 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
 #pragma unroll
   for (int r = 0; r < 8; ++r) cs[r] = 0.f;
   constexpr bool LOADS = EPI == MMU_EPI_BIAS_DROP_RES || EPI == MMU_EPI_DGELU || EPI == MMU_EPI_ADD_RES;
+  // BIAS_DROP_RES into an f32 C reads an f32 residual: the encoder's f32 hidden stream
+  constexpr bool RES32 = OUT_F32 && EPI == MMU_EPI_BIAS_DROP_RES;
   const bf16* src = EPI == MMU_EPI_DGELU ? (const bf16*)aux : res;
+  const float* src32 = RES32 && p.residual ? (const float*)p.residual + z * p.res_bstride : nullptr;
   const int64_t lds_ = EPI == MMU_EPI_DGELU ? p.ldx : p.ldr;
 #pragma unroll
   for (int pass = 0; pass < NJ / PJ; ++pass) {
     // the pass's residual / aux rows are requested up front: one memory latency per pass
-    bf16x8 in[2 * PJ];
+    bf16x8 in[RES32 ? 1 : 2 * PJ];
+    float4 in32[RES32 ? 2 * PJ : 1][2];
 #pragma unroll
     for (int it = 0; it < 2 * PJ; ++it) {
       const int64_t m = mw + 16 * PJ * pass + rr + 8 * it;
-      if (LOADS && !slab && m < p.M) in[it] = *(const bf16x8*)(src + m * lds_ + n);
-      else in[it] = bf16x8{};
+      if (RES32) {
+        if (!slab && m < p.M) {
+          in32[it][0] = *(const float4*)(src32 + m * lds_ + n);
+          in32[it][1] = *(const float4*)(src32 + m * lds_ + n + 4);
+        } else {
+          in32[it][0] = in32[it][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      } else if (LOADS && !slab && m < p.M) {
+        in[it] = *(const bf16x8*)(src + m * lds_ + n);
+      } else {
+        in[it] = bf16x8{};
+      }
     }
 #pragma unroll
     for (int jj = 0; jj < PJ; ++jj) {
@@ -238,7 +252,15 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
       }
       float v[8] = {lo.x + bv[0], lo.y + bv[1], lo.z + bv[2], lo.w + bv[3],
                     hi.x + bv[4], hi.y + bv[5], hi.z + bv[6], hi.w + bv[7]};
-      epi_oct<EPI, OUT_F32>(p, z, m, n, v, in[it], aux, scale, thr);
+      float inf[8];
+      if (RES32) {
+        inf[0] = in32[it][0].x; inf[1] = in32[it][0].y; inf[2] = in32[it][0].z; inf[3] = in32[it][0].w;
+        inf[4] = in32[it][1].x; inf[5] = in32[it][1].y; inf[6] = in32[it][1].z; inf[7] = in32[it][1].w;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) inf[r] = LOADS ? bf2f(in[RES32 ? 0 : it][r]) : 0.f;
+      }
+      epi_oct<EPI, OUT_F32>(p, z, m, n, v, inf, aux, scale, thr);
       if (want_cs) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) cs[e] += v[e];
@@ -557,452 +579,11 @@ void conv3x3_wgrad_launch(const GemmParams& p, hipStream_t s) {
   if (p.splitk > 1) splitk_reduce_launch(p, 1, s);
 }
 
-// ================================================================ persistent 256x256
-// gemm_big_kernel's tile, wave split, LDS images and K loop, but one workgroup per CU that
-// walks a list of tiles, with the 2-stage LDS-DMA pipeline running ACROSS tile boundaries:
-// the last K-step of a tile issues the first K-tile of the next one, so that tile's
-// operands are in LDS when the epilogue ends (a fresh workgroup instead waits a full
-// HBM / Infinity-Cache latency before its first MFMA), and the epilogue's stores drain
-// while the next tile's first K-step computes.  The epilogue turns its accumulators around
-// in the stage the last K-step just released (8 KiB per wave: 32-row passes); a barrier
-// after it retires those reads before the next DMA writes that stage.
-// Work list: the XCD that runs workgroup lin (lin % 8) owns a contiguous range of pids in
-// the same bijective partition xcd_remap uses, and its workgroups take that range's pids
-// round-robin, so an XCD works through consecutive (grouped) tiles as gemm_big_kernel's
-// dispatch order does.
-template <bool AK, bool BKM, int EPI, bool OUT_F32>
-__global__ __launch_bounds__(512) void gemm_persist_kernel(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * B_STAGE];
-  const int t = threadIdx.x, l_ = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wm = w >> 2, wn = w & 3;
-  const int ntiles = p.tiles_m * p.tiles_n;
-  const int per_z = ntiles * p.splitk;
-  const int total = per_z * p.batch;
-  const int G = (int)gridDim.x;
-  const int lin = (int)blockIdx.x, xcd = lin & 7;
-  // this XCD's pid range [xs, xe) (xcd_remap's partition of `total`) and its workgroup count
-  const int q8 = total >> 3, r8 = total & 7;
-  const int xs = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
-  const int xe = xs + (xcd < r8 ? q8 + 1 : q8);
-  const int gx = (G - xcd + 7) >> 3;
-  int pid = xs + (lin >> 3);
-  if (pid >= xe) return;
-  if (p.stagger > 0 && ((lin >> 3) & 1)) {  // A/B: half of each XCD's CUs start later (de-phase epilogues)
-    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
-  }
-
-  const int64_t a_bytes = (AK ? p.M * p.lda : p.K * p.lda) * 2;
-  const int64_t b_bytes = (BKM ? p.N * p.ldb : p.K * p.ldb) * 2;
-  struct Item {
-    int64_t z, m0, n0, kb;
-    int slice, nk;
-  };
-  auto decode = [&](int id) {
-    Item it;
-    it.z = id / per_z;
-    const int r = id - (int)it.z * per_z;
-    it.slice = r / ntiles;
-    int tm, tn;
-    tile_of(r - it.slice * ntiles, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
-    it.m0 = (int64_t)tm * BBM;
-    it.n0 = (int64_t)tn * BBN;
-    it.kb = (int64_t)it.slice * p.kchunk;
-    const int64_t ke = it.kb + p.kchunk < p.K ? it.kb + p.kchunk : p.K;
-    it.nk = (int)((ke - it.kb + BKT - 1) / BKT);
-    return it;
-  };
-  auto rsrc_a = [&](int64_t z) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + z * p.sA), 0, (int)(uint32_t)a_bytes, 0x00020000);
-  };
-  auto rsrc_b = [&](int64_t z) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(p.B + z * p.sB), 0, (int)(uint32_t)b_bytes, 0x00020000);
-  };
-
-  Item cur = decode(pid);
-  {
-    const int l = l_;
-    const __amdgpu_buffer_rsrc_t ra = rsrc_a(cur.z), rb = rsrc_b(cur.z);
-    dma_tile<AK>(smem, ra, p.lda, cur.m0, cur.kb, w, l);
-    dma_tile<BKM>(smem + B_TILE, rb, p.ldb, cur.n0, cur.kb, w, l);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int stage = 0;
-  f32x4 acc[4][8];
-  while (true) {
-    // lane-derived addresses are re-derived per tile rather than kept live across the
-    // epilogue and the loop (hoisted, they cost ~40 VGPRs and spill the M-major variants)
-    int l = l_;
-    asm volatile("" : "+v"(l));
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const bool has_next = pid + gx < xe;
-    for (int kt = 0; kt < cur.nk; ++kt) {
-      const char* sa = smem + stage * B_STAGE;
-      const char* sb = sa + B_TILE;
-      char* d = smem + (stage ^ 1) * B_STAGE;
-      if (kt + 1 < cur.nk) {
-        const int64_t k1 = cur.kb + (int64_t)(kt + 1) * BKT;
-        dma_tile<AK>(d, rsrc_a(cur.z), p.lda, cur.m0, k1, w, l);
-        dma_tile<BKM>(d + B_TILE, rsrc_b(cur.z), p.ldb, cur.n0, k1, w, l);
-      } else if (has_next) {  // the next tile's first K-tile
-        const Item nx = decode(pid + gx);
-        dma_tile<AK>(d, rsrc_a(nx.z), p.lda, nx.m0, nx.kb, w, l);
-        dma_tile<BKM>(d + B_TILE, rsrc_b(nx.z), p.ldb, nx.n0, nx.kb, w, l);
-      }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 fb[4], fa[8];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fb[i] = s_frag<BKM, 512>(sb, 64 * wn + 16 * i, ks, l);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) fa[j] = s_frag<AK, 512>(sa, 128 * wm + 16 * j, ks, l);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      stage ^= 1;
-    }
-    // the stage the last K-step read is free: 8 KiB of it per wave as epilogue scratch
-    epilogue_block<EPI, OUT_F32, 8, 2>(p, cur.z, cur.slice, cur.m0 + 128 * wm, cur.n0 + 64 * wn, acc, l,
-                                       smem + (stage ^ 1) * B_STAGE + w * 8192);
-    if (!has_next) break;
-    // every wave's scratch reads are done before the next DMA into that stage (raw barrier:
-    // the epilogue's global stores need not drain here)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    pid += gx;
-    cur = decode(pid);
-  }
-}
-
-// ================================================================ pipelined 256x256 (8 phases / 2 K-tiles)
-// Same tile and wave split as gemm_big_kernel, but each 64-deep K-tile is four phases,
-// one per wave-output quadrant (64 m x 32 n, 16 MFMAs), and each stage is four 16 KiB
-// HALF images so that one half of the NEXT K-tile is DMA'd per phase:
-//   half A0/A1 = rows 128*wm + 64*h + [0,64)  of the A tile   (h = quadrant m index)
-//   half B0/B1 = cols  64*wn + 32*h + [0,32)  of the B tile   (h = quadrant n index)
-//   phase 1: Q(0,0) reads A0,B0 | DMA A0(t+1) | vmcnt
-//   phase 2: Q(0,1) reads B1    | DMA B0(t+1) | vmcnt
-//   phase 3: Q(1,1) reads A1    | DMA B1(t+1)
-//   phase 4: Q(1,0) (A1,B0 in registers) | DMA A1(t+1) | vmcnt
-// Every wait is a COUNTED vmcnt before the phase's first barrier (2 half-tiles = 4 DMAs
-// stay in flight across barriers), and every half is read >= 1 phase after the wait that
-// retired it; a half is re-staged >= 4 phases after its last read.  Raw s_barrier only
-// (a __syncthreads would drain the DMA queue), one __shared__ array.
-constexpr int P_HALF = 128 * BKT * 2;  // 16 KiB
-constexpr int P_STAGE = 4 * P_HALF;    // A0 A1 B0 B1
-
-// one half image: K-major [128 rows][128 B] (chunk ^ row&7) or M/N-major [64 k][256 B]
-// (32-B block ^ sw_mn(k)); local row/col r of half h, wave-group size G (64 for A, 32 for B)
-// maps to operand row (2G)*(r/G) + G*h + r%G.
-template <bool KMAJ, int G>
-static __device__ __forceinline__ void dma_half(char* s, __amdgpu_buffer_rsrc_t rsrc, int64_t ld, int64_t r0, int h,
-                                                int64_t k0, int w, int l) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int piece = w * 2 + i;  // 1 KiB piece of the 16 KiB half
-    uint32_t src;
-    if (KMAJ) {
-      const int row = piece * 8 + (l >> 3), c = (l & 7) ^ (row & 7);
-      const int64_t gr = r0 + 2 * G * (row / G) + G * h + row % G;
-      src = (uint32_t)((gr * ld + k0 + 8 * c) * 2);
-    } else {
-      const int kr = piece * 4 + (l >> 4), j = l & 15;
-      const int cc = 16 * ((j >> 1) ^ sw_mn(kr)) + 8 * (j & 1);
-      const int64_t gc = r0 + 2 * G * (cc / G) + G * h + cc % G;
-      src = (uint32_t)(((k0 + kr) * ld + gc) * 2);
-    }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (MMU_LDS(void)*)(s + piece * 1024), 16, src, 0, 0, 0);
-  }
-}
-
-static __device__ __forceinline__ void bar() {
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-template <bool AK, bool BKM, int EPI, bool OUT_F32>
-__global__ __launch_bounds__(512) void gemm_pipe_kernel(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * P_STAGE];
-  const int t = threadIdx.x, l = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wm = w >> 2, wn = w & 3;
-  int tm, tn, slice;
-  int64_t z;
-  block_tile(p, z, slice, tm, tn);
-  const int64_t m0 = (int64_t)tm * BBM, n0 = (int64_t)tn * BBN;
-  const int64_t a_bytes = (AK ? p.M * p.lda : p.K * p.lda) * 2;
-  const int64_t b_bytes = (BKM ? p.N * p.ldb : p.K * p.ldb) * 2;
-  const __amdgpu_buffer_rsrc_t ra =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + z * p.sA), 0, (int)(uint32_t)a_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(p.B + z * p.sB), 0, (int)(uint32_t)b_bytes, 0x00020000);
-
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int64_t kb = (int64_t)slice * p.kchunk;
-  const int64_t ke = kb + p.kchunk < p.K ? kb + p.kchunk : p.K;
-  const int nk = (int)((ke - kb + BKT - 1) / BKT);
-  dma_half<AK, 64>(smem + 0 * P_HALF, ra, p.lda, m0, 0, kb, w, l);
-  dma_half<BKM, 32>(smem + 2 * P_HALF, rb, p.ldb, n0, 0, kb, w, l);
-  dma_half<BKM, 32>(smem + 3 * P_HALF, rb, p.ldb, n0, 1, kb, w, l);
-  dma_half<AK, 64>(smem + 1 * P_HALF, ra, p.lda, m0, 1, kb, w, l);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  bar();
-
-  bf16x8 fa[2][4], fb0[2][2], fb1[2][2];
-  auto read_a = [&](const char* s) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) fa[ks][j] = s_frag<AK, 256>(s, 64 * wm + 16 * j, ks, l);
-  };
-  auto read_b = [&](const char* s, bf16x8 (&fb)[2][2]) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) fb[ks][i] = s_frag<BKM, 256>(s, 32 * wn + 16 * i, ks, l);
-  };
-  auto mma = [&](const bf16x8 (&fb)[2][2], int nq, int mq) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[2 * nq + i][4 * mq + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ks][i], fa[ks][j], acc[2 * nq + i][4 * mq + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* cur = smem + (kt & 1) * P_STAGE;
-    char* nxt = smem + ((kt + 1) & 1) * P_STAGE;
-    const bool more = kt + 1 < nk;
-    const int64_t k1 = kb + (int64_t)(kt + 1) * BKT;
-    // phase 1: Q(0,0)
-    read_a(cur + 0 * P_HALF);
-    read_b(cur + 2 * P_HALF, fb0);
-    if (more) {
-      dma_half<AK, 64>(nxt + 0 * P_HALF, ra, p.lda, m0, 0, k1, w, l);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    }
-    bar();
-    mma(fb0, 0, 0);
-    bar();
-    // phase 2: Q(0,1)
-    read_b(cur + 3 * P_HALF, fb1);
-    if (more) {
-      dma_half<BKM, 32>(nxt + 2 * P_HALF, rb, p.ldb, n0, 0, k1, w, l);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    bar();
-    mma(fb1, 1, 0);
-    bar();
-    // phase 3: Q(1,1)
-    read_a(cur + 1 * P_HALF);
-    if (more) dma_half<BKM, 32>(nxt + 3 * P_HALF, rb, p.ldb, n0, 1, k1, w, l);
-    bar();
-    mma(fb1, 1, 1);
-    bar();
-    // phase 4: Q(1,0)
-    if (more) {
-      dma_half<AK, 64>(nxt + 1 * P_HALF, ra, p.lda, m0, 1, k1, w, l);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    }
-    bar();
-    mma(fb0, 0, 1);
-    bar();
-  }
-  epilogue_block<EPI, OUT_F32, 8>(p, z, slice, m0 + 128 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
-}
-
-// ================================================================ duo: 256x128, 4 waves, 2 blocks / CU
-// The 256x256 kernels hold one block per CU (128 KiB of LDS), so a tile's epilogue (HBM
-// stores, residual / aux reads, GELU) leaves the CU's matrix cores idle.  This variant
-// halves the block -- 256 x 128 tile, 4 waves of the same 128 x 64 per-wave tile -- and
-// its K step (BK = 32, 3-stage LDS-DMA ring = 72 KiB), so TWO blocks share a CU and one
-// block's epilogue overlaps the other's main loop.
-//  * K-major images: [rows][64 B], 16-B chunk c of row r at c ^ (((r >> 3) & 1) * 3)
-//    (enumerated conflict-free for the 16x16x32 operand's ds_read_b128 lane groups)
-//  * M/N-major images: [32 k][256 | 512 B] with the 32-B block ^ sw_mn(k) of the big kernel
-constexpr int DBK = 32;
-constexpr int D_A = 256 * DBK * 2;  // 16 KiB
-constexpr int D_B = 128 * DBK * 2;  //  8 KiB
-constexpr int D_STAGE = D_A + D_B;
-constexpr int D_NS = 3;
-
-static __device__ __forceinline__ int g64(int r) { return ((r >> 3) & 1) * 3; }
-
-// operand fragments of one 32-deep K step: K-major 64-B rows / M,N-major ROWB-byte k-rows
-static __device__ __forceinline__ bf16x8 d_frag_k(const char* s, int row0, int l) {
-  const int row = row0 + (l & 15), c = l >> 4;
-  return *(const bf16x8*)(s + row * 64 + ((c ^ g64(row)) << 4));
-}
-template <int ROWB>
-static __device__ __forceinline__ bf16x8 d_frag_mn(const char* s, int row0, int l) {
-  return s_frag<false, ROWB>(s, row0, 0, l);
-}
-
-// ROWS x 32 k operand tile into LDS, PIECES 1-KiB DMA pieces per wave (4 waves)
-template <bool KMAJ, int ROWS>
-static __device__ __forceinline__ void d_dma(char* s, __amdgpu_buffer_rsrc_t rsrc, int64_t ld, int64_t r0, int64_t k0,
-                                             int w, int l) {
-  constexpr int PIECES = ROWS * DBK * 2 / 1024 / 4;
-#pragma unroll
-  for (int i = 0; i < PIECES; ++i) {
-    const int piece = w * PIECES + i;
-    uint32_t src;
-    if (KMAJ) {  // 16 rows x 64 B per piece
-      const int row = piece * 16 + (l >> 2), c = (l & 3) ^ g64(row);
-      src = (uint32_t)(((r0 + row) * ld + k0 + 8 * c) * 2);
-    } else {     // 1024 / (2 ROWS) k-rows per piece
-      constexpr int KPP = 1024 / (2 * ROWS), UPR = 2 * ROWS / 16;  // k-rows per piece, 16-B units per k-row
-      const int kr = piece * KPP + l / UPR, j = l % UPR;
-      const int b = (j >> 1) ^ sw_mn(kr);
-      src = (uint32_t)(((k0 + kr) * ld + r0 + 16 * b + 8 * (j & 1)) * 2);
-    }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (MMU_LDS(void)*)(s + piece * 1024), 16, src, 0, 0, 0);
-  }
-}
-
-template <bool AK, bool BKM, int EPI, bool OUT_F32>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void gemm_duo_kernel(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[D_NS * D_STAGE];
-  const int t = threadIdx.x, l = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wm = w >> 1, wn = w & 1;
-  int tm, tn, slice;
-  int64_t z;
-  block_tile(p, z, slice, tm, tn);
-  if (p.stagger > 0) {  // first-round blocks 256..511 (the second slot of each CU) start half a tile late
-    const int lin = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
-    if (lin >= 256 && lin < 512)
-      for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
-  }
-  const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * 128;
-  const int64_t a_bytes = (AK ? p.M * p.lda : p.K * p.lda) * 2;
-  const int64_t b_bytes = (BKM ? p.N * p.ldb : p.K * p.ldb) * 2;
-  const __amdgpu_buffer_rsrc_t ra =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + z * p.sA), 0, (int)(uint32_t)a_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(p.B + z * p.sB), 0, (int)(uint32_t)b_bytes, 0x00020000);
-
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int64_t kb = (int64_t)slice * p.kchunk;
-  const int64_t ke = kb + p.kchunk < p.K ? kb + p.kchunk : p.K;
-  const int nk = (int)((ke - kb + DBK - 1) / DBK);
-  auto issue = [&](int kt) {
-    char* st = smem + (kt % D_NS) * D_STAGE;
-    const int64_t k0 = kb + (int64_t)kt * DBK;
-    d_dma<AK, 256>(st, ra, p.lda, m0, k0, w, l);
-    d_dma<BKM, 128>(st + D_A, rb, p.ldb, n0, k0, w, l);
-  };
-  // DMAs per wave per stage: A 4 + B 2
-  for (int kt = 0; kt < D_NS - 1 && kt < nk; ++kt) issue(kt);
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (kt + D_NS - 1 < nk) issue(kt + D_NS - 1);  // into the stage of kt-1: every wave is past it
-    const char* sa = smem + (kt % D_NS) * D_STAGE;
-    const char* sb = sa + D_A;
-    bf16x8 fb[4], fa[8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      fb[i] = BKM ? d_frag_k(sb, 64 * wn + 16 * i, l) : d_frag_mn<256>(sb, 64 * wn + 16 * i, l);
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      fa[j] = AK ? d_frag_k(sa, 128 * wm + 16 * j, l) : d_frag_mn<512>(sa, 128 * wm + 16 * j, l);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
-  }
-  __builtin_amdgcn_s_barrier();  // every wave's last fragment reads are done: the ring is epilogue scratch
-  asm volatile("" ::: "memory");
-  epilogue_block<EPI, OUT_F32, 8>(p, z, slice, m0 + 128 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
-}
-
 // ---------------------------------------------------------------- launch
-// MMU_GEMM_PIPE=1 selects the 8-phase kernel (read per launch, for A/B comparisons).  On the
-// BERT shapes it measures within +-3 % of the 2-stage kernel and 10 % slower on the long-K
-// weight gradients (tools/gemm_bench.py), so the 2-stage kernel is the default.
-static bool use_pipe() {
-  const char* e = getenv("MMU_GEMM_PIPE");
-  return e && e[0] == '1';
-}
-
-// MMU_GEMM_DUO=1 selects the 256x128 two-blocks-per-CU kernel (A/B while it is evaluated)
-static bool use_duo() {
-  const char* e = getenv("MMU_GEMM_DUO");
-  return e && e[0] == '1';
-}
-
-// MMU_GEMM_PERSIST=1 selects the persistent kernel (A/B while it is evaluated)
-static bool use_persist() {
-  const char* e = getenv("MMU_GEMM_PERSIST");
-  return e && e[0] == '1';
-}
-
-static int gemm_cus() {
-  static int cache[64] = {};
-  int d = 0;
-  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return 256;
-  if (!cache[d]) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || n <= 0) n = 256;
-    cache[d] = n;
-  }
-  return cache[d];
-}
-
 template <bool AK, bool BKM, int EPI, bool F32>
 static void launch_t(const GemmParams& p, bool big, int batch, hipStream_t s) {
   dim3 grid(p.tiles_m * p.tiles_n, p.splitk, batch);
-  if (big && use_persist()) {
-    GemmParams q = p;
-    q.batch = batch;
-    const char* st = getenv("MMU_GEMM_STAGGER");
-    q.stagger = st ? atoi(st) : 0;
-    const int total = p.tiles_m * p.tiles_n * p.splitk * batch;
-    const int cus = gemm_cus();
-    hipLaunchKernelGGL((gemm_persist_kernel<AK, BKM, EPI, F32>), dim3(total < cus ? total : cus), dim3(512), 0, s, q);
-  } else if (big && use_duo()) {
-    GemmParams q = p;
-    const char* st = getenv("MMU_GEMM_STAGGER");
-    q.stagger = st ? atoi(st) : 0;
-    q.tiles_n = (int)((p.N + 127) / 128);
-    dim3 g2(q.tiles_m * q.tiles_n, q.splitk, batch);
-    hipLaunchKernelGGL((gemm_duo_kernel<AK, BKM, EPI, F32>), g2, dim3(256), 0, s, q);
-  } else if (big && use_pipe()) hipLaunchKernelGGL((gemm_pipe_kernel<AK, BKM, EPI, F32>), grid, dim3(512), 0, s, p);
-  else if (big) hipLaunchKernelGGL((gemm_big_kernel<AK, BKM, EPI, F32>), grid, dim3(512), 0, s, p);
+  if (big) hipLaunchKernelGGL((gemm_big_kernel<AK, BKM, EPI, F32>), grid, dim3(512), 0, s, p);
   else hipLaunchKernelGGL((gemm_small_kernel<AK, BKM, EPI, F32>), grid, dim3(256), 0, s, p);
 }
 
@@ -1021,7 +602,10 @@ void gemm_launch(const GemmParams& p, bool ak, bool bk, bool f32out, bool big, i
       else launch_e<MMU_EPI_STORE, false>(p, ak, bk, big, batch, s);
       break;
     case MMU_EPI_BIAS_GELU: launch_e<MMU_EPI_BIAS_GELU, false>(p, ak, bk, big, batch, s); break;
-    case MMU_EPI_BIAS_DROP_RES: launch_e<MMU_EPI_BIAS_DROP_RES, false>(p, ak, bk, big, batch, s); break;
+    case MMU_EPI_BIAS_DROP_RES:
+      if (f32out) launch_e<MMU_EPI_BIAS_DROP_RES, true>(p, ak, bk, big, batch, s);
+      else launch_e<MMU_EPI_BIAS_DROP_RES, false>(p, ak, bk, big, batch, s);
+      break;
     case MMU_EPI_DGELU: launch_e<MMU_EPI_DGELU, false>(p, ak, bk, big, batch, s); break;
     case MMU_EPI_ADD_RES: launch_e<MMU_EPI_ADD_RES, false>(p, ak, bk, big, batch, s); break;
     case MMU_EPI_BIAS_DROP_QGELU: launch_e<MMU_EPI_BIAS_DROP_QGELU, false>(p, ak, bk, big, batch, s); break;
@@ -1048,80 +632,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     a.x += o.x; a.y += o.y; a.z += o.z; a.w += o.w;
   }
   *(float4*)c = a;
-}
-
-// ------------------------------------------------------------------ split-K tail
-// The last partial wave of 256x256 tiles (e.g. 3 tiles after 6 full waves of 256 at M =
-// 131328, N = 768) would hold the whole chip for a full tile time.  The host instead
-// peels those M-tile rows off the main launch, runs them as a split-K product into f32
-// slabs (rows m0.. of the workspace, slice-major) and finishes them here: slabs summed in
-// slice order, then the product's own epilogue (bias, GELU / dropout+residual / dGELU /
-// residual, column sums) at the GLOBAL row m, so dropout counters and outputs are exactly
-// those of the unsplit launch.  Thread = one (m, 8-column octet); 4 row groups x 64 octets.
-constexpr int TAIL_RB = 8;  // rows per block (2 per thread)
-template <int EPI, bool OUT_F32>
-__global__ __launch_bounds__(256) void gemm_tail_kernel(GemmParams p, int64_t m0, int64_t mt, int S,
-                                                        const float* __restrict__ ws) {
-  const int t = threadIdx.x;
-  const int64_t n = 8 * ((int64_t)blockIdx.x * 64 + (t & 63));
-  const int64_t z = blockIdx.z;
-  if (n >= p.N) return;
-  const float* bias = (p.bias && EPI != MMU_EPI_DGELU && EPI != MMU_EPI_ADD_RES) ? p.bias + z * p.bias_bstride : nullptr;
-  const bf16* res = p.residual ? (const bf16*)p.residual + z * p.res_bstride : nullptr;
-  bf16* aux = p.aux ? (bf16*)p.aux + z * p.aux_bstride : nullptr;
-  constexpr bool LOADS = EPI == MMU_EPI_BIAS_DROP_RES || EPI == MMU_EPI_DGELU || EPI == MMU_EPI_ADD_RES;
-  const bf16* src = EPI == MMU_EPI_DGELU ? (const bf16*)aux : res;
-  const int64_t lds_ = EPI == MMU_EPI_DGELU ? p.ldx : p.ldr;
-  const float scale = p.drop_p > 0.f ? 1.0f / (1.0f - p.drop_p) : 1.0f;
-  const uint32_t thr = (uint32_t)(p.drop_p * 65536.0f + 0.5f);
-  float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (bias) {
-    const float4 b0 = *(const float4*)(bias + n), b1 = *(const float4*)(bias + n + 4);
-    bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w; bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
-  }
-  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int64_t slab = mt * p.N;
-#pragma unroll
-  for (int i = 0; i < TAIL_RB / 4; ++i) {
-    const int64_t r = (int64_t)blockIdx.y * TAIL_RB + (t >> 6) + 4 * i;
-    if (r >= mt) break;
-    const int64_t m = m0 + r;
-    const bf16x8 in = LOADS ? *(const bf16x8*)(src + m * lds_ + n) : bf16x8{};
-    const float* w = ws + z * S * slab + r * p.N + n;
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = bv[e];
-    for (int k = 0; k < S; ++k) {
-      const float4 lo = *(const float4*)(w + k * slab), hi = *(const float4*)(w + k * slab + 4);
-      v[0] += lo.x; v[1] += lo.y; v[2] += lo.z; v[3] += lo.w; v[4] += hi.x; v[5] += hi.y; v[6] += hi.z; v[7] += hi.w;
-    }
-    epi_oct<EPI, OUT_F32>(p, z, m, n, v, in, aux, scale, thr);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) cs[e] += v[e];
-  }
-  if (p.colsum) {
-    float* out = p.colsum + z * p.colsum_bstride + n;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) atomicAdd(out + e, cs[e]);
-  }
-}
-
-void gemm_tail_launch(const GemmParams& p, bool f32out, int64_t m0, int S, const float* ws, int batch, hipStream_t s) {
-  const int64_t mt = p.M - m0;
-  const dim3 g((unsigned)((p.N / 8 + 63) / 64), (unsigned)((mt + TAIL_RB - 1) / TAIL_RB), (unsigned)batch);
-#define TAIL(E, F) hipLaunchKernelGGL((gemm_tail_kernel<E, F>), g, dim3(256), 0, s, p, m0, mt, S, ws)
-  switch (p.kind) {
-    case MMU_EPI_STORE:
-      if (f32out) TAIL(MMU_EPI_STORE, true);
-      else TAIL(MMU_EPI_STORE, false);
-      break;
-    case MMU_EPI_BIAS_GELU: TAIL(MMU_EPI_BIAS_GELU, false); break;
-    case MMU_EPI_BIAS_DROP_RES: TAIL(MMU_EPI_BIAS_DROP_RES, false); break;
-    case MMU_EPI_DGELU: TAIL(MMU_EPI_DGELU, false); break;
-    case MMU_EPI_ADD_RES: TAIL(MMU_EPI_ADD_RES, false); break;
-    case MMU_EPI_BIAS_DROP_QGELU: TAIL(MMU_EPI_BIAS_DROP_QGELU, false); break;
-  }
-#undef TAIL
 }
 
 void splitk_reduce_launch(const GemmParams& p, int batch, hipStream_t s) {
@@ -1210,8 +720,6 @@ __global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16* __restrict
 void colsum_bf16_launch(const bf16* X, int64_t M, int64_t N, int64_t ld, float* part, float* out, int acc,
                         hipStream_t s) {
   const int64_t gx = (N / 8 + 63) / 64;
-  static const bool v1 = getenv("MMU_COLSUM_V1") && atoi(getenv("MMU_COLSUM_V1"));  // A/B: the atomic-only path
-  if (v1) part = nullptr;
   int64_t rpb = COLSUM_BF16_ROWS;
   if (part) {  // ~1 K blocks: rows per block a multiple of 16 in [64, 1024]
     rpb = (M * gx + 1023) / 1024;

@@ -152,11 +152,73 @@ __global__ __launch_bounds__(256) void ln_fwd2_kernel(const bf16* __restrict__ X
   }
 }
 
+// forward of the f32 hidden stream (the BERT encoder's LN input S = residual + branch, kept
+// in f32 so that the 24 post-LN residual adds of the 12 layers are not rounded to bf16):
+// one wave per row, 4 consecutive f32 per lane per 256-column slab (16-B loads), writes the
+// bf16 row (the next GEMM's operand) and, when Y32 is given, the f32 row (the next residual)
+template <int NV>  // H = 256 * NV
+__global__ __launch_bounds__(256) void ln_fwd32_kernel(const float* __restrict__ X, const float* __restrict__ w,
+                                                       const float* __restrict__ b, bf16* __restrict__ Y,
+                                                       float* __restrict__ Y32, float* __restrict__ mean,
+                                                       float* __restrict__ rstd, int64_t rows, float eps,
+                                                       int64_t group_rows, int64_t pstride) {
+  constexpr int H = 256 * NV;
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  auto load = [&](int64_t row, float4 (&x)[NV]) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) x[i] = *(const float4*)(X + row * H + 256 * i + 4 * l);
+  };
+  auto process = [&](int64_t row, const float4 (&x)[NV]) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) s += (x[i].x + x[i].y) + (x[i].z + x[i].w);
+    const float mu = wave_sum(s) / H;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const float d0 = x[i].x - mu, d1 = x[i].y - mu, d2 = x[i].z - mu, d3 = x[i].w - mu;
+      q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+    }
+    const float rs = rsqrtf(wave_sum(q) / H + eps);
+    const float* wr = w + (row / group_rows) * pstride;
+    const float* br = b + (row / group_rows) * pstride;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = 256 * i + 4 * l;
+      const float4 ww = *(const float4*)(wr + c), bb = *(const float4*)(br + c);
+      const float4 y = make_float4((x[i].x - mu) * rs * ww.x + bb.x, (x[i].y - mu) * rs * ww.y + bb.y,
+                                   (x[i].z - mu) * rs * ww.z + bb.z, (x[i].w - mu) * rs * ww.w + bb.w);
+      *(bf16x4*)(Y + row * H + c) = bf16x4{f2bf(y.x), f2bf(y.y), f2bf(y.z), f2bf(y.w)};
+      if (Y32) *(float4*)(Y32 + row * H + c) = y;
+    }
+    if (l == 0 && mean) { mean[row] = mu; rstd[row] = rs; }
+  };
+  const int64_t r0 = (int64_t)blockIdx.x * LN_FWD_ROWS;
+  const int64_t rend = r0 + LN_FWD_ROWS < rows ? r0 + LN_FWD_ROWS : rows;
+  for (int64_t row = r0 + wv; row < rend; row += 8) {
+    float4 xa[NV], xb[NV];
+    const bool two = row + 4 < rend;
+    load(row, xa);
+    if (two) load(row + 4, xb);
+    process(row, xa);
+    if (two) process(row + 4, xb);
+  }
+}
+
+static __device__ __forceinline__ void ld4f(const bf16* p, float (&o)[4]) {
+  const bf16x4 v = *(const bf16x4*)p;
+  o[0] = bf2f(v[0]); o[1] = bf2f(v[1]); o[2] = bf2f(v[2]); o[3] = bf2f(v[3]);
+}
+static __device__ __forceinline__ void ld4f(const float* p, float (&o)[4]) {
+  const float4 v = *(const float4*)p;
+  o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+}
+
 // block = 4 waves; each wave walks rows_per_part/4 rows, TWO rows per step (both rows' loads
 // in flight before either reduction: the loop is latency-bound on one row at a time);
 // partial column sums reduced through one reused LDS buffer (16 KiB: occupancy)
-template <int NV>  // H = 256 * NV
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ X,
+template <int NV, typename XT>  // H = 256 * NV; XT: the LN input's type (bf16, or f32 for the hidden stream)
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dY, const XT* __restrict__ X,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ w, bf16* __restrict__ dX,
                                                      bf16* __restrict__ dXd, const bf16* __restrict__ dR,
@@ -177,7 +239,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dY
       ww[i][e] = w[256 * i + 4 * l + e];
     }
   struct Row {
-    bf16x4 a[NV], x[NV];
+    bf16x4 a[NV];
+    float x[NV][4];
     float mu, rs;
   };
   auto load = [&](int64_t row, Row& R) {
@@ -187,7 +250,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dY
     for (int i = 0; i < NV; ++i)
       if (i < nv) {
         R.a[i] = *(const bf16x4*)(dY + row * H + 256 * i + 4 * l);
-        R.x[i] = *(const bf16x4*)(X + row * H + 256 * i + 4 * l);
+        ld4f(X + row * H + 256 * i + 4 * l, R.x[i]);
       }
   };
   auto process = [&](int64_t row, const Row& R) {
@@ -199,7 +262,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dY
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           dy[i][e] = bf2f(R.a[i][e]);
-          xh[i][e] = (bf2f(R.x[i][e]) - R.mu) * R.rs;
+          xh[i][e] = (R.x[i][e] - R.mu) * R.rs;
           g[i][e] = dy[i][e] * ww[i][e];
           s1 += g[i][e];
           s2 += g[i][e] * xh[i][e];
@@ -259,14 +322,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dY
   }
 }
 
-static bool ln_v2() {
-  const char* e = getenv("MMU_LN_V2");  // 0 = the 8-B row-per-wave forward (A/B)
-  return !(e && e[0] == '0');
-}
-
 void layernorm_fwd_launch(const bf16* X, const float* w, const float* b, bf16* Y, float* mean, float* rstd,
                           int64_t rows, int64_t H, float eps, int64_t group_rows, int64_t pstride, hipStream_t s) {
-  if (ln_v2() && (group_rows % 2 == 0 || group_rows >= rows || pstride == 0) && H % 256 == 0 && H <= 1024) {
+  if ((group_rows % 2 == 0 || group_rows >= rows || pstride == 0) && H % 256 == 0 && H <= 1024) {
     const dim3 g2((unsigned)(((rows + 1) / 2 + LN2_PAIRS - 1) / LN2_PAIRS));
 #define LNF2(NV) hipLaunchKernelGGL(ln_fwd2_kernel<NV>, g2, dim3(256), 0, s, X, w, b, Y, mean, rstd, rows, eps, \
                                     group_rows, pstride)
@@ -291,11 +349,27 @@ void layernorm_fwd_launch(const bf16* X, const float* w, const float* b, bf16* Y
 #undef LNF
 }
 
-void layernorm_bwd_launch(const bf16* dY, const bf16* X, const float* mean, const float* rstd, const float* w,
-                          bf16* dX, bf16* dXdrop, const bf16* dR, float drop_p, uint64_t seed, float* pdw, float* pdb,
-                          float* pdbias, int64_t rows, int64_t H, int64_t rpp, hipStream_t s) {
+void layernorm_fwd32_launch(const float* X, const float* w, const float* b, bf16* Y, float* Y32, float* mean,
+                            float* rstd, int64_t rows, int64_t H, float eps, int64_t group_rows, int64_t pstride,
+                            hipStream_t s) {
+  const dim3 g((unsigned)((rows + LN_FWD_ROWS - 1) / LN_FWD_ROWS));
+#define LNF32(NV) hipLaunchKernelGGL(ln_fwd32_kernel<NV>, g, dim3(256), 0, s, X, w, b, Y, Y32, mean, rstd, rows, eps, \
+                                     group_rows, pstride)
+  switch (H / 256) {
+    case 1: LNF32(1); break;
+    case 2: LNF32(2); break;
+    case 3: LNF32(3); break;
+    default: LNF32(4); break;
+  }
+#undef LNF32
+}
+
+template <typename XT>
+static void ln_bwd_launch_t(const bf16* dY, const XT* X, const float* mean, const float* rstd, const float* w,
+                            bf16* dX, bf16* dXdrop, const bf16* dR, float drop_p, uint64_t seed, float* pdw,
+                            float* pdb, float* pdbias, int64_t rows, int64_t H, int64_t rpp, hipStream_t s) {
   const dim3 g((unsigned)((rows + rpp - 1) / rpp));
-#define LNB(NV) hipLaunchKernelGGL(ln_bwd_kernel<NV>, g, dim3(256), 0, s, dY, X, mean, rstd, w, dX, dXdrop, dR, \
+#define LNB(NV) hipLaunchKernelGGL((ln_bwd_kernel<NV, XT>), g, dim3(256), 0, s, dY, X, mean, rstd, w, dX, dXdrop, dR, \
                                    drop_p, seed, pdw, pdb, pdbias, rows, (int)rpp)
   switch (H / 256) {
     case 1: LNB(1); break;
@@ -304,6 +378,15 @@ void layernorm_bwd_launch(const bf16* dY, const bf16* X, const float* mean, cons
     default: LNB(4); break;
   }
 #undef LNB
+}
+
+void layernorm_bwd_launch(const bf16* dY, const void* X, bool x_f32, const float* mean, const float* rstd,
+                          const float* w, bf16* dX, bf16* dXdrop, const bf16* dR, float drop_p, uint64_t seed,
+                          float* pdw, float* pdb, float* pdbias, int64_t rows, int64_t H, int64_t rpp, hipStream_t s) {
+  if (x_f32)
+    ln_bwd_launch_t(dY, (const float*)X, mean, rstd, w, dX, dXdrop, dR, drop_p, seed, pdw, pdb, pdbias, rows, H, rpp, s);
+  else
+    ln_bwd_launch_t(dY, (const bf16*)X, mean, rstd, w, dX, dXdrop, dR, drop_p, seed, pdw, pdb, pdbias, rows, H, rpp, s);
 }
 
 }  // namespace mmu

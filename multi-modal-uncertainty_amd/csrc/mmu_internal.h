@@ -31,8 +31,6 @@ struct GemmParams {
   int splitk;
   int64_t kchunk;
   float* ws;
-  int stagger;  // duo kernel: s_sleep(127) count for the second block of each CU (A/B experiment)
-  int batch;    // batch items (the persistent kernel's 1-D grid walks tiles x slices x batch)
   // 3x3 / stride 1 / pad 1 convolutions on an NHWC map [img * conv_h * conv_w pixels][conv_c]:
   // weight gradient (gemm_convw_kernel): B[pixel][tap * conv_c + ci] gathered;
   // forward / data gradient (gemm_conva_kernel): A[pixel][tap * conv_c + c] gathered
@@ -42,7 +40,6 @@ void conv3x3_wgrad_launch(const GemmParams& p, hipStream_t s);
 void conv3x3_implicit_launch(const GemmParams& p, hipStream_t s);
 
 void splitk_reduce_launch(const GemmParams& p, int batch, hipStream_t s);
-void gemm_tail_launch(const GemmParams& p, bool f32out, int64_t m0, int S, const float* ws, int batch, hipStream_t s);
 void gemm_launch(const GemmParams& p, bool a_kmajor, bool b_kmajor, bool f32out, bool big, int batch, hipStream_t s);
 void transpose_bf16_batched_launch(const int64_t* jobs, int n_jobs, int64_t max_rows, int64_t max_cols,
                                    hipStream_t s);
@@ -70,13 +67,16 @@ struct AttnParams {
 };
 void attention_fwd_launch(const AttnParams& p, hipStream_t s);
 void attention_bwd_launch(const AttnParams& p, hipStream_t s);
-bool attention_bwd_fuses_colsum();
 
 void layernorm_fwd_launch(const bf16* X, const float* w, const float* b, bf16* Y, float* mean, float* rstd,
                           int64_t rows, int64_t H, float eps, int64_t group_rows, int64_t pstride, hipStream_t s);
-void layernorm_bwd_launch(const bf16* dY, const bf16* X, const float* mean, const float* rstd, const float* w,
-                          bf16* dX, bf16* dXdrop, const bf16* dR, float drop_p, uint64_t seed, float* pdw, float* pdb,
-                          float* pdbias, int64_t rows, int64_t H, int64_t rows_per_part, hipStream_t s);
+void layernorm_fwd32_launch(const float* X, const float* w, const float* b, bf16* Y, float* Y32, float* mean,
+                            float* rstd, int64_t rows, int64_t H, float eps, int64_t group_rows, int64_t pstride,
+                            hipStream_t s);
+void layernorm_bwd_launch(const bf16* dY, const void* X, bool x_f32, const float* mean, const float* rstd,
+                          const float* w, bf16* dX, bf16* dXdrop, const bf16* dR, float drop_p, uint64_t seed,
+                          float* pdw, float* pdb, float* pdbias, int64_t rows, int64_t H, int64_t rows_per_part,
+                          hipStream_t s);
 
 // FLAVA attention over the sequence (= batch) axis, flava.hip
 struct SeqAttnParams {
@@ -103,6 +103,7 @@ struct EmbedParams {
   uint64_t seed;
   int64_t cls_id, sep_id, V, B, T, n_img, Lout, H;
   bf16* X;
+  float* X32;  // optional f32 copy of X (the encoder's f32 hidden stream)
   float *keymask, *mean, *rstd;
 };
 void embed_fwd_launch(const EmbedParams& p, hipStream_t s);

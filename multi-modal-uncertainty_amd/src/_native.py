@@ -42,6 +42,10 @@ SIGNATURES = {
     "mmu_layernorm_fwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_i64, c_i64, c_vp]),
     "mmu_layernorm_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp, c_vp, c_vp,
                                   c_i64, c_i64, c_i64, c_vp]),
+    "mmu_layernorm_fwd_f32": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_i64, c_i64,
+                                      c_vp]),
+    "mmu_layernorm_bwd_f32": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp, c_vp, c_vp,
+                                      c_i64, c_i64, c_i64, c_vp]),
     "mmu_layernorm_bwd_res": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                       c_i64, c_vp]),
     "mmu_seqattn_fwd": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp]),
@@ -49,7 +53,7 @@ SIGNATURES = {
                                 c_i64, c_vp]),
     "mmu_embed_fwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_i64, c_i64, c_vp,
                               c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_f32, c_f32, c_u64, c_vp, c_vp, c_vp, c_vp,
-                              c_vp]),
+                              c_vp, c_vp]),
     "mmu_embed_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64,
                               c_i64, c_i64, c_i64, c_f32, c_f32, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                               c_vp]),

@@ -95,15 +95,18 @@ class GradBucketer:
                 self.seg_to_buckets.setdefault(key, []).append(b)
         prefix = f"{self.enc._prefix}img_encoder."
         mods = dict(self.enc.img_encoder.named_modules(prefix=prefix[:-1]))
-        self._blocks = {key: mods[key] for key, _, _ in segs if key not in ("emb", "stem") and key in mods}
+        self._blocks = {key: mods[key] for key, _, _ in segs if key not in ("emb", "proj", "stem") and key in mods}
         self.layer_to_bucket = {i: b for b, bk in enumerate(buckets) for i in bk["layers"]}
         self.done_layers = set()
 
     def _segment_of(self, name):
-        """tail segment of a parameter: "emb" (text / image embeddings), the ResNet residual
+        """tail segment of a parameter: "emb" (text embeddings), "proj" (the image projection,
+        reported by ProjectFunction.backward once its dW / db are enqueued), the ResNet residual
         block ``<prefix>img_encoder.model.<stage>.<block>`` (stages 4..7 = layer1..layer4), or
         "stem"."""
         prefix = f"{self.enc._prefix}img_encoder."
+        if name.startswith(f"{self.enc._prefix}img_embeddings.img_embeddings."):
+            return "proj"
         if not name.startswith(prefix):
             return "emb"
         parts = name[len(prefix):].split(".")
@@ -139,8 +142,8 @@ class GradBucketer:
         self.launched.add(b)
 
     def _on_ready(self, lw):
-        if lw == "embeddings":
-            self._on_segment("emb")
+        if lw in ("embeddings", "proj"):
+            self._on_segment({"embeddings": "emb", "proj": "proj"}[lw])
             return
         if not self.enabled or self.world == 1 or not hasattr(lw, "module"):
             return

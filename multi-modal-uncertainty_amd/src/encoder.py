@@ -2,15 +2,20 @@
 autograd Function the encoder stacks (replaces pytorch_pretrained_bert BertLayer,
 called through ``self.encoder(...)`` at src/mmbt.py:124-126).
 
-Forward per layer (M = B*L token rows, bf16 activations, f32 accumulation):
+Forward per layer (M = B*L token rows, bf16 GEMM operands, f32 accumulation):
   qkv = X Wqkv^T + bqkv                       mmu_gemm  (fused Q|K|V, [M, 2304])
   O, lse = attention(qkv, keymask)            mmu_attention_fwd (dropout on P)
-  S1 = X + dropout(O Wo^T + bo)               mmu_gemm  EPI_BIAS_DROP_RES
-  A  = LN1(S1)                                mmu_layernorm_fwd
+  S1 = X32 + dropout(O Wo^T + bo)             mmu_gemm  EPI_BIAS_DROP_RES, f32 residual + f32 out
+  A, A32 = LN1(S1)                            mmu_layernorm_fwd_f32 (bf16 operand + f32 residual)
   H  = gelu(A W1^T + b1)                      mmu_gemm  EPI_BIAS_GELU (saves Z = gelu'(.), bf16)
-  S2 = A + dropout(H W2^T + b2)               mmu_gemm  EPI_BIAS_DROP_RES
-  Y  = LN2(S2)                                mmu_layernorm_fwd
-Backward mirrors it; weight gradients are written straight into the flat f32
+  S2 = A32 + dropout(H W2^T + b2)             mmu_gemm  EPI_BIAS_DROP_RES, f32
+  Y, Y32 = LN2(S2)                            mmu_layernorm_fwd_f32
+The hidden state travels as a PAIR: bf16 X (the next GEMM's operand) and f32 X32 (the
+residual).  The residual adds and LN inputs stay f32, as in the reference's fp32 layer:
+with the stream rounded to bf16 at each of the 48 LN / residual points of 12 layers the
+logits drift by up to 1.6 % of their scale (CPU emulation of the rounding points,
+DESIGN.md §4), with it f32 by 0.5 %.
+Backward mirrors it (the gradient stream is bf16); weight gradients are written straight into the flat f32
 gradient buffer (src/params.py) and skipped when the layer is frozen
 (src/framework.py:284-285 toggles requires_grad).
 """
@@ -61,34 +66,39 @@ class LayerWeights:
         return self.anchor.requires_grad
 
 
-def layer_forward(lw, X, keymask, B, L, p_attn, p_hid, seeds, save):
+def layer_forward(lw, X, X32, keymask, B, L, p_attn, p_hid, seeds, save):
+    """(X bf16, X32 f32) [M, 768] -> (Y bf16, Y32 f32, saved)"""
     M = B * L
     dev = X.device
+    f32 = torch.float32
     qkv = torch.empty(M, 3 * HID, dtype=bf16, device=dev)
     K.gemm(X, HID, True, lw.wqkv16, HID, True, qkv, 3 * HID, M, 3 * HID, HID, epi=K.epilogue(K.EPI_STORE, bias=lw.bqkv))
     O = torch.empty(M, HID, dtype=bf16, device=dev)
     lse = torch.empty(B * HEADS, L, dtype=torch.float32, device=dev)
     dmask = K.dropmask_empty(B, L, HEADS, dev) if (save and p_attn > 0) else None
     K.attention_fwd(qkv, keymask, O, lse, B, L, HEADS, p_attn, seeds[0], dmask)
-    S1 = torch.empty(M, HID, dtype=bf16, device=dev)
+    S1 = torch.empty(M, HID, dtype=f32, device=dev)
     K.gemm(O, HID, True, lw.wo16, HID, True, S1, HID, M, HID, HID,
-           epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw.bo, residual=X, drop_p=p_hid, seed=seeds[1]))
+           epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw.bo, residual=X32, drop_p=p_hid, seed=seeds[1]))
     A = torch.empty(M, HID, dtype=bf16, device=dev)
-    mean1 = torch.empty(M, dtype=torch.float32, device=dev)
-    rstd1 = torch.empty(M, dtype=torch.float32, device=dev)
-    K.layernorm_fwd(S1, lw.ln1w, lw.ln1b, A, mean1, rstd1)
+    A32 = torch.empty(M, HID, dtype=f32, device=dev)
+    mean1 = torch.empty(M, dtype=f32, device=dev)
+    rstd1 = torch.empty(M, dtype=f32, device=dev)
+    K.layernorm_fwd_f32(S1, lw.ln1w, lw.ln1b, A, A32, mean1, rstd1)
     Z = torch.empty(M, FFN, dtype=bf16, device=dev) if save else None  # gelu'(A W1^T + b1), for the backward
     Hh = torch.empty(M, FFN, dtype=bf16, device=dev)
     K.gemm(A, HID, True, lw.w116, HID, True, Hh, FFN, M, FFN, HID, epi=K.epilogue(K.EPI_BIAS_GELU, bias=lw.b1, aux=Z))
-    S2 = torch.empty(M, HID, dtype=bf16, device=dev)
+    S2 = torch.empty(M, HID, dtype=f32, device=dev)
     K.gemm(Hh, FFN, True, lw.w216, FFN, True, S2, HID, M, HID, FFN,
-           epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw.b2, residual=A, drop_p=p_hid, seed=seeds[2]))
+           epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw.b2, residual=A32, drop_p=p_hid, seed=seeds[2]))
+    del A32
     Y = torch.empty(M, HID, dtype=bf16, device=dev)
-    mean2 = torch.empty(M, dtype=torch.float32, device=dev)
-    rstd2 = torch.empty(M, dtype=torch.float32, device=dev)
-    K.layernorm_fwd(S2, lw.ln2w, lw.ln2b, Y, mean2, rstd2)
+    Y32 = torch.empty(M, HID, dtype=f32, device=dev)
+    mean2 = torch.empty(M, dtype=f32, device=dev)
+    rstd2 = torch.empty(M, dtype=f32, device=dev)
+    K.layernorm_fwd_f32(S2, lw.ln2w, lw.ln2b, Y, Y32, mean2, rstd2)
     saved = (X, qkv, O, lse, dmask, S1, mean1, rstd1, A, Z, Hh, S2, mean2, rstd2) if save else None
-    return Y, saved
+    return Y, Y32, saved
 
 
 def _reduce(part, out):
@@ -212,23 +222,31 @@ def _mark():
 
 
 class BertLayerFunction(torch.autograd.Function):
-    """One fused BertLayer; X [B*L, 768] bf16 -> Y.  ``anchor`` (the layer's query
-    weight) only makes autograd run backward when the layer is trainable."""
+    """One fused BertLayer; (X bf16, X32 f32) [B*L, 768] -> (Y, Y32).  The layer's whole
+    input gradient is returned for X (X and X32 hold the same values; X32 gets None);
+    the output gradient arrives on Y from the next layer or on Y32 from the pooler.
+    ``anchor`` (the layer's query weight) only makes autograd run backward when the layer
+    is trainable."""
 
     @staticmethod
-    def forward(ctx, X, anchor, lw, keymask, B, L, p_attn, p_hid, seeds, on_grads_ready):
+    def forward(ctx, X, X32, anchor, lw, keymask, B, L, p_attn, p_hid, seeds, on_grads_ready):
+        ctx.set_materialize_grads(False)
         e0 = _mark()
-        Y, saved = layer_forward(lw, X, keymask, B, L, p_attn, p_hid, seeds, save=True)
+        Y, Y32, saved = layer_forward(lw, X, X32, keymask, B, L, p_attn, p_hid, seeds, save=True)
         if e0 is not None:
             _block_events.append((e0, _mark()))
         ctx.saved_bufs = saved
         ctx.meta = (lw, keymask, B, L, p_attn, p_hid, seeds, on_grads_ready)
-        return Y
+        return Y, Y32
 
     @staticmethod
-    def backward(ctx, dY):
+    def backward(ctx, dY, dY32):
         lw, keymask, B, L, p_attn, p_hid, seeds, hook = ctx.meta
         wgrad = lw.trainable()
+        if dY32 is not None:
+            dY = dY32.to(bf16) if dY is None else dY + dY32.to(bf16)
+        if dY is None:
+            return (None,) * 11
         e0 = _mark()
         dX, side = layer_backward(lw, ctx.saved_bufs, dY.contiguous(), keymask, B, L, p_attn, p_hid, seeds, wgrad)
         if e0 is not None:
@@ -241,7 +259,7 @@ class BertLayerFunction(torch.autograd.Function):
             _join_side_at_end(side)
         elif wgrad and hook is not None:
             hook(lw)
-        return dX, None, None, None, None, None, None, None, None, None
+        return dX, None, None, None, None, None, None, None, None, None, None
 
 
 _pending_join = set()

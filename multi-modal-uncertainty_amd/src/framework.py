@@ -60,6 +60,48 @@ def _all_ranks_any(flag, device=None):
     return bool(t.item())
 
 
+class ShardSampler(torch.utils.data.Sampler):
+    """Evaluation shard of one data-parallel rank: samples rank, rank + world, ... in order
+    (no padding, so every sample is evaluated exactly once over the ranks)."""
+
+    def __init__(self, data_source, world, rank):
+        self.n, self.world, self.rank = len(data_source), world, rank
+
+    def __iter__(self):
+        return iter(range(self.rank, self.n, self.world))
+
+    def __len__(self):
+        return len(range(self.rank, self.n, self.world))
+
+
+def shard_eval_loader(loader, world, rank):
+    """The same evaluation loader over this rank's ShardSampler (DevicePrefetcher kept)."""
+    inner = getattr(loader, "loader", loader)
+    dl = torch.utils.data.DataLoader(inner.dataset, batch_size=inner.batch_size, shuffle=False,
+                                     sampler=ShardSampler(inner.dataset, world, rank), num_workers=inner.num_workers,
+                                     collate_fn=inner.collate_fn, pin_memory=inner.pin_memory)
+    if inner is not loader:
+        return type(loader)(dl, loader.device, loader.mean, loader.std, loader.dtype)
+    return dl
+
+
+def _combine_over_ranks(it, preds, labels, want_preds):
+    """Sample-weighted loss / metric sums (and, for AUC, predictions) of the ranks' eval
+    shards combined: the values a single process evaluating the whole split reports."""
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([it.losses_sum, it.sizes_sum] + list(it.metrics_sum), dtype=torch.float64, device=dev)
+    dist.all_reduce(t)
+    t = t.cpu().numpy()
+    it.losses_sum, it.sizes_sum, it.metrics_sum = float(t[0]), float(t[1]), t[2:]
+    if want_preds:
+        parts = [None] * dist.get_world_size()
+        dist.all_gather_object(parts, (preds, labels))
+        preds = np.concatenate([p for p, _ in parts])
+        labels = np.concatenate([lb for _, lb in parts])
+    return preds, labels
+
+
 def _get_step_iterator(steps, generator):
     if steps is None:
         return zip(itertools.count(1), generator)
@@ -121,6 +163,7 @@ class Model_:
         self.device = None
         self.verbose = verbose
         self.verbose_logs = {}
+        self.shard_eval = False  # data parallel: eval loaders hold per-rank shards (train.py), combined here
 
     # ------------------------------------------------------------------ helpers
     def _metric_tensors(self, pred_y, y, eval, dummy_dim):
@@ -186,6 +229,8 @@ class Model_:
                 labels.append(y)
         preds = torch.cat(preds, dim=0).cpu().numpy()
         labels = torch.cat(labels, dim=0).cpu().numpy()
+        if self.shard_eval:  # data parallel: each rank evaluated its ShardSampler slice
+            preds, labels = _combine_over_ranks(it, preds, labels, auc)
         out = {f"{phase}_loss": it.loss}
         out.update({f"{phase}_{k}": v for k, v in it.extra_lists.items()})
         out.update({f"{phase}_{k}": v for k, v in it.metrics.items()})

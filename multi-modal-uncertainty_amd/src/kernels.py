@@ -78,8 +78,7 @@ def gemm(A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, M, N_, K, epi=None, batch=1
     cdt = N.MMU_F32 if C.dtype == torch.float32 else N.MMU_BF16
     if C.dtype not in (torch.float32, torch.bfloat16):
         raise N.NativeError("gemm C must be f32 or bf16")
-    # the per-stream f32 scratch serves split-K weight gradients and the split-K tail of
-    # every big-tile product (mmu_gemm: the partial last wave of 256x256 tiles)
+    # the per-stream f32 scratch serves the split-K weight gradients
     if epi is None:
         epi = epilogue(EPI_STORE)
     if not epi.workspace:  # (on a copy: a caller's epilogue may be reused on another stream)
@@ -179,14 +178,27 @@ def layernorm_fwd(X, w, b, Y, mean, rstd, eps=1e-12, group_rows=0, param_stride=
            int(group_rows), int(param_stride), _stream(X))
 
 
+def layernorm_fwd_f32(X, w, b, Y, Y32=None, mean=None, rstd=None, eps=1e-12, group_rows=0, param_stride=0):
+    """LN of the f32 hidden stream: X f32 -> Y bf16 (GEMM operand) [+ Y32 f32 (next residual)]."""
+    _dev_check(X, w, b, Y)
+    _want(X, torch.float32, "layernorm_fwd_f32 X")
+    _want(Y, torch.bfloat16, "layernorm_fwd_f32 Y")
+    if Y32 is not None:
+        _want(Y32, torch.float32, "layernorm_fwd_f32 Y32")
+    rows, H = X.shape
+    N.call("mmu_layernorm_fwd_f32", _ptr(X), _ptr(w), _ptr(b), _ptr(Y), _ptr(Y32), _ptr(mean), _ptr(rstd), rows, H,
+           float(eps), int(group_rows), int(param_stride), _stream(X))
+
+
 LN_ROWS_PER_PART = 64
 
 
 def layernorm_bwd(dY, X, mean, rstd, w, dX, dXdrop=None, drop_p=0.0, seed=0, part_dw=None, part_db=None,
                   part_dbias=None):
+    """X: the forward's LN input, bf16 or f32 (the f32 hidden stream: mmu_layernorm_bwd_f32)."""
     _dev_check(dY, X, mean, rstd, w, dX)
     rows, H = X.shape
-    N.call("mmu_layernorm_bwd", _ptr(dY), _ptr(X), _ptr(mean), _ptr(rstd), _ptr(w), _ptr(dX), _ptr(dXdrop),
+    N.call("mmu_layernorm_bwd_f32" if X.dtype == torch.float32 else "mmu_layernorm_bwd", _ptr(dY), _ptr(X), _ptr(mean), _ptr(rstd), _ptr(w), _ptr(dX), _ptr(dXdrop),
            float(drop_p), int(seed), _ptr(part_dw), _ptr(part_db), _ptr(part_dbias), rows, H, LN_ROWS_PER_PART,
            _stream(X))
 
@@ -224,11 +236,16 @@ def ln_parts(rows):
 
 
 def embed_fwd(ids, seg, txt_mask, proj, word, pos, typ, ln_w, ln_b, eps, cls_id, sep_id, idx, V, B, T, n_img, Lout,
-              X, keymask, mean=None, rstd=None, drop_txt=0.0, drop_img=0.0, seed=0):
+              X, keymask, mean=None, rstd=None, drop_txt=0.0, drop_img=0.0, seed=0, X32=None):
+    """X32 (optional, f32 like X): the same rows in f32, the encoder's f32 hidden stream."""
     _dev_check(proj, word, pos, typ, ln_w, ln_b, X, keymask)
+    if X32 is not None:
+        _want(X32, torch.float32, "embed_fwd X32")
+        _dev_check(X32)
     N.call("mmu_embed_fwd", _ptr(ids), _ptr(seg), _ptr(txt_mask), _ptr(proj), _ptr(word), _ptr(pos), _ptr(typ),
            _ptr(ln_w), _ptr(ln_b), float(eps), int(cls_id), int(sep_id), _ptr(idx), V, B, T, n_img, Lout, 768,
-           float(drop_txt), float(drop_img), int(seed), _ptr(X), _ptr(keymask), _ptr(mean), _ptr(rstd), _stream(X))
+           float(drop_txt), float(drop_img), int(seed), _ptr(X), _ptr(X32), _ptr(keymask), _ptr(mean), _ptr(rstd),
+           _stream(X))
 
 
 def embed_bwd(dX, ids, seg, proj, word, pos, typ, ln_w, mean, rstd, cls_id, sep_id, B, T, n_img, d_word, d_pos,
@@ -454,8 +471,8 @@ def _count_alg(M, N_, K, batch, c_bytes, epi):
     if epi is not None:
         if epi.accumulate:
             b += c_bytes * M * N_
-        if epi.residual:
-            b += 2.0 * M * N_
+        if epi.residual:  # f32 residual with an f32 BIAS_DROP_RES output (the hidden stream)
+            b += (4.0 if (c_bytes == 4 and epi.kind == EPI_BIAS_DROP_RES) else 2.0) * M * N_
         if epi.aux:
             b += 2.0 * M * N_
     _alg["bytes"] += b * batch

@@ -195,20 +195,23 @@ class EmbedFunction(torch.autograd.Function):
         L = n + 2 + T
         dev = proj.device
         X = torch.empty(B * L, 768, dtype=torch.bfloat16, device=dev)
+        X32 = torch.empty(B * L, 768, dtype=torch.float32, device=dev)
         km = torch.empty(B, L, dtype=torch.float32, device=dev)
         mean = torch.empty(B * L, dtype=torch.float32, device=dev)
         rstd = torch.empty(B * L, dtype=torch.float32, device=dev)
         e = enc.txt_embeddings
         K.embed_fwd(ids, seg, txt_mask, proj, e.word_embeddings.weight, e.position_embeddings.weight,
                     e.token_type_embeddings.weight, e.LayerNorm.weight, e.LayerNorm.bias, LN_EPS, enc.cls_id,
-                    enc.sep_id, None, 1, B, T, n, L, X, km, mean, rstd, drop_txt, drop_img, seed)
+                    enc.sep_id, None, 1, B, T, n, L, X, km, mean, rstd, drop_txt, drop_img, seed, X32=X32)
         ctx.save_for_backward(proj, ids, seg, mean, rstd)
         ctx.meta = (enc, B, T, n, drop_txt, drop_img, seed)
-        ctx.mark_non_differentiable(km)
-        return X, km
+        # the gradient of the encoder input arrives on the bf16 X (BertLayerFunction returns
+        # the whole input gradient there); X32 is the same values in f32
+        ctx.mark_non_differentiable(X32, km)
+        return X, X32, km
 
     @staticmethod
-    def backward(ctx, dX, _dkm):
+    def backward(ctx, dX, _dX32, _dkm):
         proj, ids, seg, mean, rstd = ctx.saved_tensors
         enc, B, T, n, drop_txt, drop_img, seed = ctx.meta
         e = enc.txt_embeddings
@@ -223,6 +226,35 @@ class EmbedFunction(torch.autograd.Function):
         if enc._grad_ready_hook is not None:
             enc._grad_ready_hook("embeddings")
         return d_proj, None, None, None, None, None, None, None, None
+
+
+class ProjectFunction(torch.autograd.Function):
+    """img_embeddings Linear(2048 -> 768) on the pooled features (reference src/mmbt.py:61,70).
+    Its backward accumulates dW / db straight into the flat gradient store and only then
+    reports the "proj" gradient segment done (src/dp.py), so the segment's all-reduce is
+    ordered after the accumulation on the compute stream (an AccumulateGrad node of
+    autograd's own would run at an unspecified point after the embedding hook)."""
+
+    @staticmethod
+    def forward(ctx, feats, weight, bias, enc):
+        ctx.save_for_backward(feats, weight)
+        ctx.enc = enc
+        return F.linear(feats, weight, bias)
+
+    @staticmethod
+    def backward(ctx, d):
+        feats, weight = ctx.saved_tensors
+        enc = ctx.enc
+        d2 = d.reshape(-1, d.shape[-1]).float()
+        dfeats = (d2 @ weight).view(feats.shape) if ctx.needs_input_grad[0] else None
+        st, pre = enc._store, enc._prefix + "img_embeddings.img_embeddings."
+        if ctx.needs_input_grad[1]:
+            st.grad_of(pre + "weight").addmm_(d2.t(), feats.reshape(-1, feats.shape[-1]))
+        if ctx.needs_input_grad[2]:
+            st.grad_of(pre + "bias").add_(d2.sum(0))
+        if enc._grad_ready_hook is not None:
+            enc._grad_ready_hook("proj")
+        return dfeats, None, None, None
 
 
 # ----------------------------------------------------------------------------- image side
@@ -270,7 +302,11 @@ class ImageBertEmbeddings(nn.Module):
         self._owner = None
 
     def project(self, feats):
-        return F.linear(feats.float(), self.img_embeddings.weight, self.img_embeddings.bias)
+        w, b = self.img_embeddings.weight, self.img_embeddings.bias
+        if torch.is_grad_enabled() and self._owner is not None and self._owner._store is not None and (
+                feats.requires_grad or w.requires_grad or b.requires_grad):
+            return ProjectFunction.apply(feats.float(), w, b, self._owner)
+        return F.linear(feats.float(), w, b)
 
     def forward(self, input_imgs, token_type_ids=None):
         """[B,N,2048] -> [B,N+2,768] (reference forward, src/mmbt.py:58-83)."""
@@ -382,20 +418,24 @@ class MultimodalBertEncoder(nn.Module):
         seed = _seed() if (drop_txt > 0 or drop_img > 0) else 0
         txt, segment, txt_mask = (t.contiguous().long() for t in (txt, segment, txt_mask))
         if idx is None and torch.is_grad_enabled():
-            X, km = EmbedFunction.apply(proj, self.txt_embeddings.word_embeddings.weight, self, txt, segment,
-                                        txt_mask, drop_txt, drop_img, seed)
-            return X, km, self.n_img + 2 + T
+            X, X32, km = EmbedFunction.apply(proj, self.txt_embeddings.word_embeddings.weight, self, txt, segment,
+                                             txt_mask, drop_txt, drop_img, seed)
+            return (X, X32), km, self.n_img + 2 + T
         L = self.n_img + 2 + T if idx is None else Lout
         X = torch.empty(V * B * L, 768, dtype=torch.bfloat16, device=dev)
+        X32 = torch.empty(V * B * L, 768, dtype=torch.float32, device=dev)
         km = torch.empty(V * B, L, dtype=torch.float32, device=dev)
         e = self.txt_embeddings
         K.embed_fwd(txt, segment, txt_mask, proj.contiguous(), e.word_embeddings.weight, e.position_embeddings.weight,
                     e.token_type_embeddings.weight, e.LayerNorm.weight, e.LayerNorm.bias, LN_EPS, self.cls_id,
-                    self.sep_id, idx, V, B, T, self.n_img, L, X, km, drop_txt=drop_txt, drop_img=drop_img, seed=seed)
-        return X, km, L
+                    self.sep_id, idx, V, B, T, self.n_img, L, X, km, drop_txt=drop_txt, drop_img=drop_img, seed=seed,
+                    X32=X32)
+        return (X, X32), km, L
 
-    def _encode(self, X, km, nb, L):
-        """X [nb*L, 768] bf16, km [nb, L] -> last hidden [nb*L, 768] bf16."""
+    def _encode(self, XX, km, nb, L):
+        """(X bf16, X32 f32) [nb*L, 768], km [nb, L] -> last hidden [nb*L, 768] f32 (the f32
+        hidden stream; see src/encoder.py)."""
+        X, X32 = XX
         act = self._dropout_active()
         p_attn, p_hid = (self.attn_dropout, self.hidden_dropout) if act else (0.0, 0.0)
         base = _seed() if act and (p_attn > 0 or p_hid > 0) else 0
@@ -403,10 +443,11 @@ class MultimodalBertEncoder(nn.Module):
         for i, lw in enumerate(self._lw):
             seeds = (_mix(base, 3 * i), _mix(base, 3 * i + 1), _mix(base, 3 * i + 2))
             if need_grad:
-                X = BertLayerFunction.apply(X, lw.anchor, lw, km, nb, L, p_attn, p_hid, seeds, self._grad_ready_hook)
+                X, X32 = BertLayerFunction.apply(X, X32, lw.anchor, lw, km, nb, L, p_attn, p_hid, seeds,
+                                                 self._grad_ready_hook)
             else:
-                X, _ = layer_forward(lw, X, km, nb, L, p_attn, p_hid, seeds, save=False)
-        return X
+                X, X32, _ = layer_forward(lw, X, X32, km, nb, L, p_attn, p_hid, seeds, save=False)
+        return X32
 
     def _pool(self, X, nb, L):
         return self.pooler(X.view(nb, L, 768))
@@ -454,6 +495,7 @@ class MultimodalBertEncoder(nn.Module):
         B, L, H = hidden.shape
         km = ext_mask.reshape(B, L).float().contiguous()
         X = hidden.reshape(B * L, H).to(torch.bfloat16).contiguous()
+        X32 = hidden.reshape(B * L, H).detach().float().contiguous()
         act = self._dropout_active()
         p_attn, p_hid = (self.attn_dropout, self.hidden_dropout) if act else (0.0, 0.0)
         base = _seed() if act else 0
@@ -461,19 +503,19 @@ class MultimodalBertEncoder(nn.Module):
         for i, lw in enumerate(self._lw):
             seeds = (_mix(base, 3 * i), _mix(base, 3 * i + 1), _mix(base, 3 * i + 2))
             if torch.is_grad_enabled():
-                X = BertLayerFunction.apply(X, lw.anchor, lw, km, B, L, p_attn, p_hid, seeds, None)
+                X, X32 = BertLayerFunction.apply(X, X32, lw.anchor, lw, km, B, L, p_attn, p_hid, seeds, None)
             else:
-                X, _ = layer_forward(lw, X, km, B, L, p_attn, p_hid, seeds, save=False)
-            outs.append(X.view(B, L, H))
+                X, X32, _ = layer_forward(lw, X, X32, km, B, L, p_attn, p_hid, seeds, save=False)
+            outs.append(X32.view(B, L, H))
         return outs if all_layers else outs[-1:]
 
     def _image_embeddings(self, proj):
         self._prepare()
         B = proj.shape[0]
         dummy = torch.zeros(B, 0, dtype=torch.long, device=proj.device)
-        X, _, L = self._embed(dummy, dummy, dummy, proj, idx=torch.arange(self.n_img + 2, device=proj.device),
-                              Lout=self.n_img + 2)
-        return X.view(B, L, 768).float()
+        (_, X32), _, L = self._embed(dummy, dummy, dummy, proj, idx=torch.arange(self.n_img + 2, device=proj.device),
+                                     Lout=self.n_img + 2)
+        return X32.view(B, L, 768)
 
     def _text_embeddings(self, ids, token_type_ids=None):
         self._prepare()
@@ -481,8 +523,8 @@ class MultimodalBertEncoder(nn.Module):
         seg = torch.zeros_like(ids) if token_type_ids is None else token_type_ids
         proj = torch.zeros(B, self.n_img, 768, device=ids.device)
         idx = torch.arange(T, device=ids.device) + self.n_img + 2
-        X, _, L = self._embed(ids, torch.ones_like(ids), seg, proj, idx=idx, Lout=T)
-        return X.view(B, T, 768).float()
+        (_, X32), _, L = self._embed(ids, torch.ones_like(ids), seg, proj, idx=idx, Lout=T)
+        return X32.view(B, T, 768)
 
 
 def control_indices(total_embeds, num_embeds):

@@ -75,9 +75,14 @@ class ParamStore:
         for n in self.compute_names:
             self.coffsets[n] = off
             off += self.params[n].numel()
-        self._tcopies, self._tjobs = {}, None  # re-allocated on the (new) device
+        # transposed and flipped copies are re-allocated on the (new) device: a job table
+        # holding the old buffers' pointers would write through a foreign-device pointer
+        self._tcopies, self._tjobs = {}, None
         for key, shape in self._tspecs.items():
             self._alloc_transposed(key, shape)
+        for name in list(self._fcopies):
+            O, I = self.params[name].shape[:2]
+            self._fcopies[name] = torch.empty(I, 3, 3, O, dtype=torch.bfloat16, device=device)
         self.sync_compute()
 
     @property

@@ -81,7 +81,10 @@ class BatchNorm2d(nn.BatchNorm2d):
                 skip = skip.contiguous(memory_format=torch.channels_last)
             if self.training and self.track_running_stats:
                 return _BatchNormAct.apply(x, self.weight, self.bias, skip, self, relu, skip_sink)
-            if not self.training:
+            if not self.training and not (torch.is_grad_enabled() and (
+                    x.requires_grad or self.weight.requires_grad or (skip is not None and skip.requires_grad))):
+                # the one-pass running-statistics kernel has no backward: a graph through an
+                # eval-mode BN (frozen statistics during training) takes the torch path below
                 Y = torch.empty_like(x)
                 K.batchnorm_fwd(x, Y, self.weight, self.bias, self.running_mean, self.running_var, False,
                                 self.momentum, self.eps, relu=relu, skip=skip)

@@ -47,31 +47,38 @@ class EnsembleMMBT:
         self.clf_b = torch.stack([m.clf.bias.detach() for m in self.members])
         self.hidden_dropout, self.attn_dropout = enc0.hidden_dropout, enc0.attn_dropout
 
-    def _layer(self, lw, X, km, nb, L, p_attn, p_hid, seeds):
+    def _layer(self, lw, X, X32, km, nb, L, p_attn, p_hid, seeds):
+        """(X bf16, X32 f32) [K*M, 768] -> (Y, Y32): src/encoder.py layer_forward batched over
+        the members (the same f32 hidden stream)."""
         Km, M = self.K, nb * L
         dev = X.device
+        f32 = torch.float32
         qkv = torch.empty(Km * M, 3 * HID, dtype=bf16, device=dev)
         K.gemm(X, HID, True, lw["wqkv16"], HID, True, qkv, 3 * HID, M, 3 * HID, HID, batch=Km, sA=M * HID,
                sB=3 * HID * HID, sC=M * 3 * HID, epi=K.epilogue(K.EPI_STORE, bias=lw["bqkv"], bias_bstride=3 * HID))
         O = torch.empty(Km * M, HID, dtype=bf16, device=dev)
         lse = torch.empty(Km * nb * 12, L, dtype=torch.float32, device=dev)
         K.attention_fwd(qkv, km, O, lse, Km * nb, L, 12, p_attn, seeds[0])
-        S1 = torch.empty_like(O)
+        S1 = torch.empty(Km * M, HID, dtype=f32, device=dev)
         K.gemm(O, HID, True, lw["wo16"], HID, True, S1, HID, M, HID, HID, batch=Km, sA=M * HID, sB=HID * HID,
-               sC=M * HID, epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw["bo"], bias_bstride=HID, residual=X,
+               sC=M * HID, epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw["bo"], bias_bstride=HID, residual=X32,
                                           res_bstride=M * HID, drop_p=p_hid, seed=seeds[1]))
         A = torch.empty_like(O)
-        K.layernorm_fwd(S1, lw["ln1w"], lw["ln1b"], A, None, None, LN_EPS, group_rows=M, param_stride=HID)
+        A32 = torch.empty_like(S1)
+        K.layernorm_fwd_f32(S1, lw["ln1w"], lw["ln1b"], A, A32, eps=LN_EPS, group_rows=M, param_stride=HID)
+        del S1
         Hh = torch.empty(Km * M, FFN, dtype=bf16, device=dev)
         K.gemm(A, HID, True, lw["w116"], HID, True, Hh, FFN, M, FFN, HID, batch=Km, sA=M * HID, sB=FFN * HID,
                sC=M * FFN, epi=K.epilogue(K.EPI_BIAS_GELU, bias=lw["b1"], bias_bstride=FFN))
-        S2 = torch.empty_like(O)
+        S2 = torch.empty(Km * M, HID, dtype=f32, device=dev)
         K.gemm(Hh, FFN, True, lw["w216"], FFN, True, S2, HID, M, HID, FFN, batch=Km, sA=M * FFN, sB=HID * FFN,
-               sC=M * HID, epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw["b2"], bias_bstride=HID, residual=A,
+               sC=M * HID, epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw["b2"], bias_bstride=HID, residual=A32,
                                           res_bstride=M * HID, drop_p=p_hid, seed=seeds[2]))
+        del A32
         Y = torch.empty_like(O)
-        K.layernorm_fwd(S2, lw["ln2w"], lw["ln2b"], Y, None, None, LN_EPS, group_rows=M, param_stride=HID)
-        return Y
+        Y32 = torch.empty_like(S2)
+        K.layernorm_fwd_f32(S2, lw["ln2w"], lw["ln2b"], Y, Y32, eps=LN_EPS, group_rows=M, param_stride=HID)
+        return Y, Y32
 
     @torch.no_grad()
     def logits(self, txt, mask, segment, img, mc_samples=1, mc_dropout=None):
@@ -85,6 +92,7 @@ class EnsembleMMBT:
         M = nb * S
         dev = img.device
         X = torch.empty(self.K * M, HID, dtype=bf16, device=dev)
+        X32 = torch.empty(self.K * M, HID, dtype=torch.float32, device=dev)
         km = torch.empty(self.K * nb, S, dtype=torch.float32, device=dev)
         p_txt = self.hidden_dropout if mc else 0.0
         idx = torch.arange(S, device=dev).repeat(T_mc, 1)  # T_mc copies of the identity gather
@@ -96,13 +104,13 @@ class EnsembleMMBT:
             K.embed_fwd(txt, segment, mask, proj, et.word_embeddings.weight, et.position_embeddings.weight,
                         et.token_type_embeddings.weight, et.LayerNorm.weight, et.LayerNorm.bias, LN_EPS, e.cls_id,
                         e.sep_id, idx, T_mc, B, Tt, e.n_img, S, X[k * M:(k + 1) * M], km[k * nb:(k + 1) * nb],
-                        drop_txt=p_txt, drop_img=0.0, seed=_seed() if mc else 0)
+                        drop_txt=p_txt, drop_img=0.0, seed=_seed() if mc else 0, X32=X32[k * M:(k + 1) * M])
         p_attn, p_hid = (self.attn_dropout, self.hidden_dropout) if mc else (0.0, 0.0)
         base = _seed() if mc else 0
         for i, lw in enumerate(self.layers):
-            X = self._layer(lw, X, km, nb, S, p_attn, p_hid, (_mix(base, 3 * i), _mix(base, 3 * i + 1),
-                                                              _mix(base, 3 * i + 2)))
-        h0 = X.view(self.K, nb, S, HID)[:, :, 0].float()                       # [K, nb, 768]
+            X, X32 = self._layer(lw, X, X32, km, nb, S, p_attn, p_hid, (_mix(base, 3 * i), _mix(base, 3 * i + 1),
+                                                                        _mix(base, 3 * i + 2)))
+        h0 = X32.view(self.K, nb, S, HID)[:, :, 0]                             # [K, nb, 768] f32
         pooled = torch.tanh(torch.baddbmm(self.pool_b.unsqueeze(1), h0, self.pool_w.transpose(1, 2)))
         out = torch.baddbmm(self.clf_b.unsqueeze(1), pooled, self.clf_w.transpose(1, 2))
         return out.view(self.K, T_mc, B, -1)

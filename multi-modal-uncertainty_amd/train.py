@@ -7,7 +7,8 @@ Additions (all optional):
   --gin_file F [F ...] / --gin_param 'train.lr=5e-5'   gin-style bindings onto the flags (src/gin.py)
   --synthetic N      train on N seeded synthetic Food-101 samples (no dataset offline)
   data parallel      launch with torch.distributed.run: one rank per GPU, RCCL all-reduce,
-                     train set sharded per rank, val/test evaluated whole on every rank,
+                     train set sharded per rank, val/test sharded per rank (ShardSampler,
+                     loss / metric sums combined over the ranks in Model_.eval_loop),
                      rank 0 writes history / checkpoints.
   --synthetic with --framework flava: seeded FLAVA embeddings (197 image + <= 77 text tokens)
 The ViLT branch (another model family, remote weights) is out of scope and refused.
@@ -25,7 +26,7 @@ import torch.optim as optim  # noqa: E402
 
 from src import dataset  # noqa: E402
 from src import gin  # noqa: E402
-from src.framework import Model_  # noqa: E402
+from src.framework import Model_, shard_eval_loader  # noqa: E402
 from src.training_loop import _construct_default_callbacks  # noqa: E402
 from src.utils import set_seed  # noqa: E402
 
@@ -184,7 +185,7 @@ def food101_data(args, rank=0, world=1):
         return mk(tr, True, sampler), mk(va, False), mk(te, False), 101, _Vocab()
     gpu = bool(args.gpu_normalize) and torch.cuda.is_available()
     # data parallel: every rank draws a disjoint shard of the train split (reshuffled per
-    # epoch by Model_.train_loop); dev / test are evaluated whole on every rank
+    # epoch by Model_.train_loop); dev / test shards are cut in main() (shard_eval_loader)
     sampler = (lambda ds: torch.utils.data.DistributedSampler(ds, world, rank, shuffle=True, seed=args.seed)) \
         if world > 1 else None
     return dataset.get_food101(datapath=args.datapath, batch_size=args.batch_size,
@@ -280,6 +281,9 @@ def main(argv=None):
             _dp_wrap(model, optimizer, args.gradient_accumulation_steps)
         else:
             _dp_wrap_flat(model, optimizer)
+        # evaluation sharded over the ranks, sample-weighted sums combined in eval_loop
+        valid, test = (shard_eval_loader(dl, world, rank) for dl in (valid, test))
+        m.shard_eval = True
     m.train_loop(train, valid_generator=valid, test_generator=test, steps_per_epoch=len(train),
                  validation_steps=len(valid), test_steps=len(test), epochs=args.n_epochs, callbacks=callbacks,
                  patience=args.patience, epoch_start=epoch_start, scheduler_step_on=args.scheduler_step_on,

@@ -14,6 +14,8 @@ Run:  python -m oracle.gen_golden          (needs /root/reference; CPU only)
   oracle/flava_ref.make_state_dict (strict), synthetic embeddings (seeded):
   eval logits + losses, a train-mode loss (dropout 0) with per-tensor grad norms,
   and the MIMO permutations of data_forming_func_transformer (src/dataset.py:30-54).
+* robustness fixtures (A11): the eval_mmbt_robustness.py:77-93 per-batch loop over the
+  reference model, [B, 3 + 2n, C] with the drawn control index sets.
 * framework fixture: the reference ``Model_.train_loop`` (src/framework.py:213)
   with ``_construct_default_callbacks`` (src/training_loop.py:23-47) driving
   oracle/tiny_model.TinyMMBT for 2 epochs x 3 steps; history + checkpoint keys.
@@ -141,6 +143,52 @@ def gen_mmbt(tag, cfg, B, T, lens, seed=0, wseed=0):
     print(f"wrote mmbt_{tag}: loss_eval={out['loss_eval']:.6f} loss_train={out['loss_train']:.6f}")
 
 
+def gen_robustness(tag, cfg, B, T, lens, n_repeats, seed=0, wseed=0, rng_seed=2024):
+    """A11: the per-batch loop of eval_mmbt_robustness.py:77-93 on the reference's own
+    MultimodalBertClf (eval mode): full, image-only, text-only, then n_repeats image-control
+    and n_repeats text-control forwards, stacked along dim 1 -> [B, 3 + 2n, C].  The control
+    index sets come from the global torch RNG (src/mmbt.py:199), seeded once before the
+    batch; the drawn index sets are recorded too."""
+    from oracle.weights import make_state_dict, checksum
+    mmbt, _, _ = _import_reference(cfg, 0.0)
+    torch.manual_seed(1234)
+    model = mmbt.MultimodalBertClf(_args(cfg))
+    sd = make_state_dict(wseed, cfg)
+    model.load_state_dict(sd, strict=True)
+    x, y = make_inputs(cfg, B, T, lens, seed)
+    model.eval()
+    real_randperm = torch.randperm
+    drawn = []
+
+    def rp(n, *a, **k):
+        r = real_randperm(n, *a, **k)
+        drawn.append(r.clone())
+        return r
+    torch.randperm = rp
+    try:
+        torch.manual_seed(rng_seed)
+        with torch.no_grad():
+            outputs = [model(*x), model.forward_img_only(*x), model.forward_txt_only(*x)]
+            for modal in ("image", "text"):
+                for _ in range(n_repeats):
+                    outputs.append(model.forward_control(*x, modal))
+    finally:
+        torch.randperm = real_randperm
+    stack = torch.stack(outputs, dim=1)
+    idx = []
+    for j, r in enumerate(drawn):
+        n = cfg.num_image_embeds + 1 if j < n_repeats else T
+        idx.append(np.concatenate([[0], np.sort(r[:n].numpy() + 1)]))
+    out = {"text": x[0].numpy(), "segment": x[1].numpy(), "mask": x[2].numpy(), "y": y.numpy(),
+           "img_sum": np.float64(x[3].double().sum()), "weight_checksum": np.float64(checksum(sd)),
+           "seed": np.int64(seed), "wseed": np.int64(wseed), "rng_seed": np.int64(rng_seed),
+           "n_repeats": np.int64(n_repeats), "preds": stack.numpy(),
+           "indices_image": np.stack(idx[:n_repeats]), "indices_text": np.stack(idx[n_repeats:])}
+    os.makedirs(OUT, exist_ok=True)
+    np.savez_compressed(os.path.join(OUT, f"robustness_{tag}.npz"), **out)
+    print(f"wrote robustness_{tag}: preds {tuple(stack.shape)}")
+
+
 def _reference_function(relpath, name):
     """One top-level function of a reference module whose other imports are absent here
     (src/dataset.py needs torchvision transforms, a tokenizer, ViltProcessor): the
@@ -249,14 +297,15 @@ def gen_framework():
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("--what", default="all", choices=["all", "small", "full", "framework", "flava"])
+    ap.add_argument("--what", default="all", choices=["all", "small", "full", "framework", "flava",
+                                                       "robustness"])
     a = ap.parse_args()
     sys.path.insert(0, REPO)
     from oracle.weights import SMALL, FULL
     # each generator imports the reference fresh with its own stub config -> run each in a subprocess
     if a.what == "all":
         import subprocess
-        for w in ("small", "full", "framework", "flava"):
+        for w in ("small", "full", "framework", "flava", "robustness"):
             subprocess.check_call([sys.executable, "-m", "oracle.gen_golden", "--what", w], cwd=REPO)
     elif a.what == "small":
         gen_mmbt("small_t16", SMALL, B=2, T=16, lens=[16, 9], seed=0)
@@ -266,5 +315,8 @@ if __name__ == "__main__":
         from oracle.flava_ref import FlavaConfig
         for tag, (kw, B, Li, Lt, seed) in FLAVA_CASES.items():
             gen_flava(tag, FlavaConfig(**kw), B, Li, Lt, seed)
+    elif a.what == "robustness":
+        gen_robustness("small_t16", SMALL, B=3, T=16, lens=[16, 9, 12], n_repeats=3, seed=5)
+        gen_robustness("full_t508", FULL, B=2, T=508, lens=[508, 301], n_repeats=2, seed=6)
     else:
         gen_framework()

@@ -194,3 +194,22 @@ def control_indices(total_embeds, num_embeds, gen=None):
 
 def cross_entropy(logits, y):
     return F.cross_entropy(logits, y)
+
+
+def robustness(sd, txt, mask, segment, img, cfg=FULL, n_repeats=20, feats=None):
+    """Per-batch loop of eval_mmbt_robustness.py:77-93 (eval mode): full, image-only,
+    text-only, then ``n_repeats`` image-control and ``n_repeats`` text-control forwards
+    (src/mmbt.py:186-234), each control drawing its index set from the global torch RNG
+    in that order; stacked along dim 1 -> [B, 3 + 2n, C].  The trunk output is shared
+    (it is a pure function of the image in eval mode)."""
+    if feats is None:
+        feats = image_encoder(sd, img, cfg)
+    T = txt.shape[1]
+    total = T + cfg.num_image_embeds + 2
+    outs = [forward(sd, txt, mask, segment, img, cfg, v, feats=feats) for v in ("full", "img_only", "txt_only")]
+    for modal in ("image", "text"):
+        n = cfg.num_image_embeds + 1 if modal == "image" else T
+        for _ in range(n_repeats):
+            outs.append(forward(sd, txt, mask, segment, img, cfg, "control",
+                                indices=control_indices(total, n), feats=feats))
+    return torch.stack(outs, dim=1)

@@ -161,6 +161,62 @@ def test_food101_train_shards_are_disjoint_and_reshuffled(tmp_path):
     for r in res:
         assert r[1][0] != r[1][1], "DistributedSampler not reshuffled between epochs"
         assert r[2] == (n // world + 3) // 4  # per-rank batches: the epoch is 1/world as long
-        assert r[3] == n                      # dev evaluated whole on every rank
+        assert r[3] == n                      # the whole dev split (main() cuts the eval shards)
         assert r[4] is True                   # one rank's stop flag stops every rank
         assert r[5] == [0.5] * 4 and r[6] == [2.0] * 4
+
+
+class _Samples(torch.utils.data.Dataset):
+    """Per-sample ((text, segment, mask, img), y) items for a default-collated DataLoader."""
+
+    def __init__(self, n, seed):
+        from oracle.tiny_model import tiny_batches
+        self.items = []
+        for (txt, seg, mask, img), y in tiny_batches(n, bsz=1, seed=seed):
+            self.items.append(((txt[0], seg[0], mask[0], img[0]), y[0]))
+
+    def __len__(self):
+        return len(self.items)
+
+    def __getitem__(self, i):
+        return self.items[i]
+
+
+def _eval_shard_worker(rank, world, port, q, n):
+    """Model_.eval_loop with train.py's DP evaluation: each rank evaluates its ShardSampler
+    slice of the dev split and the sample-weighted loss / metric sums (and, with auc, the
+    predictions) are combined over the ranks."""
+    try:
+        import sys
+        here = os.path.dirname(os.path.abspath(__file__))
+        sys.path[:0] = [os.path.join(os.path.dirname(here), "multi-modal-uncertainty_amd"), os.path.dirname(here)]
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from oracle.tiny_model import TinyMMBT, acc
+        from src.framework import Model_, shard_eval_loader
+        model = TinyMMBT()
+        m = Model_(model=model, optimizer=None, scheduler=None, data_forming_func=lambda x, y, phase="train": (x, y),
+                   metrics=[acc], verbose=False)
+        def collate(items):  # collate_fn order: ((text, segment, mask, img), y)
+            return tuple(torch.stack([it[0][k] for it in items]) for k in range(4)), torch.stack([it[1] for it in items])
+        full = torch.utils.data.DataLoader(_Samples(n, seed=7), batch_size=3, shuffle=False, collate_fn=collate)
+        whole = m.eval_loop(full, "val", mmbt=True)
+        shard = shard_eval_loader(full, world, rank)
+        m.shard_eval = True
+        sharded = m.eval_loop(shard, "val", mmbt=True)
+        q.put((rank, whole, sharded, len(shard.sampler)))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, "ERR", traceback.format_exc()))
+
+
+def test_eval_sharded_over_ranks_equals_whole_split():
+    n, world = 23, 2
+    res = _spawn(_eval_shard_worker, world, n)
+    assert sorted(r[3] for r in res) == [11, 12]  # disjoint shards cover the split once
+    for rank, whole, sharded, _ in res:
+        assert set(whole) == set(sharded) == {"val_loss", "val_acc"}
+        # per-batch f32 means over differently composed batches: equal to f32 rounding
+        assert abs(whole["val_loss"] - sharded["val_loss"]) < 1e-6 * max(1.0, abs(whole["val_loss"]))
+        assert abs(whole["val_acc"] - sharded["val_acc"]) < 1e-6 * 100

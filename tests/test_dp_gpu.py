@@ -1,9 +1,16 @@
 """Two ranks on ONE MI355X over gloo (RCCL needs one GPU per rank; the 8-GPU RCCL run is
-the driver's): a real bf16 training backward of the small MMBT with the gradient
-bucketer (src/dp.py) attached, so its buckets are launched by the hooks that fire inside
-backward -- the BERT layers', the embedding backward's and the ResNet blocks' input-gradient
-hooks -- and the flat gradient after finish() equals the mean of the two ranks' local
-gradients (each rank's own backward without the bucketer, all-gathered)."""
+the driver's).
+
+* A real bf16 training backward of the small MMBT with the gradient bucketer (src/dp.py)
+  attached, so its buckets are launched by the hooks that fire inside backward -- the BERT
+  layers', the embedding backward's, the image projection's and the ResNet blocks'
+  input-gradient hooks -- and the flat gradient after finish() equals the mean of the two
+  ranks' local gradients (each rank's own backward without the bucketer, all-gathered).
+  Run with 4 MiB buckets and with 1-byte buckets (every segment its own bucket, so the
+  text-embedding bucket is issued before the image projection's gradient exists).
+* SURVEY §8(e) parity: one device on the global batch vs two ranks on its halves (BN
+  running statistics, dropout 0): averaged gradients and the parameters after one fused
+  BertAdam step agree (reference single-device semantics, src/framework.py:276-319)."""
 import os
 import socket
 
@@ -23,7 +30,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, bucket_bytes):
     try:
         import sys
         here = os.path.dirname(os.path.abspath(__file__))
@@ -50,7 +57,7 @@ def _worker(rank, world, port, q):
 
         backward()  # local gradient (no bucketer yet)
         local = model.store.grad.clone()
-        bk = GradBucketer(model, bucket_bytes=4 << 20)
+        bk = GradBucketer(model, bucket_bytes=bucket_bytes)
         issued = []
         orig = bk._issue
 
@@ -69,6 +76,11 @@ def _worker(rank, world, port, q):
         want = sum(parts) / world
         err = (got - want).abs().max().item()
         scale = want.abs().max().item()
+        st = model.store
+        o0, n0 = st.span(["enc.img_embeddings.img_embeddings.weight", "enc.img_embeddings.img_embeddings.bias"])
+        perr = (got[o0:o0 + n0] - want[o0:o0 + n0]).abs().max().item()
+        pscale = want[o0:o0 + n0].abs().max().item()
+        assert perr <= 1e-6 * pscale + 1e-9, f"image projection gradient not averaged: {perr:.3e} vs {pscale:.3e}"
         q.put((rank, err, scale, during, len(bk.buckets), n_tail, (local - want).abs().max().item()))
         dist.destroy_process_group()
     except Exception:  # pragma: no cover - reported to the parent
@@ -76,12 +88,28 @@ def _worker(rank, world, port, q):
         q.put((rank, "ERR", traceback.format_exc()))
 
 
-def test_bucketer_hooks_average_real_backward():
+def _spawn(target, world, *extra):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + extra) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    errs = [r for r in res if r[1] == "ERR"]
+    assert not errs, errs[0][2]
+    return res
+
+
+@pytest.mark.parametrize("bucket_bytes", [4 << 20, 1])
+def test_bucketer_hooks_average_real_backward(bucket_bytes):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, bucket_bytes)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
@@ -94,3 +122,77 @@ def test_bucketer_hooks_average_real_backward():
         assert err <= 1e-6 * scale + 1e-9, f"rank {rank}: averaged gradient off by {err:.3e} (scale {scale:.3e})"
         assert during >= 1, "no bucket launched inside backward"
         assert n_tail >= 1, "no embedding / trunk bucket launched inside backward"
+
+
+def _parity_worker(rank, world, port, q):
+    try:
+        import sys
+        here = os.path.dirname(os.path.abspath(__file__))
+        sys.path[:0] = [os.path.join(os.path.dirname(here), "multi-modal-uncertainty_amd"), os.path.dirname(here)]
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.backends.cudnn.deterministic = True
+        from src.dp import GradBucketer, broadcast_parameters
+        from src.mmbt import MultimodalBertClf
+        from src.optim import BertAdam
+        from src.testing import small_args, synthetic_batch
+        from oracle.weights import SMALL
+        dev = "cuda:0"
+        B = 8
+
+        def make():
+            torch.manual_seed(0)
+            m = MultimodalBertClf(small_args(bert_hidden_dropout=0.0, bert_attn_dropout=0.0, dropout=0.0,
+                                             img_precision="fp32")).to(dev)
+            m.eval()  # BN on running statistics (per-sample independent), dropout off
+            named = list(m.named_parameters())
+            nd = ["bias", "LayerNorm.bias", "LayerNorm.weight"]
+            groups = [{"params": [p for n, p in named if not any(k in n for k in nd)], "weight_decay": 0.01},
+                      {"params": [p for n, p in named if any(k in n for k in nd)], "weight_decay": 0.0}]
+            return m, BertAdam(groups, lr=1e-3, warmup=0.1, t_total=10.0)
+
+        x, y = synthetic_batch(B, 16, lens=[16, 9, 12, 16, 5, 16, 11, 14], vocab=SMALL.vocab, seed=31)
+        x, y = tuple(t.to(dev) for t in x), y.to(dev)
+        # single device, global batch (what every rank would see without DP).  Two optimizer
+        # steps: BertAdam's warmup_linear schedule gives the first step lr 0 (step read before
+        # its increment), so the second one moves the parameters
+        m1, o1 = make()
+        for it in range(2):
+            p0 = m1.store.flat.clone()
+            o1.zero_grad()
+            m1.compute_loss(m1(*x), y).backward()
+            g1 = m1.store.grad.clone()
+            o1.step()
+        p1 = m1.store.flat.clone()
+        # two ranks, each on its half, bucketed all-reduce inside backward
+        m2, o2 = make()
+        broadcast_parameters(m2)
+        bk = GradBucketer(m2, bucket_bytes=1 << 20)
+        sl = slice(rank * B // world, (rank + 1) * B // world)
+        for it in range(2):
+            o2.zero_grad()
+            m2.compute_loss(m2(*(t[sl] for t in x)), y[sl]).backward()
+            bk.finish()
+            g2 = m2.store.grad.clone()
+            o2.step()
+        p2 = m2.store.flat.clone()
+        torch.cuda.synchronize()
+        gerr = ((g2 - g1).norm() / g1.norm()).item()
+        perr = ((p2 - p1).norm() / (p1 - p0).norm()).item()
+        q.put((rank, gerr, perr, (p1 - p0).abs().max().item()))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, "ERR", traceback.format_exc()))
+
+
+def test_dp_two_ranks_equal_single_device_global_batch():
+    """grads and post-step params of 2 ranks x (B/2) == 1 device x B.
+    Tolerance: the two sides run the same bf16 kernels on different row counts (the
+    weight-gradient split-K sums and MIOpen's fp32 conv algorithms depend on the batch),
+    so they agree to rounding: relative Frobenius error of the gradient <= 1e-2, and of the
+    parameter change of the BertAdam step <= 2e-2."""
+    for rank, gerr, perr, upd in _spawn(_parity_worker, 2):
+        assert upd > 0, "the optimizer step changed nothing"
+        assert gerr <= 1e-2, f"rank {rank}: averaged gradient vs global-batch gradient {gerr:.3e}"
+        assert perr <= 2e-2, f"rank {rank}: post-step parameters vs single device {perr:.3e}"

@@ -171,10 +171,10 @@ def test_transpose_bf16_strided_flipped_filter(dev):
 
 
 @pytest.mark.parametrize("Kd", [256, 768])
-def test_gemm_split_k_tail(dev, Kd, monkeypatch):
-    """M = 257 tile rows x 3 column tiles = 771 tiles: the partial last wave (3 tiles) runs as a
-    split-K tail + finishing epilogue.  Same results as the unsplit launch (MMU_GEMM_TAIL=0):
-    identical dropout pattern, outputs within one bf16 rounding, same column sums."""
+def test_gemm_partial_last_wave(dev, Kd):
+    """M = 256 * 257 rows x 3 column tiles = 771 tiles (a partial last wave of 3 tiles on 256
+    CUs, the N = 768 BERT products' shape class): every epilogue against torch on the last
+    tile row, the dropout quads of BIAS_DROP_RES recovered from a zero residual."""
     k = K()
     M, N = 256 * 257, 768
     A, B = rnd(M, Kd, dev=dev, seed=61), rnd(N, Kd, dev=dev, seed=62, scale=0.1)
@@ -182,56 +182,37 @@ def test_gemm_split_k_tail(dev, Kd, monkeypatch):
     R = rnd(M, N, dev=dev, seed=63)
     Zr = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
     aux = (torch.rand(M, N, device=dev) + 0.5).to(torch.bfloat16)
-
-    def run(kind, **kw):
-        outs = {}
-        for tail in ("1", "0"):
-            monkeypatch.setenv("MMU_GEMM_TAIL", tail)
-            f32 = kind == "f32"
-            out = torch.full((M, N), 0.25, dtype=torch.float32 if f32 else torch.bfloat16, device=dev)
-            cs = torch.zeros(N, device=dev)
-            ax = torch.empty(M, N, dtype=torch.bfloat16, device=dev) if kind == k.EPI_BIAS_GELU else kw.get("aux")
-            e = k.epilogue(k.EPI_STORE, accumulate=True) if f32 else k.epilogue(
-                kind, colsum=cs, **{**kw, **({"aux": ax} if ax is not None else {})})
-            k.gemm(A, Kd, True, B, Kd, True, out, N, M, N, Kd, epi=e)
-            outs[tail] = (out.float(), cs, ax)
-        return outs
-
     ref = A.float() @ B.float().t()
-    o = run(k.EPI_BIAS_DROP_RES, bias=bias * 0, residual=Zr, drop_p=0.1, seed=77)
-    assert torch.equal(o["1"][0] == 0, o["0"][0] == 0)  # same dropout counters
     tl = slice(M - 256, M)
-    kept = o["1"][0][tl] != 0
-    close(o["1"][0][tl][kept], (ref[tl] / 0.9)[kept])
-    for kind, kw in ((k.EPI_STORE, {"bias": bias}), (k.EPI_BIAS_GELU, {"bias": bias}),
-                     (k.EPI_DGELU, {"aux": aux}), (k.EPI_ADD_RES, {"residual": R}), ("f32", {})):
-        o = run(kind, **kw)
-        a, b = o["1"][0], o["0"][0]
-        torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2)
-        torch.testing.assert_close(o["1"][1], o["0"][1], rtol=1e-3, atol=1e-1)
-        if kind == k.EPI_BIAS_GELU:
-            torch.testing.assert_close(o["1"][2].float(), o["0"][2].float(), rtol=1e-2, atol=1e-2)
-        want = {k.EPI_STORE: ref + bias, k.EPI_DGELU: ref * aux.float(), k.EPI_ADD_RES: ref + R.float(),
-                "f32": ref + 0.25}.get(kind)
-        if want is not None:
-            close(a[tl], want[tl])
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    k.gemm(A, Kd, True, B, Kd, True, out, N, M, N, Kd,
+           epi=k.epilogue(k.EPI_BIAS_DROP_RES, bias=bias * 0, residual=Zr, drop_p=0.1, seed=77))
+    kept = out.float()[tl] != 0
+    frac = kept.float().mean().item()
+    assert 0.88 < frac < 0.92, frac
+    close(out.float()[tl][kept], (ref[tl] / 0.9)[kept])
+    for kind, kw, want in ((k.EPI_STORE, {"bias": bias}, ref + bias), (k.EPI_DGELU, {"aux": aux}, ref * aux.float()),
+                           (k.EPI_ADD_RES, {"residual": R}, ref + R.float())):
+        cs = torch.zeros(N, device=dev)
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        k.gemm(A, Kd, True, B, Kd, True, out, N, M, N, Kd, epi=k.epilogue(kind, colsum=cs, **kw))
+        close(out.float()[tl], want[tl])
+        torch.testing.assert_close(cs, want.sum(0), rtol=2e-2, atol=2e-2 * want.abs().sum(0).max().item() / 100)
+    f = torch.full((M, N), 0.25, dtype=torch.float32, device=dev)
+    k.gemm(A, Kd, True, B, Kd, True, f, N, M, N, Kd, epi=k.epilogue(k.EPI_STORE, accumulate=True))
+    close(f[tl], ref[tl] + 0.25)
 
 
-def test_gemm_split_k_tail_batched(dev, monkeypatch):
-    """batch 2 x 129 tile rows x 3 column tiles = 774 tiles: tail rows peeled in every batch item"""
+def test_gemm_partial_last_wave_batched(dev):
+    """batch 2 x 129 tile rows x 3 column tiles = 774 tiles, per-item bias"""
     k = K()
     Bt, M, N, Kd = 2, 256 * 129, 768, 512
     A, B = rnd(Bt, M, Kd, dev=dev, seed=64), rnd(Bt, N, Kd, dev=dev, seed=65, scale=0.1)
     bias = torch.randn(Bt, N, device=dev) * 0.1
-    res = {}
-    for tail in ("1", "0"):
-        monkeypatch.setenv("MMU_GEMM_TAIL", tail)
-        C = torch.empty(Bt, M, N, dtype=torch.bfloat16, device=dev)
-        k.gemm(A, Kd, True, B, Kd, True, C, N, M, N, Kd, batch=Bt, sA=M * Kd, sB=N * Kd, sC=M * N,
-               epi=k.epilogue(k.EPI_STORE, bias=bias, bias_bstride=N))
-        res[tail] = C.float()
-    torch.testing.assert_close(res["1"], res["0"], rtol=1e-2, atol=1e-2)
-    close(res["1"][:, -256:], (A.float() @ B.float().transpose(1, 2) + bias[:, None, :])[:, -256:])
+    C = torch.empty(Bt, M, N, dtype=torch.bfloat16, device=dev)
+    k.gemm(A, Kd, True, B, Kd, True, C, N, M, N, Kd, batch=Bt, sA=M * Kd, sB=N * Kd, sC=M * N,
+           epi=k.epilogue(k.EPI_STORE, bias=bias, bias_bstride=N))
+    close(C.float()[:, -256:], (A.float() @ B.float().transpose(1, 2) + bias[:, None, :])[:, -256:])
 
 
 def test_gemm_bias_dropout_residual(dev):
@@ -254,6 +235,36 @@ def test_gemm_bias_dropout_residual(dev):
     assert (kept | dropped).float().mean().item() > 0.999
     rate = (dropped & ~kept).float().mean().item()
     assert abs(rate - p) < 0.01, rate
+
+
+def test_gemm_bias_dropout_residual_f32_stream(dev):
+    """BIAS_DROP_RES into an f32 C reads an f32 residual (the encoder's f32 hidden stream):
+    C = R32 + dropout(A B^T + bias) with no bf16 rounding of R32 or C; the dropout quads are
+    the bf16-output epilogue's (same seed -> same keep pattern); batched with strides."""
+    k = K()
+    Bt, M, N, Kd = 2, 640, 768, 256
+    A, B = rnd(Bt, M, Kd, dev=dev, seed=111), rnd(Bt, N, Kd, dev=dev, seed=112, scale=0.1)
+    bias = torch.randn(Bt, N, device=dev) * 0.1
+    R32 = torch.randn(Bt, M, N, device=dev) * 3.0 + 1.0 / 3.0  # not representable in bf16
+    out = torch.empty(Bt, M, N, dtype=torch.float32, device=dev)
+    y = A.float() @ B.float().transpose(1, 2) + bias[:, None, :]
+    k.gemm(A, Kd, True, B, Kd, True, out, N, M, N, Kd, batch=Bt, sA=M * Kd, sB=N * Kd, sC=M * N,
+           epi=k.epilogue(k.EPI_BIAS_DROP_RES, bias=bias, bias_bstride=N, residual=R32, res_bstride=M * N))
+    torch.testing.assert_close(out, R32 + y, rtol=1e-5, atol=2e-5 * y.abs().max().item())
+    p = 0.1
+    k.gemm(A, Kd, True, B, Kd, True, out, N, M, N, Kd, batch=Bt, sA=M * Kd, sB=N * Kd, sC=M * N,
+           epi=k.epilogue(k.EPI_BIAS_DROP_RES, bias=bias, bias_bstride=N, residual=R32, res_bstride=M * N,
+                          drop_p=p, seed=99))
+    ob = torch.empty(Bt, M, N, dtype=torch.bfloat16, device=dev)
+    Z = torch.zeros(Bt, M, N, dtype=torch.bfloat16, device=dev)
+    k.gemm(A, Kd, True, B, Kd, True, ob, N, M, N, Kd, batch=Bt, sA=M * Kd, sB=N * Kd, sC=M * N,
+           epi=k.epilogue(k.EPI_BIAS_DROP_RES, bias=bias, bias_bstride=N, residual=Z, res_bstride=M * N,
+                          drop_p=p, seed=99))
+    d = out - R32
+    keep = ob.float() != 0
+    torch.testing.assert_close(d[keep], (y / (1 - p))[keep], rtol=1e-5, atol=2e-5 * y.abs().max().item())
+    assert (d[~keep].abs() <= 1e-6 * R32.abs().max()).all()
+    assert abs((~keep).float().mean().item() - p) < 0.01
 
 
 def test_gemm_batched(dev):
@@ -422,10 +433,10 @@ def test_attention_dropout_inference_matches_training_forward(dev, B, L):
 
 # ----------------------------------------------------------------------------- layernorm
 @pytest.mark.parametrize("H,groups,rows_per", [(768, 3, 130), (768, 2, 77), (256, 1, 9), (1024, 2, 64)])
-def test_layernorm_fwd_grouped(dev, H, groups, rows_per, monkeypatch):
+def test_layernorm_fwd_grouped(dev, H, groups, rows_per):
     """row groups with their own affine parameters (the K ensemble members in one launch):
-    both forward kernels (16-B row pairs when the group size is even, else row per wave)
-    against torch per group; odd total row counts."""
+    both forward kernels (16-B row pairs when the group size is even or there is one group,
+    else row per wave: the 77-row groups) against torch per group; odd total row counts."""
     k = K()
     rows = groups * rows_per
     X = rnd(rows, H, dev=dev, seed=31, scale=2.0)
@@ -433,13 +444,11 @@ def test_layernorm_fwd_grouped(dev, H, groups, rows_per, monkeypatch):
     b = torch.randn(groups, H, device=dev) * 0.1
     ref = torch.cat([torch.nn.functional.layer_norm(X[g * rows_per:(g + 1) * rows_per].float(), (H,), w[g], b[g],
                                                     eps=1e-12) for g in range(groups)])
-    for v2 in ("1", "0"):
-        monkeypatch.setenv("MMU_LN_V2", v2)
-        Y = torch.empty_like(X)
-        mean, rstd = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
-        k.layernorm_fwd(X, w, b, Y, mean, rstd, group_rows=rows_per, param_stride=H)
-        close(Y, ref)
-        torch.testing.assert_close(mean, X.float().mean(1), rtol=1e-4, atol=1e-4)
+    Y = torch.empty_like(X)
+    mean, rstd = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+    k.layernorm_fwd(X, w, b, Y, mean, rstd, group_rows=rows_per, param_stride=H)
+    close(Y, ref)
+    torch.testing.assert_close(mean, X.float().mean(1), rtol=1e-4, atol=1e-4)
 
 
 def test_layernorm_fwd_bwd(dev):
@@ -475,6 +484,43 @@ def test_layernorm_fwd_bwd(dev):
     assert (kept | zero).all()
     assert abs(zero.float().mean().item() - p) < 0.01
     torch.testing.assert_close(sbias, dd.sum(0), rtol=1e-2, atol=0.05)
+
+
+@pytest.mark.parametrize("groups", [1, 3])
+def test_layernorm_f32_stream_fwd_bwd(dev, groups):
+    """mmu_layernorm_fwd_f32 (f32 X -> bf16 Y + f32 Y32, grouped affine params as for the
+    ensemble members) and mmu_layernorm_bwd_f32 against torch fp32 on the same f32 input."""
+    k = K()
+    rows_per, H, p, seed = 111, 768, 0.1, 5
+    rows = groups * rows_per
+    X = torch.randn(rows, H, device=dev) * 3.0 + 0.5
+    w = torch.randn(groups, H, device=dev) * 0.1 + 1
+    b = torch.randn(groups, H, device=dev) * 0.1
+    Y = torch.empty(rows, H, dtype=torch.bfloat16, device=dev)
+    Y32 = torch.empty(rows, H, device=dev)
+    mean, rstd = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+    k.layernorm_fwd_f32(X, w, b, Y, Y32, mean, rstd, group_rows=rows_per, param_stride=H)
+    ref = torch.cat([torch.nn.functional.layer_norm(X[g * rows_per:(g + 1) * rows_per], (H,), w[g], b[g], eps=1e-12)
+                     for g in range(groups)])
+    torch.testing.assert_close(Y32, ref, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(Y.float(), ref, rtol=2 ** -8, atol=1e-3)  # one bf16 rounding of the f32 row
+    torch.testing.assert_close(mean, X.mean(1), rtol=1e-5, atol=1e-5)
+    if groups > 1:
+        return
+    xr, wr, br = X.clone().requires_grad_(True), w[0].clone().requires_grad_(True), b[0].clone().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (H,), wr, br, eps=1e-12)
+    dY = rnd(rows, H, dev=dev, seed=22)
+    dX, dXd = torch.empty_like(Y), torch.empty_like(Y)
+    P = k.ln_parts(rows)
+    pw, pb, pbias = (torch.empty(P, H, device=dev) for _ in range(3))
+    k.layernorm_bwd(dY, X, mean, rstd, w[0], dX, dXd, p, seed, pw, pb, pbias)
+    gx, gw, gb = torch.autograd.grad(yr, (xr, wr, br), dY.float())
+    close(dX, gx)
+    sw, sb = torch.empty(H, device=dev), torch.empty(H, device=dev)
+    k.colsum_reduce(pw, sw)
+    k.colsum_reduce(pb, sb)
+    torch.testing.assert_close(sw, gw, rtol=1e-2, atol=0.05)
+    torch.testing.assert_close(sb, gb, rtol=1e-2, atol=0.05)
 
 
 # ----------------------------------------------------------------------------- pooling / adam / uncertainty

@@ -2,7 +2,7 @@
 (tests/golden, produced by oracle/gen_golden.py from /root/reference src/mmbt.py)
 and against the CPU oracle on the same seeded weights / inputs.
 
-Tolerance (north star: 1e-2 for bf16): max |logit error| <= 2e-2 * max|logit| + 2e-3;
+Tolerance (north star: 1e-2 for bf16): max |logit error| <= 1e-2 * max|logit|;
 the HIP path computes in bf16 (f32 accumulation) while the reference is fp32.
 """
 import json
@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
-def tol_check(got, ref, rel=2e-2, abs_=2e-3, what=""):
+def tol_check(got, ref, rel=1e-2, abs_=0.0, what=""):
     got, ref = np.asarray(got, dtype=np.float64), np.asarray(ref, dtype=np.float64)
     err = np.abs(got - ref).max()
     scale = np.abs(ref).max()
@@ -93,7 +93,7 @@ def test_train_step_grads_match_reference_golden(dev):
     model.store.zero_grad()
     loss = model.compute_loss(model(*x), y.to(dev))
     loss.backward()
-    assert abs(loss.item() - float(g["loss_train"])) < 2e-2 * abs(float(g["loss_train"]))
+    assert abs(loss.item() - float(g["loss_train"])) < 1e-2 * abs(float(g["loss_train"]))
     got = dict(model.named_parameters())
     bad = []
     # floor: key biases have an exactly-zero true gradient (softmax shift invariance); the

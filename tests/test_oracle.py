@@ -77,3 +77,29 @@ def test_uncertainty_reference_definitions():
     conf = p.max(1)
     acc = (p.argmax(1) == y).astype(float)
     assert abs(U.ece(p, y, 15) - np.mean(np.abs(conf - acc))) < 1e-12  # one sample per bin here
+
+
+@pytest.mark.parametrize("tag", ["small_t16", "full_t508"])
+def test_oracle_robustness_matches_reference_golden(tag):
+    """A11 (eval_mmbt_robustness.py:77-93): the oracle's [B, 3+2n, C] stack, with the control
+    index sets drawn from the global RNG in the reference's order, equals the reference's."""
+    from oracle import mmbt_ref as R
+    from oracle.gen_golden import make_inputs
+    from oracle.weights import SMALL, FULL, make_state_dict, checksum
+    cfg = SMALL if tag.startswith("small") else FULL
+    g = np.load(os.path.join(GOLD, f"robustness_{tag}.npz"))
+    sd = make_state_dict(int(g["wseed"]), cfg)
+    assert abs(checksum(sd) - float(g["weight_checksum"])) <= 1e-9 * float(g["weight_checksum"])
+    B, T = g["text"].shape
+    x, y = make_inputs(cfg, B, T, g["mask"].sum(1).tolist(), int(g["seed"]))
+    assert np.array_equal(x[0].numpy(), g["text"])
+    txt, seg, mask, img = x
+    n = int(g["n_repeats"])
+    torch.manual_seed(int(g["rng_seed"]))
+    with torch.no_grad():
+        got = R.robustness(sd, txt, seg, mask, img, cfg, n_repeats=n)
+    assert got.shape == g["preds"].shape == (B, 3 + 2 * n, cfg.n_classes)
+    np.testing.assert_allclose(got.numpy(), g["preds"], rtol=1e-4, atol=1e-5)
+    torch.manual_seed(int(g["rng_seed"]))
+    idx = [R.control_indices(T + cfg.num_image_embeds + 2, cfg.num_image_embeds + 1) for _ in range(n)]
+    assert np.array_equal(np.stack(idx), g["indices_image"])
