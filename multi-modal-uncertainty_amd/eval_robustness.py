@@ -8,9 +8,11 @@ per op (src/uncertainty.py) and writes
   <save_path>/uncertainty_<phase>_logits.npy   [S, K, T, n_classes]
   <save_path>/uncertainty_<phase>_labels.npy   [S]
   <save_path>/uncertainty_<phase>_metrics.json {nll, ece, acc, n, K, T}
-Without --mmbt the reference evaluates FashionMNIST MIMO ResNets / transformers
-with one view zeroed (eval_robustness.py:42-121) -- another model family, out of
-scope for this build, and refused with a message.
+Without --mmbt: the reference's FashionMNIST MIMO robustness pass (eval_robustness.py:42-121,
+BASELINE config 1's model family): each of the 4 quarter-crop views zeroed in turn (the
+weight-sharing model sees the other 3), predictions [4, S, heads, 10] and labels written as
+<checkpoint>_predictions_robustness.npy / <checkpoint>_labels.npy.  --data_dir / --sample_size
+as in train_fashionmnist.py (images synthetic when only the label files exist).
 """
 import argparse
 import json
@@ -41,6 +43,7 @@ FLAGS = [
     ("--num_image_embeds", dict(type=int, default=3)), ("--n_workers", dict(type=int, default=0)),
     ("--bert_model", dict(type=str, default="bert-base-uncased")),
     ("--gin_file", dict(nargs="*", default=[])), ("--gin_param", dict(nargs="*", default=[])),
+    ("--data_dir", dict(type=str, default=None)), ("--sample_size", dict(type=int, default=None)),
 ]
 
 
@@ -94,6 +97,52 @@ def run_mmbt(args):
     return res
 
 
+def run_fmnist(args):
+    """eval_robustness.py:42-121: view i zeroed (or dropped for the weight-sharing model) for
+    i = 0..3 over the test loader, in the reference's loop order."""
+    from src import dataset
+    from src.training_loop import _load_pretrained_model
+    from train_fashionmnist import build_model
+    if args.checkpoint_path is None:
+        raise ValueError("--checkpoint_path is required without --mmbt")
+    model = build_model(args)
+    _, valid, _ = dataset.get_fmnist(datapath=args.data_dir, batch_size=args.batch_size, download=True,
+                                     shuffle=True, sample_size=args.sample_size, seed=args.seed)
+    print("Loading Checkpoint from {}".format(args.checkpoint_path))
+    _load_pretrained_model(model, args.checkpoint_path)
+    dev = torch.device("cuda:{}".format(args.device)) if args.use_gpu and torch.cuda.is_available() \
+        else torch.device("cpu")
+    model.to(dev).eval()
+    outputs, labels, m = [], [], 4
+    with torch.no_grad():
+        for i in range(m):
+            y_hat = []
+            for x, y in valid:
+                if args.model_type != "single-model-weight-sharing":
+                    x, y = dataset.data_forming_func(x, y, "eval", model_type=args.model_type)
+                    x_ = x.to(dev).clone()
+                    x_[:, i] = 0  # view i zeroed, the others kept
+                    y_ = model(x_)
+                else:
+                    b, mm, c, h, w = x.shape
+                    keep = [j for j in range(mm) if j != i]
+                    x_, y = dataset.data_forming_func(x[:, keep].contiguous(), y, "eval", model_type=args.model_type)
+                    y_ = model(x_.to(dev)).view(b, mm - 1, -1)
+                y_hat.append(y_.float().cpu().numpy())
+                if i == 0:
+                    labels.append(y.cpu().numpy())
+            outputs.append(np.concatenate(y_hat, axis=0))
+    outputs = np.stack(outputs, axis=0)
+    M_, S, M, C = outputs.shape
+    print("Gathered predictions of {} samples, {} views, {} dups, {} classes".format(S, M_, M, C))
+    labels = np.concatenate(labels, axis=0)
+    os.makedirs(args.save_path, exist_ok=True)
+    name = args.checkpoint_path.split("/")[-1].split(".")[0]
+    np.save(os.path.join(args.save_path, f"{name}_predictions_robustness.npy"), outputs)
+    np.save(os.path.join(args.save_path, f"{name}_labels.npy"), labels)
+    return outputs, labels
+
+
 def main(argv=None):
     parser = argparse.ArgumentParser(description="Train Models")
     get_args(parser)
@@ -101,10 +150,7 @@ def main(argv=None):
     assert remaining == [], remaining
     from src import gin
     gin.load(args, args.gin_file, args.gin_param)
-    if not args.mmbt:
-        raise NotImplementedError("FashionMNIST MIMO robustness (reference eval_robustness.py:42-121) is another "
-                                  "model family, out of scope for the MI355X MMBT build; use --mmbt")
-    return run_mmbt(args)
+    return run_mmbt(args) if args.mmbt else run_fmnist(args)
 
 
 if __name__ == "__main__":

@@ -378,3 +378,130 @@ class SyntheticFlava(Dataset):
         img = torch.randn(self.l_img, self.width, generator=g)
         txt = torch.randn(T, self.width, generator=g)
         return img, txt, torch.randint(0, self.n_classes, (1,), generator=g)
+
+
+# ------------------------------------------------------------------------------ FashionMNIST
+# BASELINE config 1 (train_fashionmnist.py on CPU).  Reference src/dataset.py:56-182.
+def data_forming_func(x, y, phase, model_type):
+    """Targets per head / view shuffles of a quarter-crop batch x [B, m, C, H, W]
+    (reference src/dataset.py:56-100; the same global-RNG draws in the same order)."""
+    b, m, c, h, w = x.shape
+    if model_type == "Vanilla" and phase == "train":
+        y = y.unsqueeze(1).repeat(1, 1)
+    elif model_type == "single-model-weight-sharing":
+        y = y.unsqueeze(1).repeat(1, m).view(-1)  # [B*m]
+        x = x.view(-1, c, h, w)                   # [B*m, C, H, W]
+    elif model_type == "MultiHead" and phase == "train":
+        y = y.unsqueeze(1).repeat(1, m)
+    elif model_type == "MIMO-shuffle-instance" and phase == "train":
+        # 4 independent instance permutations, one per view (the reference hard-codes 4)
+        xs, ys = [], []
+        for i in range(4):
+            idx = torch.randperm(x.size(0))
+            xs.append(x[idx, i])
+            ys.append(y[idx])
+        x, y = torch.stack(xs, dim=1), torch.stack(ys, dim=1)
+    elif model_type == "MIMO-shuffle-view" and phase == "train":
+        x = x[:, torch.randperm(x.size(1))]
+        y = y.unsqueeze(1).repeat(1, m)
+    elif model_type == "MIMO-shuffle-all" and phase == "train":
+        xs, ys = [], []
+        for i in range(m):
+            idx = torch.randperm(x.size(0))
+            xs.append(x[idx, i])
+            ys.append(y[idx])
+        x, y = torch.stack(xs, dim=1), torch.stack(ys, dim=1)
+        ind = torch.randperm(x.size(1))
+        x, y = x[:, ind], y[:, ind]
+    return x, y
+
+
+class QuarterCrop(object):
+    """28x28 image -> its 4 quarters [upper-left, upper-right, lower-left, lower-right]
+    (reference src/dataset.py:103-127).  Works on an [H, W] array / tensor."""
+
+    def __init__(self, expected_size):
+        self.expected_size = expected_size
+        self.crop_size_w = int(expected_size[0] / 2)
+        self.crop_size_h = int(expected_size[1] / 2)
+
+    def __call__(self, img):
+        h, w = img.shape[-2:]
+        assert w == self.expected_size[0] and h == self.expected_size[1]
+        ch, cw = self.crop_size_h, self.crop_size_w
+        tops, lefts = [0, 0, cw, ch], [0, ch, 0, ch]  # the reference's (starts_x, starts_y) as (top, left)
+        return [img[..., t:t + ch, l:l + cw] for t, l in zip(tops, lefts)]
+
+
+def read_idx(path):
+    """IDX file (optionally .gz) -> numpy array (the FashionMNIST / MNIST container format)."""
+    import gzip
+    op = gzip.open if path.endswith(".gz") else open
+    with op(path, "rb") as f:
+        data = f.read()
+    magic = int.from_bytes(data[0:4], "big")
+    if magic >> 8 != 0x08:
+        raise ValueError(f"{path}: not a uint8 IDX file (magic {magic:#x})")
+    nd = magic & 0xFF
+    dims = [int.from_bytes(data[4 + 4 * i:8 + 4 * i], "big") for i in range(nd)]
+    arr = np.frombuffer(data, dtype=np.uint8, offset=4 + 4 * nd)
+    if arr.size != int(np.prod(dims)):
+        raise ValueError(f"{path}: {arr.size} bytes for dims {dims}")
+    return arr.reshape(dims)
+
+
+def _find_idx(root, stem):
+    for d in (os.path.join(root, "FashionMNIST", "raw"), os.path.join(root, "FashionMNIST"), root):
+        for name in (stem, stem + ".gz"):
+            p = os.path.join(d, name)
+            if os.path.exists(p):
+                return p
+    return None
+
+
+class FashionMNISTQuarters(Dataset):
+    """FashionMNIST as the reference serves it (torchvision FashionMNIST + QuarterCrop +
+    ToTensor: [4, 1, 14, 14] float in [0, 1], int64 label; reference src/dataset.py:148-162).
+
+    Labels come from the IDX label file under ``datapath``.  The image files are absent
+    from this offline checkout (only the label files ship): when no image file
+    is found the images are SYNTHETIC -- seeded uint8 28x28 noise per index -- and
+    ``self.synthetic`` is True."""
+
+    def __init__(self, datapath, train=True, seed=777, sample_size=None):
+        pre = "train" if train else "t10k"
+        lab = _find_idx(datapath, f"{pre}-labels-idx1-ubyte")
+        if lab is None:
+            raise FileNotFoundError(f"no FashionMNIST {pre} label file under {datapath}")
+        self.labels = torch.from_numpy(read_idx(lab).astype(np.int64))
+        img = _find_idx(datapath, f"{pre}-images-idx3-ubyte")
+        self.synthetic = img is None
+        if self.synthetic:
+            g = torch.Generator().manual_seed(seed + (0 if train else 1))
+            self.images = torch.randint(0, 256, (len(self.labels), 28, 28), generator=g, dtype=torch.uint8)
+        else:
+            self.images = torch.from_numpy(read_idx(img).copy())
+        if sample_size is not None:
+            self.labels, self.images = self.labels[:sample_size], self.images[:sample_size]
+        self.crop = QuarterCrop((28, 28))
+
+    def __len__(self):
+        return len(self.labels)
+
+    def __getitem__(self, i):
+        quarters = self.crop(self.images[i].float().div(255.0))  # ToTensor: /255
+        return torch.stack([q.unsqueeze(0) for q in quarters]), self.labels[i]
+
+
+def get_fmnist(datapath=None, batch_size=128, download=False, shuffle=True, sample_size=None, seed=777):
+    """(train_loader, test_loader, None) of [B, 4, 1, 14, 14] quarter crops (reference
+    src/dataset.py:130-175; ``download`` is accepted and ignored: there is no network)."""
+    if datapath is None:
+        from . import DATA_DIR as datapath
+    torch.manual_seed(seed)
+    training = FashionMNISTQuarters(datapath, True, seed, sample_size)
+    testing = FashionMNISTQuarters(datapath, False, seed, sample_size)
+    train_loader = torch.utils.data.DataLoader(training, batch_size=batch_size, shuffle=shuffle)
+    test_loader = torch.utils.data.DataLoader(testing, batch_size=batch_size, shuffle=False)
+    print("training_loader LENGTH:", len(train_loader))
+    return train_loader, test_loader, None

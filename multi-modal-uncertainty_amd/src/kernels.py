@@ -329,9 +329,13 @@ def conv3x3_implicit(X, Wk, Y):
     n, c, h, w = X.shape
     nout = Y.shape[1]
     cl = torch.channels_last
-    if (Y.shape != (n, nout, h, w) or Y.dtype != torch.bfloat16 or Wk.numel() != nout * 9 * c
-            or not X.is_contiguous(memory_format=cl) or not Y.is_contiguous(memory_format=cl)
-            or not (Wk.is_contiguous() or Wk.is_contiguous(memory_format=cl))):
+    # the kernel reads Wk[n][tap * C + c]: either a [Nout, 3, 3, C] contiguous tensor or a
+    # [Nout, C, 3, 3] filter whose memory is channels-last (both are [Nout][3][3][C] in memory)
+    wk_ok = Wk.dim() == 4 and (
+        (tuple(Wk.shape) == (nout, 3, 3, c) and Wk.is_contiguous())
+        or (tuple(Wk.shape) == (nout, c, 3, 3) and Wk.is_contiguous(memory_format=cl)))
+    if (Y.shape != (n, nout, h, w) or Y.dtype != torch.bfloat16 or not wk_ok
+            or not X.is_contiguous(memory_format=cl) or not Y.is_contiguous(memory_format=cl)):
         raise N.NativeError("conv3x3_implicit: X / Y channels-last bf16 [N, C, H, W], Wk [Nout][3][3][C] bf16")
     N.call("mmu_conv3x3_implicit", _ptr(X), _ptr(Wk), _ptr(Y), n, h, w, c, nout, _stream(X))
 

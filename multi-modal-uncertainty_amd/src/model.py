@@ -359,3 +359,125 @@ class FlavaFusionTransfomerwithCLSToken(FlavaFusionTransfomer):
         for i, fc in enumerate(self.output_layers):
             out_list.append(fc(out[:, i, :]))
         return torch.stack(out_list, dim=1)
+
+
+# ------------------------------------------------------------------ FashionMNIST MIMO family
+# BASELINE config 1 (train_fashionmnist.py, CPU plumbing).  Same class names, constructor
+# arguments, module trees and state_dict keys as the reference src/model.py:8-171.
+model_configure = {  # model_type -> (emb_dim = views stacked as channels, out_dim = heads)
+    "Vanilla": (4, 1),
+    "MIMO-shuffle-instance": (4, 4),
+    "MIMO-shuffle-view": (4, 4),
+    "MultiHead": (4, 4),
+    "MIMO-shuffle-all": (4, 4),
+    "single-model-weight-sharing": (1, 1),
+}
+
+
+class ResNet(nn.Module):
+    """src/model.py:17-56: 3x3 stem (stride 1, no max-pool), layer1 / layer2 of ``block``,
+    AvgPool2d(4); convs N(0, sqrt(2 / (k*k*out))), BN gamma 1 beta 0."""
+
+    def __init__(self, num_channels, block, layers):
+        self.inplanes = 64
+        super().__init__()
+        self.conv1 = nn.Conv2d(num_channels, 64, kernel_size=3, stride=1, padding=1, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.layer1 = self._make_layer(block, 64, layers[0])
+        self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
+        self.avgpool = nn.AvgPool2d(4)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                fan = m.kernel_size[0] * m.kernel_size[1] * m.out_channels
+                m.weight.data.normal_(0, (2.0 / fan) ** 0.5)
+            elif isinstance(m, nn.BatchNorm2d):
+                m.weight.data.fill_(1)
+                m.bias.data.zero_()
+
+    def _make_layer(self, block, planes, blocks, stride=1):
+        downsample = None
+        if stride != 1 or self.inplanes != planes * block.expansion:
+            downsample = nn.Sequential(
+                nn.Conv2d(self.inplanes, planes * block.expansion, kernel_size=1, stride=stride, bias=False),
+                nn.BatchNorm2d(planes * block.expansion))
+        mods = [block(self.inplanes, planes, stride, downsample)]
+        self.inplanes = planes * block.expansion
+        mods += [block(self.inplanes, planes) for _ in range(1, blocks)]
+        return nn.Sequential(*mods)
+
+
+class MultiHeadFC(nn.Module):
+    """src/model.py:58-70: one Linear with out_dim * num_classes outputs -> [B, out_dim, C]."""
+
+    def __init__(self, input_dim, num_classes, out_dim):
+        super().__init__()
+        self.num_classes = num_classes
+        self.fc = nn.Linear(input_dim, num_classes * out_dim)
+
+    def forward(self, x):
+        out = self.fc(x)
+        return out.view(*out.shape[:-1], -1, self.num_classes)  # == stack(split(out, C, -1), 1)
+
+
+def _mimo_loss(loss_fn, y_hat, y, eval):
+    """src/model.py:102-112 / 161-171: per-head CE in training, CE of the head mean in eval."""
+    assert y.shape[0] == y_hat.shape[0]
+    y = y.view(-1)
+    y_hat = y_hat.reshape(-1, y_hat.shape[2]) if not eval else y_hat.mean(1)
+    return loss_fn(y_hat, y)
+
+
+class MIMOResNet(ResNet):
+    """src/model.py:72-112.  The views (or ensemble members) of x [B, E, C, H, W] are stacked
+    as channels; a 4-D input is the weight-sharing model's [B*E, C, H, W]."""
+
+    def __init__(self, num_channels, emb_dim, out_dim, num_classes):
+        from .layers import BasicBlock
+        super().__init__(num_channels * emb_dim, BasicBlock, [2, 2, 2])
+        self.output_layer = MultiHeadFC(128 * BasicBlock.expansion, num_classes, out_dim)
+        self.loss = torch.nn.CrossEntropyLoss()
+
+    def forward(self, x):
+        if x.dim() == 5:
+            x = x.reshape(x.size(0), -1, x.size(3), x.size(4))
+        x = self.relu(self.bn1(self.conv1(x)))
+        x = self.layer2(self.layer1(x))
+        x = self.avgpool(x).flatten(1)
+        return self.output_layer(x)  # [B, out_dim, num_classes]
+
+    def compute_loss(self, y_hat, y, eval=False):
+        return _mimo_loss(self.loss, y_hat, y, eval)
+
+
+class MIMOTransfomer(nn.Module):
+    """src/model.py:114-171: each view's 14x14 pixels -> Linear(196, hidden) token, ln_pre,
+    the fusion Transformer (HIP blocks of this module: attention over the SAMPLE axis, the
+    reference's batch_first=False quirk), ln_post, per-head Linear on view i's token.
+    GPU only (the blocks have no CPU path)."""
+
+    def __init__(self, out_dim, num_classes, hidden_size, image_dim=14 * 14, multimodal_num_hidden_layers=3,
+                 multimodal_num_attention_heads=3, drop=0):
+        super().__init__()
+        self.image_to_mm_projection = nn.Linear(image_dim, hidden_size)
+        self.mm_encoder = Transformer(width=hidden_size, layers=multimodal_num_hidden_layers,
+                                      heads=multimodal_num_attention_heads, drop=drop)
+        self.output_layers = nn.ModuleList([nn.Linear(hidden_size, num_classes) for _ in range(out_dim)])
+        self.loss = torch.nn.CrossEntropyLoss()
+        self.ln_pre = nn.LayerNorm(hidden_size)
+        self.ln_post = nn.LayerNorm(hidden_size)
+
+    def forward(self, x):
+        K._dev_check(x)
+        b, e, c, h, w = x.shape
+        # Linear(196 -> E) in f32 (K = 196 rows are not 16-B aligned in bf16; 0.3 MFLOP/token)
+        t = torch.nn.functional.linear(x.reshape(b, e * c, h * w).float(), self.image_to_mm_projection.weight,
+                                       self.image_to_mm_projection.bias)
+        t = LNFunction.apply(t.to(bf16).contiguous(), self.ln_pre.weight, self.ln_pre.bias, self.ln_pre.eps)
+        t = self.mm_encoder(t)
+        t = LNFunction.apply(t, self.ln_post.weight, self.ln_post.bias, self.ln_post.eps).float()
+        t = t.view(b, e, c, -1).mean(2)  # [B, E, hidden]
+        return torch.stack([fc(t[:, i, :]) for i, fc in enumerate(self.output_layers)], dim=1)
+
+    def compute_loss(self, y_hat, y, eval=False):
+        return _mimo_loss(self.loss, y_hat, y, eval)

@@ -258,6 +258,70 @@ FLAVA_CASES = {  # tag: (cfg kwargs, B, L_img, L_txt, seed)
 }
 
 
+FMNIST_TYPES = ["Vanilla", "MIMO-shuffle-instance", "MIMO-shuffle-view", "MultiHead", "MIMO-shuffle-all",
+                "single-model-weight-sharing"]
+
+
+def gen_fmnist():
+    """BASELINE config 1: the reference src/model.py MIMOResNet / MIMOTransfomer and
+    src/dataset.py data_forming_func on a seeded [B, 4, 1, 14, 14] quarter-crop batch, the
+    reference train_fashionmnist.py acc, and one SGD step (train_fashionmnist.py:115-118)."""
+    from oracle.weights import SMALL
+    _import_reference(SMALL, 0.0)
+    from src import model as ref_model  # the reference's own module
+    forming = _reference_function("src/dataset.py", "data_forming_func")
+    ref_acc = _reference_function("train_fashionmnist.py", "acc")
+    B = 6
+    g = torch.Generator().manual_seed(31)
+    x = torch.rand(B, 4, 1, 14, 14, generator=g)
+    y = torch.randint(0, 10, (B,), generator=g)
+    out = {"x": x.numpy(), "y": y.numpy()}
+    for mt in FMNIST_TYPES:
+        torch.manual_seed(500)
+        xf, yf = forming(x, y, "train", model_type=mt)
+        out[f"form_{mt}_x"], out[f"form_{mt}_y"] = xf.numpy(), yf.numpy()
+        emb, od = ref_model.model_configure[mt]
+        torch.manual_seed(600)
+        model = ref_model.MIMOResNet(num_channels=1, emb_dim=emb, out_dim=od, num_classes=10)
+        sd = model.state_dict()
+        # weights: the reference's own seeded init; the build's module tree must draw the same
+        # numbers in the same order (checked per tensor by these sums)
+        out[f"init_{mt}_sums"] = np.array([float(v.double().sum()) for v in sd.values()])
+        opt = torch.optim.SGD(model.parameters(), lr=0.1, weight_decay=0.001, momentum=0.9)
+        model.train()
+        yh = model(xf)
+        loss = model.compute_loss(yh, yf)
+        opt.zero_grad()
+        loss.backward()
+        out[f"train_{mt}_logits"] = yh.detach().numpy()
+        out[f"train_{mt}_loss"] = np.float64(loss.detach())
+        out[f"train_{mt}_acc"] = np.float64(ref_acc(yh.detach(), yf, False))
+        out[f"train_{mt}_grad_norms"] = np.array([float(p.grad.double().norm()) for p in model.parameters()])
+        opt.step()
+        out[f"train_{mt}_param_sums"] = np.array([float(p.detach().double().sum()) for p in model.parameters()])
+        model.eval()
+        with torch.no_grad():
+            xe, ye = forming(x, y, "eval", model_type=mt)
+            ye_hat = model(xe)
+            out[f"eval_{mt}_logits"] = ye_hat.numpy()
+            out[f"eval_{mt}_loss"] = np.float64(model.compute_loss(ye_hat, ye, eval=True))
+            out[f"eval_{mt}_acc"] = np.float64(ref_acc(ye_hat, ye, True))
+        out[f"keys_{mt}"] = np.array(list(model.state_dict().keys()))
+    # MIMOTransfomer (eval, dropout 0): logits the HIP fusion blocks must reproduce
+    for mt in ("MultiHead", "MIMO-shuffle-instance"):
+        torch.manual_seed(700)
+        model = ref_model.MIMOTransfomer(out_dim=4, num_classes=10, hidden_size=768, image_dim=196,
+                                         multimodal_num_hidden_layers=3, multimodal_num_attention_heads=3, drop=0)
+        model.eval()
+        out[f"tf_{mt}_init_sums"] = np.array([float(v.double().sum()) for v in model.state_dict().values()])
+        out[f"tf_{mt}_keys"] = np.array(list(model.state_dict().keys()))
+        with torch.no_grad():
+            out[f"tf_{mt}_logits"] = model(x).numpy()
+            out[f"tf_{mt}_loss_eval"] = np.float64(model.compute_loss(model(x), y, eval=True))
+    np.savez_compressed(os.path.join(OUT, "fmnist.npz"), **out)
+    print("wrote fmnist.npz")
+
+
 def gen_framework():
     from oracle.weights import SMALL
     from oracle.tiny_model import TinyMMBT, tiny_batches, acc
@@ -298,14 +362,14 @@ def gen_framework():
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="all", choices=["all", "small", "full", "framework", "flava",
-                                                       "robustness"])
+                                                       "robustness", "fmnist"])
     a = ap.parse_args()
     sys.path.insert(0, REPO)
     from oracle.weights import SMALL, FULL
     # each generator imports the reference fresh with its own stub config -> run each in a subprocess
     if a.what == "all":
         import subprocess
-        for w in ("small", "full", "framework", "flava", "robustness"):
+        for w in ("small", "full", "framework", "flava", "robustness", "fmnist"):
             subprocess.check_call([sys.executable, "-m", "oracle.gen_golden", "--what", w], cwd=REPO)
     elif a.what == "small":
         gen_mmbt("small_t16", SMALL, B=2, T=16, lens=[16, 9], seed=0)
@@ -318,5 +382,7 @@ if __name__ == "__main__":
     elif a.what == "robustness":
         gen_robustness("small_t16", SMALL, B=3, T=16, lens=[16, 9, 12], n_repeats=3, seed=5)
         gen_robustness("full_t508", FULL, B=2, T=508, lens=[508, 301], n_repeats=2, seed=6)
+    elif a.what == "fmnist":
+        gen_fmnist()
     else:
         gen_framework()

@@ -1,0 +1,177 @@
+"""BASELINE config 1 (train_fashionmnist.py, CPU plumbing) and the gin front end.
+
+Parity: tests/golden/fmnist.npz was written by oracle/gen_golden.py --what fmnist from the
+REFERENCE's own src/model.py MIMOResNet, src/dataset.py data_forming_func and
+train_fashionmnist.py acc (seeded inputs / init).  The label fixtures are the reference's
+own FashionMNIST label files (fashionMNIST/FashionMNIST/raw/*-labels-idx1-ubyte.gz); the
+image files are absent from the reference checkout, so images are synthetic.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(HERE, "..", "multi-modal-uncertainty_amd")
+sys.path.insert(0, PKG)
+
+from src import dataset, gin  # noqa: E402
+from src.model import MIMOResNet, model_configure  # noqa: E402
+
+G = np.load(os.path.join(HERE, "golden", "fmnist.npz"))
+FM_ROOT = os.path.join(HERE, "golden", "fmnist")
+TYPES = ["Vanilla", "MIMO-shuffle-instance", "MIMO-shuffle-view", "MultiHead", "MIMO-shuffle-all",
+         "single-model-weight-sharing"]
+
+
+def _acc():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("train_fmnist", os.path.join(PKG, "train_fashionmnist.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_label_files_read():
+    """IDX reader on the reference's label files: 60k / 10k labels, 10 balanced classes."""
+    tr = dataset.read_idx(os.path.join(FM_ROOT, "FashionMNIST", "train-labels-idx1-ubyte.gz"))
+    te = dataset.read_idx(os.path.join(FM_ROOT, "FashionMNIST", "t10k-labels-idx1-ubyte.gz"))
+    assert tr.shape == (60000,) and te.shape == (10000,)
+    assert np.bincount(tr).tolist() == [6000] * 10 and np.bincount(te).tolist() == [1000] * 10
+    ds = dataset.FashionMNISTQuarters(FM_ROOT, train=False, seed=3, sample_size=5)
+    x, y = ds[2]
+    assert ds.synthetic and x.shape == (4, 1, 14, 14) and x.dtype == torch.float32 and int(y) == int(te[2])
+    # quarters tile the 28x28 image: UL, UR, LL, LR
+    full = ds.images[2].float() / 255
+    assert torch.equal(torch.cat([torch.cat([x[0, 0], x[1, 0]], 1), torch.cat([x[2, 0], x[3, 0]], 1)], 0), full)
+
+
+@pytest.mark.parametrize("mt", TYPES)
+def test_data_forming_matches_reference(mt):
+    x, y = torch.from_numpy(G["x"]), torch.from_numpy(G["y"])
+    torch.manual_seed(500)
+    xf, yf = dataset.data_forming_func(x, y, "train", model_type=mt)
+    assert np.array_equal(xf.numpy(), G[f"form_{mt}_x"]) and np.array_equal(yf.numpy(), G[f"form_{mt}_y"])
+
+
+@pytest.mark.parametrize("mt", TYPES)
+def test_mimo_resnet_matches_reference(mt):
+    """Seeded init (same RNG draws), train forward / loss / grads / acc, one SGD step, eval."""
+    acc = _acc().acc
+    x, y = torch.from_numpy(G["x"]), torch.from_numpy(G["y"])
+    torch.manual_seed(500)
+    xf, yf = dataset.data_forming_func(x, y, "train", model_type=mt)
+    emb, od = model_configure[mt]
+    torch.manual_seed(600)
+    model = MIMOResNet(num_channels=1, emb_dim=emb, out_dim=od, num_classes=10)
+    sd = model.state_dict()
+    assert list(sd.keys()) == [str(k) for k in G[f"keys_{mt}"]]
+    np.testing.assert_allclose([float(v.double().sum()) for v in sd.values()], G[f"init_{mt}_sums"], rtol=1e-6,
+                               atol=1e-6)
+    opt = torch.optim.SGD(model.parameters(), lr=0.1, weight_decay=0.001, momentum=0.9)
+    model.train()
+    yh = model(xf)
+    loss = model.compute_loss(yh, yf)
+    opt.zero_grad()
+    loss.backward()
+    np.testing.assert_allclose(yh.detach().numpy(), G[f"train_{mt}_logits"], rtol=1e-4, atol=1e-5)
+    assert abs(float(loss) - float(G[f"train_{mt}_loss"])) < 1e-5
+    assert abs(float(acc(yh.detach(), yf, False)) - float(G[f"train_{mt}_acc"])) < 1e-4
+    np.testing.assert_allclose([float(p.grad.double().norm()) for p in model.parameters()],
+                               G[f"train_{mt}_grad_norms"], rtol=1e-4, atol=1e-6)
+    opt.step()
+    np.testing.assert_allclose([float(p.detach().double().sum()) for p in model.parameters()],
+                               G[f"train_{mt}_param_sums"], rtol=1e-5, atol=1e-5)
+    model.eval()
+    with torch.no_grad():
+        xe, ye = dataset.data_forming_func(x, y, "eval", model_type=mt)
+        ye_hat = model(xe)
+    np.testing.assert_allclose(ye_hat.numpy(), G[f"eval_{mt}_logits"], rtol=1e-4, atol=1e-5)
+    assert abs(float(model.compute_loss(ye_hat, ye, eval=True)) - float(G[f"eval_{mt}_loss"])) < 1e-5
+    assert abs(float(acc(ye_hat, ye, True)) - float(G[f"eval_{mt}_acc"])) < 1e-4
+
+
+@pytest.mark.parametrize("mt", ["Vanilla", "MIMO-shuffle-all", "single-model-weight-sharing"])
+def test_train_fashionmnist_entry(tmp_path, mt):
+    """The entry point end to end on the CPU: gin file + CLI, 2 epochs through Model_ and the
+    default callbacks (history.csv, checkpoints), then --resume for one more epoch."""
+    mod = _acc()
+    gf = tmp_path / "t.gin"
+    gf.write_text("# config-1 bindings\ntrain.batch_size = 16\ntrain.lr=0.05\nMMTM_MVCNN.num_views=2\n")
+    save = tmp_path / "run"
+    argv = ["--save_path", str(save), "--data_dir", FM_ROOT, "--sample_size", "48", "--n_epochs", "3",
+            "--model_type", mt, "--gin_file", str(gf)]
+    H = mod.main(argv)
+    assert H["epoch"] == [1, 2]
+    for k in ("loss", "acc", "val_loss", "val_acc", "test_loss", "test_acc"):
+        assert len(H[k]) == 2 and all(np.isfinite(H[k]))
+    files = set(os.listdir(save))
+    assert {"history.csv", "model_last_epoch.pt", "model_epoch_1.pt", "model_epoch_2.pt"} <= files
+    H2 = mod.main(argv[:-2] + ["--n_epochs", "4", "--resume"])
+    assert list(H2["epoch"]) == [1, 2, 3]
+
+
+def test_gin_parser_and_mapping():
+    import types
+    text = ("# comment\nMMTM_MVCNN.pretraining=False\ntrain.lr=0.1\ntrain.callbacks=['A', 'B',\n  'C']\n"
+            "training_loop.n_epochs=300\nX.f = @some_fn\nnum = 3  # trailing\n")
+    b = gin.parse_bindings(text)
+    assert b["train.callbacks"] == ["A", "B", "C"] and b["X.f"] == "@some_fn" and b["num"] == 3
+    args = types.SimpleNamespace(lr=0.5, n_epochs=10, num=1)
+    unused = gin.apply_to_args(args, b)
+    assert args.lr == 0.1 and args.n_epochs == 300 and args.num == 3
+    assert "MMTM_MVCNN.pretraining" in unused and "train.callbacks" in unused
+    with pytest.raises(ValueError):
+        gin.parse_bindings("train.lr = [1,\n")
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/configs"), reason="reference configs not present")
+def test_gin_parses_reference_configs():
+    """Every .gin file the reference ships parses; train.* bindings land on train flags."""
+    import glob
+    import types
+    files = sorted(glob.glob("/root/reference/configs/*.gin"))
+    assert len(files) == 5
+    for f in files:
+        b = gin.parse_bindings(open(f).read())
+        assert b, f
+    args = types.SimpleNamespace(batch_size=32, lr=0.5, wd=0.1, momentum=0.9)
+    gin.load(args, [os.path.join("/root/reference/configs", "training.gin")])
+    assert (args.batch_size, args.lr, args.wd, args.momentum) == (8, 0.1, 0.0, 0)
+
+
+@pytest.mark.parametrize("mt", ["MultiHead", "single-model-weight-sharing"])
+def test_eval_robustness_fmnist(tmp_path, mt):
+    """eval_robustness.py without --mmbt (reference eval_robustness.py:42-121): [4 views, S,
+    heads, 10] predictions with view i zeroed (dropped for weight sharing), labels [S(*3)]."""
+    import importlib.util
+    mod = _acc()
+    save = tmp_path / "run"
+    mod.main(["--save_path", str(save), "--data_dir", FM_ROOT, "--sample_size", "24", "--n_epochs", "2",
+              "--batch_size", "8", "--model_type", mt])
+    spec = importlib.util.spec_from_file_location("eval_rob", os.path.join(PKG, "eval_robustness.py"))
+    ev = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ev)
+    ck = str(save / "model_last_epoch.pt")
+    outs, labels = ev.main(["--checkpoint_path", ck, "--save_path", str(tmp_path / "ev"), "--data_dir", FM_ROOT,
+                            "--sample_size", "24", "--batch_size", "8", "--model_type", mt])
+    heads = model_configure[mt][1] if mt != "single-model-weight-sharing" else 3
+    S = 24
+    assert outs.shape == (4, S, heads, 10) and np.isfinite(outs).all()
+    assert labels.shape == ((S,) if mt != "single-model-weight-sharing" else (S * 3,))
+    assert os.path.exists(tmp_path / "ev" / "model_last_epoch_predictions_robustness.npy")
+    # view 0 zeroed, recomputed directly from the checkpoint on the test set's first batch
+    model = mod.build_model(type("A", (), {"transformer": False, "model_type": mt})())
+    model.load_state_dict(torch.load(ck, weights_only=True)["model"])
+    model.eval()
+    ds = dataset.FashionMNISTQuarters(FM_ROOT, train=False, seed=42, sample_size=24)
+    x = torch.stack([ds[i][0] for i in range(8)])
+    with torch.no_grad():
+        if mt == "single-model-weight-sharing":
+            ref = model(x[:, 1:].reshape(-1, 1, 14, 14)).view(8, 3, -1)
+        else:
+            x[:, 0] = 0
+            ref = model(x)
+    np.testing.assert_allclose(outs[0, :8], ref.numpy(), rtol=1e-5, atol=1e-5)
