@@ -22,6 +22,7 @@ Rank 0 prints one JSON line (see README/DESIGN for the field definitions).
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -56,16 +57,41 @@ def parse():
     ap.add_argument("--flava-batch", type=int, default=128, help="FLAVA per-rank batch (train.py --batch_size)")
     ap.add_argument("--flava-tokens", type=str, default="197,77", help="FLAVA image,text embedding lengths")
     ap.add_argument("--cpu-batch", type=int, default=2)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: affinity, capped by OMP_NUM_THREADS")
     return ap.parse_args()
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def _cpu_threads(args):
+    """Host threads for the CPU baseline: --cpu-threads, else this process's CPU affinity
+    capped by OMP_NUM_THREADS (the GPU box grants 16 CPUs per GPU and exports
+    OMP_NUM_THREADS=16, while os.cpu_count() there reports the whole machine)."""
+    if args.cpu_threads:
+        return args.cpu_threads
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return min(n, int(omp)) if omp and omp.isdigit() else n
+
+
 def cpu_baseline(args, L_text):
-    """The oracle (fp32 CPU restatement, oracle/mmbt_ref.py) doing the same train step on host cores."""
+    """The oracle (fp32 CPU restatement, oracle/mmbt_ref.py -- the reference's algorithm,
+    pinned to it by tests/golden) on the host cores: the train step (fwd + bwd + BertAdam,
+    what ``value`` reports), the eval full forward, and the 43-variant robustness pass of
+    eval_mmbt_robustness.py:77-93."""
     from oracle import mmbt_ref as R
     from oracle.bertadam_ref import bertadam_step
     from oracle.weights import FULL, make_state_dict
-    torch.set_num_threads(args.cpu_threads)
+    threads = _cpu_threads(args)
+    torch.set_num_threads(threads)
     sd = make_state_dict(0, FULL)
     params = {}
     for k, v in sd.items():
@@ -92,15 +118,27 @@ def cpu_baseline(args, L_text):
         with torch.no_grad():
             steps = bertadam_step(uniq, [p.grad for p in uniq], ms, vs, steps, 5e-5, [0.01] * len(uniq), 0.1, 1000.0)
 
-    one()  # warm-up
-    t0 = time.perf_counter()
+    def timed(fn, n):
+        fn()  # warm-up
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        return (time.perf_counter() - t0) / n
+
     n = 2
-    for _ in range(n):
-        one()
-    dt = time.perf_counter() - t0
-    return {"value": round(B * n / dt, 4), "unit": "samples/s", "cores": args.cpu_threads, "kind": "port",
+    t_train = timed(one, n)
+    with torch.no_grad():
+        t_eval = timed(lambda: R.forward(sd, txt, mask, mask, img, FULL), n)
+        torch.manual_seed(0)
+        t_rob = timed(lambda: R.robustness(sd, txt[:1], mask[:1], mask[:1], img[:1], FULL, n_repeats=20), 1)
+    return {"value": round(B / t_train, 4), "unit": "samples/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
+            "eval_forward": {"value": round(B / t_eval, 4), "unit": "samples/s"},
+            "robustness_43": {"value": round(1 / t_rob, 4), "unit": "samples/s",
+                              "sample": "1 sample x 43 variants (full, img-only, txt-only, 20+20 controls), "
+                                        "trunk computed once"},
             "sample": f"oracle fp32 train step (fwd+bwd+BertAdam), B={B}, L={L_text + 5}, {n} timed steps after 1 "
-                      f"warm-up, torch CPU {torch.get_num_threads()} threads"}
+                      f"warm-up; eval forward B={B}; torch CPU {torch.get_num_threads()} threads"}
 
 
 def gemm_traffic():
@@ -119,7 +157,7 @@ def gemm_traffic():
 def flava_cpu_baseline(args, L_img, L_txt, B=16):
     """The oracle's fp32 FLAVA train step (oracle/flava_ref.py) on host cores."""
     from oracle import flava_ref as FR
-    torch.set_num_threads(args.cpu_threads)
+    torch.set_num_threads(_cpu_threads(args))
     cfg = FR.FlavaConfig(out_dim=2)
     sd = {k: v.requires_grad_(True) for k, v in FR.make_state_dict(0, cfg).items()}
     img, txt, y = FR.make_inputs(B, L_img, L_txt, 2, 2, 0)
@@ -136,7 +174,7 @@ def flava_cpu_baseline(args, L_img, L_txt, B=16):
     for _ in range(n):
         one()
     dt = time.perf_counter() - t0
-    return {"value": round(B * n / dt, 3), "unit": "samples/s", "cores": args.cpu_threads, "kind": "port",
+    return {"value": round(B * n / dt, 3), "unit": "samples/s", "cores": _cpu_threads(args), "kind": "port",
             "sample": f"oracle fp32 FLAVA train step (fwd+bwd+AdamW), B={B}, L={L_img}+{L_txt}, {n} timed steps "
                       f"after 1 warm-up, torch CPU {torch.get_num_threads()} threads"}
 
@@ -231,7 +269,7 @@ def uncertainty_cpu_baseline(args, L_text, B=2, passes=2):
     ResNet features computed once (as the HIP path does), ``passes`` dropout passes."""
     from oracle import mmbt_ref as R
     from oracle.weights import FULL, make_state_dict
-    torch.set_num_threads(args.cpu_threads)
+    torch.set_num_threads(_cpu_threads(args))
     sd = make_state_dict(0, FULL)
     g = torch.Generator().manual_seed(0)
     txt = torch.randint(1000, 30522, (B, L_text), generator=g)
@@ -247,7 +285,7 @@ def uncertainty_cpu_baseline(args, L_text, B=2, passes=2):
         t2 = time.perf_counter()
     # one evaluated sample = K ResNet trunks + K x T MC-dropout encoder passes
     per_sample = (args.members * (t1 - t0) + args.members * args.mc_samples * (t2 - t1) / passes) / B
-    return {"value": round(1.0 / per_sample, 5), "unit": "samples/s", "cores": args.cpu_threads, "kind": "port",
+    return {"value": round(1.0 / per_sample, 5), "unit": "samples/s", "cores": _cpu_threads(args), "kind": "port",
             "sample": f"oracle fp32 eval: 1 member, ResNet once + {passes} MC-dropout encoder passes, B={B}, "
                       f"L={L_text + 5}, timed and scaled to K={args.members} trunks + K x T={args.mc_samples} "
                       f"encoder passes per sample, torch CPU {torch.get_num_threads()} threads"}
