@@ -3,12 +3,11 @@
 One step = one optimizer step of the reference train loop over a synthetic Food-101
 batch (src/framework.py:276-319 with accum = 1, freeze epochs over, every one of the
 169.3 M parameters trainable): ResNet-152 + 12 fused BERT layers forward, CE loss,
-backward, (N>1: RCCL gradient all-reduce), fused BertAdam.  Each rank trains on a batch of
-256 (224x224 image, 508 word-pieces -> 513 tokens) -- the metric's bs=256, which in the
-reference is the per-process DataLoader batch (train.py:41,238) -- so per-GPU work is fixed
-as N grows ("scaling": "weak") and every rank's ResNet BatchNorm normalises over the same
-256 samples as the reference's single process does.  --global-batch G instead splits G
-samples over the N ranks ("scaling": "strong"; DESIGN.md §6 has both measured).
+backward, (N>1: RCCL gradient all-reduce), fused BertAdam.  The global batch is the metric's
+bs = 256 (224x224 image, 508 word-pieces -> 513 tokens), split evenly over the N ranks
+(BASELINE config 4 / SURVEY §8d: "bs=256 global, 32 per GPU at 8 GPUs"): total work is fixed
+as N grows, "scaling": "strong".  --per-rank-batch B (without --global-batch) keeps B samples
+per rank instead ("scaling": "weak"; DESIGN.md §6 has both).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -45,9 +44,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--per-rank-batch", type=int, default=256, help="samples per rank per step (weak scaling)")
     ap.add_argument("--global-batch", type=int, default=None,
-                    help="split this many samples over the ranks instead (strong scaling)")
+                    help="samples per step split over the ranks (strong scaling; default 256)")
+    ap.add_argument("--per-rank-batch", type=int, default=None,
+                    help="samples per rank per step instead (weak scaling)")
     ap.add_argument("--text-len", type=int, default=508, help="word-pieces per sample (L = 5 + this)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", default="mmbt", choices=["mmbt", "flava", "uncertainty"])
@@ -398,10 +398,12 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    if args.global_batch is None:
+    if args.global_batch is None and args.per_rank_batch is not None:
         args.global_batch = args.per_rank_batch * world
         scaling = "weak"
     else:
+        if args.global_batch is None:
+            args.global_batch = 256
         if args.global_batch % world:
             raise SystemExit("global batch must divide evenly over ranks")
         scaling = "strong"

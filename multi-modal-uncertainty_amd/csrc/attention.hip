@@ -50,6 +50,12 @@ static __device__ __forceinline__ float max3f(float a, float b, float c) {
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
+// (m & a) | (~m & b) as ONE v_bfi_b32 (hipcc otherwise rebuilds ~m & b from a sign test)
+static __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
 static __host__ __device__ __forceinline__ uint32_t drop_thr(float p) { return (uint32_t)(p * 65536.0f + 0.5f); }
 
 static __device__ __forceinline__ int fsw(int r) { return (((r >> 1) & 1) << 2) | ((r >> 3) & 3); }
@@ -111,6 +117,18 @@ static __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// (query / key block, batch-head) of this workgroup.  The grid is (blocks per head-row,
+// B * heads); the dispatcher deals workgroups to the 8 XCDs round-robin by linear id, so
+// without a remap the blocks of one head-row (which all stream the same K / V, or Q / dO,
+// rows) land on different XCDs and each XCD's L2 fetches them again.  xcd_remap gives each
+// XCD a contiguous range of linear work ids: the blocks of a head-row share one L2.
+static __device__ __forceinline__ void block_coords(int& bx, int& bh) {
+  const int gx = gridDim.x;
+  const int wid = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gridDim.y);
+  bh = wid / gx;
+  bx = wid - bh * gx;
+}
+
 // ---------------------------------------------------------------- forward ring geometry
 constexpr int FWD_NS = 2;                      // K/V ring depth (tiles)
 constexpr int FWD_TILE = 64 * 128;             // 64 keys x 64 d bf16
@@ -137,8 +155,21 @@ constexpr int FWD_MAX_NKV = 9;                 // L <= 576 (BERT: 512 text + ima
 //  * O leaves through LDS as 16-B row stores.
 // Needs ceil(L/64) <= FWD_MAX_NKV and ld_out % 8 == 0.
 constexpr float DEFER_LOG2 = 8.0f;
-__constant__ uint32_t kDropMul[8] = {0x9E3779B1u, 0x85EBCA77u, 0xC2B2AE3Du, 0x27D4EB2Fu,
-                                     0x165667B1u, 0xD3A2646Du, 0xFD7046C5u, 0xB55A4F09u};
+// 24-bit odd multipliers of the per-pair draws (v_mul_u32_u24: full rate; the 32-bit
+// v_mul_lo_u32 of the earlier draws is a quarter-rate op, 20 of them per tile)
+constexpr uint32_t kDropMul24[8] = {0x9E3779u, 0x85EBCBu, 0xC2B2AFu, 0xA7D4EBu,
+                                    0x965667u, 0xD3A265u, 0xFD7047u, 0xB55A4Fu};
+
+// 32 bits of pair i's two 16-bit draws from the block hash hb: rotate hb by 4i (so every
+// pair multiplies a different 24-bit window), 24-bit multiply, fold the high half into
+// the low one.  Measured over 2^22 random hb: per-key drop rates 0.1 +- 3e-4, the 120
+// pairwise correlations of the 16 decisions within noise (max |r| 1.4e-3 vs 1/sqrt(N) =
+// 4.9e-4), joint drop counts binomial (tools/dropout_draws.py).
+static __device__ __forceinline__ uint32_t pair_draw(uint32_t hb, int i) {
+  const uint32_t src = i ? __builtin_amdgcn_alignbit(hb, hb, 4 * i) : hb;  // rotr(hb, 4i)
+  const uint32_t x = __umul24(src, kDropMul24[i]);
+  return x ^ (x >> 16);
+}
 
 static __device__ __forceinline__ int kperm(int i) {  // LDS row i of a 32-key half -> key
   return (((i >> 2) & 1) << 4) | (((i >> 3) & 3) << 2) | (i & 3);
@@ -148,27 +179,29 @@ static __device__ __forceinline__ int kperm(int i) {  // LDS row i of a 32-key h
 // zero the dropped P values and shift the two keep bits into w (odd key first, so that a
 // descending walk leaves bit k of w = element k)
 // the same decisions without the keep bits (inference: no backward reads them)
-static __device__ __forceinline__ void drop_pair_zero(uint32_t hsh, uint32_t thr, uint32_t thr_hi, float& e0,
-                                                      float& e1) {
+static __device__ __forceinline__ void drop_pair_zero(uint32_t hsh, uint32_t thr, uint32_t thr_hi, float e0,
+                                                      float e1, float& o0, float& o1) {
   asm("v_cmp_le_u32 vcc, %[th], %[h]\n\t"
-      "v_cndmask_b32 %[d1], 0, %[d1], vcc\n\t"
+      "v_cndmask_b32 %[o1], 0, %[e1], vcc\n\t"
       "v_cmp_le_u16 vcc, %[t], %[h]\n\t"
-      "v_cndmask_b32 %[d0], 0, %[d0], vcc"
-      : [d0] "+v"(e0), [d1] "+v"(e1)
-      : [h] "v"(hsh), [t] "s"(thr), [th] "s"(thr_hi)
+      "v_cndmask_b32 %[o0], 0, %[e0], vcc"
+      : [o0] "=&v"(o0), [o1] "=&v"(o1)
+      : [e0] "v"(e0), [e1] "v"(e1), [h] "v"(hsh), [t] "s"(thr), [th] "s"(thr_hi)
       : "vcc");
 }
 
-static __device__ __forceinline__ void drop_pair_apply(uint32_t hsh, uint32_t thr, uint32_t thr_hi, float& e0,
-                                                       float& e1, uint32_t& w) {
+// the kept values go to fresh registers (o0, o1): the undropped e0 / e1 stay live for the
+// row sum without the copies an in-place ("+v") operand costs (32 v_mov per tile)
+static __device__ __forceinline__ void drop_pair_apply(uint32_t hsh, uint32_t thr, uint32_t thr_hi, float e0,
+                                                       float e1, float& o0, float& o1, uint32_t& w) {
   asm("v_cmp_le_u32 vcc, %[th], %[h]\n\t"
-      "v_cndmask_b32 %[d1], 0, %[d1], vcc\n\t"
+      "v_cndmask_b32 %[o1], 0, %[e1], vcc\n\t"
       "v_addc_co_u32 %[w], vcc, %[w], %[w], vcc\n\t"
       "v_cmp_le_u16 vcc, %[t], %[h]\n\t"
-      "v_cndmask_b32 %[d0], 0, %[d0], vcc\n\t"
+      "v_cndmask_b32 %[o0], 0, %[e0], vcc\n\t"
       "v_addc_co_u32 %[w], vcc, %[w], %[w], vcc"
-      : [d0] "+v"(e0), [d1] "+v"(e1), [w] "+v"(w)
-      : [h] "v"(hsh), [t] "s"(thr), [th] "s"(thr_hi)
+      : [o0] "=&v"(o0), [o1] "=&v"(o1), [w] "+v"(w)
+      : [e0] "v"(e0), [e1] "v"(e1), [h] "v"(hsh), [t] "s"(thr), [th] "s"(thr_hi)
       : "vcc");
 }
 
@@ -180,9 +213,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   uint64_t* kbuf_all = (uint64_t*)(smem + FWD_NS * FWD_STAGE);
   const int t = threadIdx.x, l = t & 63, l_ = l, h = l >> 5;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int bh = blockIdx.y, b = bh / p.heads, hd = bh - b * p.heads;
+  int bx, bh;
+  block_coords(bx, bh);
+  const int b = bh / p.heads, hd = bh - b * p.heads;
   const int L = p.L, HD = p.heads * 64;
-  const int q0w = blockIdx.x * 128 + 32 * w, q = q0w + (l & 31);
+  const int q0w = bx * 128 + 32 * w, q = q0w + (l & 31);
   const bool wave_live = q0w < L;
   const bf16* base = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64;
   const uint32_t thr = drop_thr(p.drop_p), thr_hi = thr << 16;
@@ -203,7 +238,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   f32x16 o[2];
 #pragma unroll
   for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
-  float m_run = NEG_INF, nml = 0.f, l_run = 0.f;  // nml = -m_run * log2e
+  float m_run = NEG_INF, nml = 0.f;  // nml = -m_run * log2e
+  f32x2 lsum[2] = {{0.f, 0.f}, {0.f, 0.f}};  // row-sum partials (packed pairs)
 
   // per tile: waves 0,1 -> K pieces, waves 2,3 -> V pieces (4 each, rows in kperm order);
   // wave 0 also the (unpermuted) mask row
@@ -279,7 +315,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     if (__builtin_amdgcn_ballot_w64(upd)) {
       const float mnew = upd ? mx : m_run;
       const float alpha = upd ? __builtin_amdgcn_exp2f((m_run - mnew) * LOG2E) : 1.0f;  // exp2(-inf) = 0
-      l_run *= alpha;
+      const f32x2 a2 = {alpha, alpha};
+      lsum[0] *= a2;
+      lsum[1] *= a2;
 #pragma unroll
       for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
       m_run = mnew;
@@ -293,27 +331,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       if (s2 == 1 && !two) break;
+      // exponent arguments and the row sum as packed f32 pairs (v_pk_fma_f32 / v_pk_add_f32:
+      // half the VALU instructions of the scalar forms), two partial sums per half-wave
+      const f32x2 nml2 = {nml, nml}, lg2 = {LOG2E, LOG2E};
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float e = __builtin_amdgcn_exp2f(fmaf(sc[s2][r], LOG2E, nml));
-        sc[s2][r] = e;
-        l_run += e;
+      for (int i = 0; i < 8; ++i) {
+        const f32x2 x = f32x2{sc[s2][2 * i], sc[s2][2 * i + 1]} * lg2 + nml2;
+        const f32x2 e = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+        sc[s2][2 * i] = e.x;
+        sc[s2][2 * i + 1] = e.y;
+        lsum[i & 1] += e;
       }
       if (DROP) {
-        // one full hash per (row, tile, half, half-wave); its 8 pairs' 32-bit draws are
-        // hb * C_i folded by x ^ (x >> 16) (2 VALU per pair instead of a 7-VALU hash; the
-        // 16 decisions measured pairwise-uncorrelated to 2e-3 over 2^21 draws, joint
-        // drop counts binomial)
+        // one full hash per (row, tile, half, half-wave); its 8 pairs' 32-bit draws come
+        // from pair_draw (3 full-rate VALU per pair instead of a 7-VALU hash)
         const uint32_t hb = lowbias32(c0 + (uint32_t)s2);
 #pragma unroll
         for (int i = 7; i >= 0; --i) {
-          uint32_t hsh = hb * kDropMul[i];
-          hsh ^= hsh >> 16;
-          float e0 = sc[s2][2 * i], e1 = sc[s2][2 * i + 1];
-          if (STORE) drop_pair_apply(hsh, thr, thr_hi, e0, e1, wb[s2]);
-          else drop_pair_zero(hsh, thr, thr_hi, e0, e1);
-          sc[s2][2 * i] = e0;
-          sc[s2][2 * i + 1] = e1;
+          const uint32_t hsh = pair_draw(hb, i);
+          float o0, o1;
+          if (STORE) drop_pair_apply(hsh, thr, thr_hi, sc[s2][2 * i], sc[s2][2 * i + 1], o0, o1, wb[s2]);
+          else drop_pair_zero(hsh, thr, thr_hi, sc[s2][2 * i], sc[s2][2 * i + 1], o0, o1);
+          sc[s2][2 * i] = o0;
+          sc[s2][2 * i + 1] = o1;
         }
       }
 #pragma unroll
@@ -334,15 +374,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   for (int j = 0; j < FWD_NS - 1 && j < nkv; ++j) issue(j);
-  for (int j = 0; j < nkv; ++j) {
+  // full tiles in the loop, the partial last tile (if any) peeled after it: one tile body
+  // per loop keeps the O / row-sum registers in place across iterations (a full / partial
+  // select inside the loop made hipcc shuffle them with ~18 v_mov_b64 per tile)
+  const int nfull = L / 64;
+  auto step = [&](int j) {
     const int ahead = nkv - 1 - j < FWD_NS - 2 ? nkv - 1 - j : FWD_NS - 2;
     wait_for(ahead);
     raw_barrier();
     if (j + FWD_NS - 1 < nkv) issue(j + FWD_NS - 1);
-    if (wave_live) {
-      if (64 * (j + 1) > L) tile(j, std::integral_constant<bool, true>{});
-      else tile(j, std::integral_constant<bool, false>{});
-    }
+  };
+  for (int j = 0; j < nfull; ++j) {
+    step(j);
+    if (wave_live) tile(j, std::integral_constant<bool, false>{});
+  }
+  if (nfull < nkv) {
+    step(nfull);
+    if (wave_live) tile(nfull, std::integral_constant<bool, true>{});
   }
   raw_barrier();  // every wave is done with the ring: it becomes the O staging area
   if (!wave_live) return;
@@ -351,8 +399,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const int rows = L - q0w < 32 ? L - q0w : 32;
     for (int i = l; i < rows * nkv; i += 64) dst[i] = kbuf[i];
   }
-  const float lsum = l_run + __shfl_xor(l_run, 32, 64);
-  const float inv = (DROP ? 1.0f / (1.0f - p.drop_p) : 1.0f) / lsum;
+  const float l_run = (lsum[0].x + lsum[0].y) + (lsum[1].x + lsum[1].y);
+  const float lsum_row = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = (DROP ? 1.0f / (1.0f - p.drop_p) : 1.0f) / lsum_row;
   // O rows through LDS: [32 rows][128 B] per wave, 16-B chunk c of row r at c ^ (r & 7)
   char* os = smem + w * 4096;
   const int qr = l & 31;
@@ -364,7 +413,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                         f2bf(o[dt][4 * g + 3] * inv)};
       *(bf16x4*)(os + qr * 128 + (((4 * dt + g) ^ (qr & 7)) << 4) + 8 * h) = v;
     }
-  if (h == 0 && q < L) p.lse[(int64_t)bh * L + q] = m_run + logf(lsum);
+  if (h == 0 && q < L) p.lse[(int64_t)bh * L + q] = m_run + logf(lsum_row);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS rows are written (wave-private)
   bf16* ob = p.out + hd * 64;
 #pragma unroll
@@ -400,7 +449,7 @@ void attention_fwd_launch(const AttnParams& p, hipStream_t s) {
 // (no __syncthreads: it would drain the DMA queue).
 constexpr int DK_NS = 4;                                   // ring depth
 constexpr int DK_TILE = 32 * 128;                          // 32 rows x 64 d bf16
-constexpr int DK_ROWS = 32 * 4 + 32 * 4 + 32 * 8;          // -lse (as lse), delta, keep words
+constexpr int DK_ROWS = 32 * 4 + 32 * 4 + 32 * 8;          // -lse (as lse), -delta, keep words
 constexpr int DK_STAGE = 2 * DK_TILE + DK_ROWS;            // 8704 B
 
 
@@ -411,13 +460,16 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
   __shared__ __attribute__((aligned(16))) char smem[DK_NS * DK_STAGE];
   const int t = threadIdx.x, l = t & 63, h = l >> 5;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int bh = blockIdx.y, b = bh / p.heads, hd = bh - b * p.heads;
+  int bx, bh;
+  block_coords(bx, bh);
+  const int b = bh / p.heads, hd = bh - b * p.heads;
   const int L = p.L, HD = p.heads * 64;
-  const int k0w = blockIdx.x * 64 + 32 * w, key = k0w + (l & 31);
+  const int k0w = bx * 64 + 32 * w, key = k0w + (l & 31);
   const bool wave_live = k0w < L, kv = key < L;
   const bool drop = DROP;
   const float zs = drop ? 1.0f / (1.0f - p.drop_p) : 1.0f;
-  const uint32_t lanebit = 1u << (l & 31);
+  const float izs = drop ? 1.0f - p.drop_p : 1.0f;
+  const int lane31 = l & 31;
   const int nkv = (L + 63) / 64;
   const float mkey = kv ? p.keymask[(int64_t)b * L + key] * LOG2E : NEG_INF;
   const bf16* base = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64;
@@ -464,7 +516,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
         dma16(rdo, st + DK_TILE + pc * 1024, (uint32_t)(((q0 + row) * p.ld_do + hd * 64 + 8 * c) * 2));
       }
       // keep word of query row q0 + l/2 for this key block: 4 B per lane (low / high half)
-      dma4(rk, st + 2 * DK_TILE + 256, (uint32_t)((((q0 + (l >> 1)) * nkv + blockIdx.x) * 8) + 4 * (l & 1)));
+      dma4(rk, st + 2 * DK_TILE + 256, (uint32_t)((((q0 + (l >> 1)) * nkv + bx) * 8) + 4 * (l & 1)));
     }
   };
   // vmcnt: this wave's DMAs per tile (6 or 5) times the tiles allowed to stay in flight
@@ -496,19 +548,27 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
     if (wave_live) {
       // row constants of the 16 query rows a lane's registers hold: r -> row (r&3) + 8(r>>2) + 4h,
       // i.e. four runs of 4 consecutive rows -> 16-B LDS reads (keep words: stride-2 pairs)
-      f32x4 nl4[4], dl4[4];
+      f32x4 nl4[4], nd4[4];  // -lse, -delta of the 16 rows
       uint32_t kwr[16];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         nl4[j] = -*(const f32x4*)(lse + 8 * j + 4 * h);
-        dl4[j] = *(const f32x4*)(dlt + 8 * j + 4 * h);
+        nd4[j] = *(const f32x4*)(dlt + 8 * j + 4 * h);
         if (DROP)
 #pragma unroll
           for (int i = 0; i < 4; ++i) kwr[4 * j + i] = kbit[2 * (8 * j + 4 * h + i)];
       }
-      f32x16 sc, dp;  // S starts at -lse of its query row (row constant as initial accumulator)
+      // S starts at -lse of its query row, dP at -delta / zs (row constants as initial
+      // accumulators): then dS = p (keep ? dp zs : -delta) and dropped-P = keep ? p zs : 0,
+      // the keep bit as an all-ones / zero mask (v_bfe_i32 of the row's keep word at this
+      // lane's key) bit-selecting between the two; products as packed pairs
+      const f32x2 lg2 = {LOG2E, LOG2E}, mk2 = {mkey, mkey}, zs2 = {zs, zs};
+      f32x16 sc, dp;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { sc[r] = nl4[r >> 2][r & 3]; dp[r] = 0.f; }
+      for (int r = 0; r < 16; ++r) {
+        sc[r] = nl4[r >> 2][r & 3];
+        dp[r] = nd4[r >> 2][r & 3] * izs;
+      }
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Qs, 0, ks, l), kf[ks], sc, 0, 0, 0);
@@ -516,16 +576,28 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
       }
       f32x16 pz;  // dropped P (for dV)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float pr = __builtin_amdgcn_exp2f(fmaf(sc[r], LOG2E, mkey));
-        const float dl = dl4[r >> 2][r & 3];
+      for (int i = 0; i < 8; ++i) {
+        const f32x2 x = f32x2{sc[2 * i], sc[2 * i + 1]} * lg2 + mk2;
+        const f32x2 pr = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
         if (DROP) {
-          const float z = (kwr[r] & lanebit) ? zs : 0.f;
-          pz[r] = pr * z;
-          sc[r] = pr * fmaf(dp[r], z, -dl);  // dS
+          const f32x2 pzs = pr * zs2, y = f32x2{dp[2 * i], dp[2 * i + 1]} * zs2;
+          f32x2 v;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int r = 2 * i + e;
+            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)kwr[r], lane31, 1);
+            pz[r] = __uint_as_float(m & __float_as_uint(pzs[e]));
+            v[e] = __uint_as_float(bfi(m, __float_as_uint(y[e]), __float_as_uint(nd4[r >> 2][r & 3])));
+          }
+          const f32x2 d = pr * v;
+          sc[2 * i] = d.x;
+          sc[2 * i + 1] = d.y;
         } else {
-          pz[r] = pr;
-          sc[r] = pr * (dp[r] - dl);
+          pz[2 * i] = pr.x;
+          pz[2 * i + 1] = pr.y;
+          const f32x2 d = pr * f32x2{dp[2 * i], dp[2 * i + 1]};
+          sc[2 * i] = d.x;
+          sc[2 * i + 1] = d.y;
         }
       }
 #pragma unroll
@@ -563,7 +635,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
     if (t < 128) {
       const int nqb = (L + 127) / 128, nkb = (L + 63) / 64, B = p.batch;
       const float v = red[t] + red[128 + t];
-      const int64_t row = (int64_t)nqb * B + (t < 64 ? 0 : (int64_t)nkb * B) + (int64_t)blockIdx.x * B + b;
+      const int64_t row = (int64_t)nqb * B + (t < 64 ? 0 : (int64_t)nkb * B) + (int64_t)bx * B + b;
       p.colsum[row * HD + hd * 64 + (t & 63)] = v;
     }
   }
@@ -595,9 +667,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   __shared__ __attribute__((aligned(16))) char smem[DQ_NS * DQ_STAGE];
   const int t = threadIdx.x, l = t & 63, h = l >> 5;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int bh = blockIdx.y, b = bh / p.heads, hd = bh - b * p.heads;
+  int bx, bh;
+  block_coords(bx, bh);
+  const int b = bh / p.heads, hd = bh - b * p.heads;
   const int L = p.L, HD = p.heads * 64;
-  const int q0w = blockIdx.x * 128 + 32 * w, q = q0w + (l & 31);
+  const int q0w = bx * 128 + 32 * w, q = q0w + (l & 31);
   const bool wave_live = q0w < L, qv = q < L;
   const bool drop = drop_thr(p.drop_p) != 0;
   const float zs = drop ? 1.0f / (1.0f - p.drop_p) : 1.0f;
@@ -632,11 +706,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
       for (int e = 0; e < 8; ++e) dsum = fmaf(bf2f(ov[e]), bf2f(df[ks][e]), dsum);
     }
     dsum += __shfl_xor(dsum, 32, 64);
-    if (qv && h == 0) p.delta[(int64_t)bh * L + q] = dsum;
+    if (qv && h == 0) p.delta[(int64_t)bh * L + q] = -dsum;  // stored negated: dK/dV uses -delta
   }
   const float nlse = qv ? -p.lse[(int64_t)bh * L + q] : -__builtin_huge_valf();
   const float dlt = dsum;
   const float ndz = -dlt / zs;
+  const uint32_t ndl_bits = __float_as_uint(-dlt);
+  const f32x2 lg2 = {LOG2E, LOG2E}, zs2 = {zs, zs};
   f32x16 dq[2];
 #pragma unroll
   for (int i = 0; i < 16; ++i) { dq[0][i] = 0.f; dq[1][i] = 0.f; }
@@ -685,20 +761,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
 #pragma unroll
       for (int st2 = 0; st2 < 2; ++st2) {
         const uint32_t kw32 = (uint32_t)(kwh >> (32 * st2));
+        // S starts at -lse + mask: register r holds key kl = 32 st2 + 8 (r >> 2) + 4 h + (r & 3),
+        // so each group of 4 registers takes 4 contiguous mask entries (one f32x4 read)
         f32x16 sc, dp;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) { sc[i] = nlse; dp[i] = ndz; }
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 mv = *(const f32x4*)(mk + 32 * st2 + 8 * g + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            sc[4 * g + e] = nlse + mv[e];
+            dp[4 * g + e] = ndz;
+          }
+        }
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ks, 32 * st2, ks, l), qf[ks], sc, 0, 0, 0);
           dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Vs, 32 * st2, ks, l), df[ks], dp, 0, 0, 0);
         }
+        // p = exp2(log2e S');  dS^T = p * (keep ? dP zs - delta : -delta).  dp started at
+        // -delta / zs, so dp zs = dP zs - delta; the keep bit becomes an all-ones / zero mask
+        // (v_bfe_i32) that bit-selects it against -delta (without dropout kw is all ones).
+        // Products as packed pairs.
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int kc = (r & 3) + 8 * (r >> 2), kl = 32 * st2 + kc + 4 * h;
-          const float pr = __builtin_amdgcn_exp2f((sc[r] + mk[kl]) * LOG2E);
-          const float v = (kw32 & (1u << kc)) ? dp[r] * zs : -dlt;
-          sc[r] = pr * v;  // dS^T
+        for (int i = 0; i < 8; ++i) {
+          const f32x2 x = f32x2{sc[2 * i], sc[2 * i + 1]} * lg2;
+          const f32x2 pr = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+          const f32x2 y = f32x2{dp[2 * i], dp[2 * i + 1]} * zs2;
+          f32x2 v;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int r = 2 * i + e, kc = (r & 3) + 8 * (r >> 2);
+            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)kw32, kc, 1);
+            v[e] = __uint_as_float(bfi(m, __float_as_uint(y[e]), ndl_bits));
+          }
+          const f32x2 d = pr * v;
+          sc[2 * i] = d.x;
+          sc[2 * i + 1] = d.y;
         }
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
@@ -727,7 +825,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     if (t < 64) {
       float v = 0.f;
       for (int r = 0; r < 128; ++r) v += rows[r * 64 + t];
-      p.colsum[((int64_t)blockIdx.x * p.batch + b) * HD + hd * 64 + t] = v;
+      p.colsum[((int64_t)bx * p.batch + b) * HD + hd * 64 + t] = v;
     }
   }
   if (!qv) return;
