@@ -610,7 +610,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
         }
       }
     }
-  }
+    }
   if (p.colsum) {  // bias-gradient partials of K and V: this block's 64 keys, per column
     // each lane holds ONE column (32 dt + l&31) for 16 keys: in-lane sum + the other half-wave
     float* red = (float*)smem;  // [2 waves][K 64 | V 64]
@@ -659,7 +659,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
 // buffer_load...lds into a 3-deep ring, issued 2 tiles ahead, one raw barrier per tile.
 // Keys past L read as zero K / V rows and mask 0: their P is finite but multiplies zero K
 // rows (dQ += dS K) and zero V rows (dP), so they add nothing.
-constexpr int DQ_NS = 3;
+constexpr int DQ_NS = 3;  // (the main loop below is unrolled by exactly 3)
 constexpr int DQ_TILE = 64 * 128;                         // 64 keys x 64 d bf16
 constexpr int DQ_STAGE = 2 * DQ_TILE + 256 + 4 * 256;     // K, V, mask row, 4 waves x 32 keep words
 
@@ -744,12 +744,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   };
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   for (int j = 0; j < DQ_NS - 1 && j < nkv; ++j) issue(j);
-  for (int j = 0; j < nkv; ++j) {
+  // the loop is unrolled by the ring depth so each tile's stage is a compile-time constant
+  // and folds into the ds_read immediate offsets (a runtime (j % 3) * stage base cost ~37
+  // address VALU per tile)
+  auto tile_step = [&](int j, auto sg_tag) {
+    constexpr int SG = decltype(sg_tag)::value;
     const int ahead = nkv - 1 - j < DQ_NS - 2 ? nkv - 1 - j : DQ_NS - 2;
     wait_for(ahead);
     raw_barrier();
     if (j + DQ_NS - 1 < nkv) issue(j + DQ_NS - 1);
-    const char* st = smem + (j % DQ_NS) * DQ_STAGE;
+    const char* st = smem + SG * DQ_STAGE;  // compile-time stage: constant LDS offsets
     const char* Ks = st;
     const char* Vs = st + DQ_TILE;
     const float* mk = (const float*)(st + 2 * DQ_TILE);
@@ -808,6 +812,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
         }
       }
     }
+    };
+  for (int j0 = 0; j0 < nkv; j0 += DQ_NS) {
+    tile_step(j0, std::integral_constant<int, 0>{});
+    if (j0 + 1 < nkv) tile_step(j0 + 1, std::integral_constant<int, 1>{});
+    if (j0 + 2 < nkv) tile_step(j0 + 2, std::integral_constant<int, 2>{});
   }
   if (p.colsum) {  // bias-gradient partials of Q: this block's 128 queries, per column
     // lane (query l&31) holds columns 32 dt + 8 g + 4 h + e: rows to LDS, then column sums
