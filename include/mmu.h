@@ -73,6 +73,15 @@ typedef struct mmu_epilogue {
                                order, so results stay deterministic.
                                Stream-ordered: one workspace per stream.                */
   int64_t workspace_floats;
+  /* BIAS_DROP_RES into an f32 C only (optional, all four or none): the f32 residual is the
+     LayerNorm OUTPUT recomputed from its f32 input, residual[m][n] =
+     (r[m][n] - res_ln_mean[m]) * res_ln_rstd[m] * res_ln_w[n] + res_ln_b[n], with r the
+     `residual` rows -- the encoder passes the previous LayerNorm's input (kept for its
+     backward anyway) instead of materialising its f32 output.                          */
+  const float* res_ln_mean;
+  const float* res_ln_rstd;
+  const float* res_ln_w;
+  const float* res_ln_b;
 } mmu_epilogue;
 
 int mmu_gemm(const void* A, int64_t lda, int a_kmajor,

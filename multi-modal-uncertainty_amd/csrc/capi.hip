@@ -129,6 +129,8 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
     p.aux = epi->aux; p.ldx = epi->ldx; p.aux_bstride = epi->aux_bstride;
     p.colsum = epi->colsum; p.colsum_bstride = epi->colsum_bstride;
     p.drop_p = epi->drop_p; p.seed = epi->seed;
+    p.res_ln_mean = epi->res_ln_mean; p.res_ln_rstd = epi->res_ln_rstd;
+    p.res_ln_w = epi->res_ln_w; p.res_ln_b = epi->res_ln_b;
   }
   p.kind = kind;
   if (kind < 0 || kind > MMU_EPI_BIAS_DROP_QGELU) return fail("mmu_gemm: bad epilogue kind %d", kind);
@@ -136,6 +138,11 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
     return fail("mmu_gemm: fused epilogues other than BIAS_DROP_RES write bf16");
   if (kind == MMU_EPI_BIAS_DROP_RES && c_dtype == MMU_F32 && (ldc % 4 || (epi && epi->ldr % 4)))
     return fail("mmu_gemm: f32 hidden-stream epilogue needs 16-B aligned rows");
+  {
+    const int nln = !!p.res_ln_mean + !!p.res_ln_rstd + !!p.res_ln_w + !!p.res_ln_b;
+    if (nln && (nln != 4 || kind != MMU_EPI_BIAS_DROP_RES || c_dtype != MMU_F32))
+      return fail("mmu_gemm: res_ln_* (all four) only with BIAS_DROP_RES into an f32 C");
+  }
   if (kind == MMU_EPI_DGELU && !p.aux) return fail("mmu_gemm: DGELU epilogue needs aux");
   if ((kind == MMU_EPI_BIAS_DROP_RES || kind == MMU_EPI_ADD_RES) && !p.residual)
     return fail("mmu_gemm: epilogue needs residual");

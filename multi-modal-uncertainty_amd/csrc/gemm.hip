@@ -207,18 +207,37 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
   const bf16* src = EPI == MMU_EPI_DGELU ? (const bf16*)aux : res;
   const float* src32 = RES32 && p.residual ? (const float*)p.residual + z * p.res_bstride : nullptr;
   const int64_t lds_ = EPI == MMU_EPI_DGELU ? p.ldx : p.ldr;
+  // residual = LN(residual rows): per-column gamma / beta here, per-row mean / rstd per pass
+  const bool res_ln = RES32 && p.res_ln_w != nullptr && !slab;
+  float lw[8], lb[8];
+  if (RES32) {
+    float4 w0 = make_float4(1.f, 1.f, 1.f, 1.f), w1 = w0, b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
+    if (res_ln) {
+      w0 = *(const float4*)(p.res_ln_w + n); w1 = *(const float4*)(p.res_ln_w + n + 4);
+      b0 = *(const float4*)(p.res_ln_b + n); b1 = *(const float4*)(p.res_ln_b + n + 4);
+    }
+    lw[0] = w0.x; lw[1] = w0.y; lw[2] = w0.z; lw[3] = w0.w; lw[4] = w1.x; lw[5] = w1.y; lw[6] = w1.z; lw[7] = w1.w;
+    lb[0] = b0.x; lb[1] = b0.y; lb[2] = b0.z; lb[3] = b0.w; lb[4] = b1.x; lb[5] = b1.y; lb[6] = b1.z; lb[7] = b1.w;
+  }
 #pragma unroll
   for (int pass = 0; pass < NJ / PJ; ++pass) {
     // the pass's residual / aux rows are requested up front: one memory latency per pass
     bf16x8 in[RES32 ? 1 : 2 * PJ];
     float4 in32[RES32 ? 2 * PJ : 1][2];
+    float rmu[RES32 ? 2 * PJ : 1], rrs[RES32 ? 2 * PJ : 1];
 #pragma unroll
     for (int it = 0; it < 2 * PJ; ++it) {
       const int64_t m = mw + 16 * PJ * pass + rr + 8 * it;
       if (RES32) {
+        rmu[it] = 0.f;
+        rrs[it] = 1.f;
         if (!slab && m < p.M) {
           in32[it][0] = *(const float4*)(src32 + m * lds_ + n);
           in32[it][1] = *(const float4*)(src32 + m * lds_ + n + 4);
+          if (res_ln) {
+            rmu[it] = p.res_ln_mean[z * p.M + m];
+            rrs[it] = p.res_ln_rstd[z * p.M + m];
+          }
         } else {
           in32[it][0] = in32[it][1] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
@@ -256,6 +275,10 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
       if (RES32) {
         inf[0] = in32[it][0].x; inf[1] = in32[it][0].y; inf[2] = in32[it][0].z; inf[3] = in32[it][0].w;
         inf[4] = in32[it][1].x; inf[5] = in32[it][1].y; inf[6] = in32[it][1].z; inf[7] = in32[it][1].w;
+        if (res_ln) {  // the LayerNorm output, as mmu_layernorm_fwd_f32 computes it
+#pragma unroll
+          for (int e = 0; e < 8; ++e) inf[e] = fmaf((inf[e] - rmu[it]) * rrs[it], lw[e], lb[e]);
+        }
       } else {
 #pragma unroll
         for (int r = 0; r < 8; ++r) inf[r] = LOADS ? bf2f(in[RES32 ? 0 : it][r]) : 0.f;

@@ -27,6 +27,8 @@ struct GemmParams {
   int64_t colsum_bstride;
   float drop_p;
   uint64_t seed;
+  // f32 residual = LN(residual rows) recomputed per element (mmu_epilogue res_ln_*)
+  const float *res_ln_mean, *res_ln_rstd, *res_ln_w, *res_ln_b;
   // split-K (EPI_STORE, f32 C, no bias/colsum): grid.y slices of kchunk, slabs in ws
   int splitk;
   int64_t kchunk;

@@ -5,13 +5,16 @@ called through ``self.encoder(...)`` at src/mmbt.py:124-126).
 Forward per layer (M = B*L token rows, bf16 GEMM operands, f32 accumulation):
   qkv = X Wqkv^T + bqkv                       mmu_gemm  (fused Q|K|V, [M, 2304])
   O, lse = attention(qkv, keymask)            mmu_attention_fwd (dropout on P)
-  S1 = X32 + dropout(O Wo^T + bo)             mmu_gemm  EPI_BIAS_DROP_RES, f32 residual + f32 out
-  A, A32 = LN1(S1)                            mmu_layernorm_fwd_f32 (bf16 operand + f32 residual)
+  S1 = R + dropout(O Wo^T + bo)               mmu_gemm  EPI_BIAS_DROP_RES, f32 residual + f32 out
+  A = LN1(S1)                                 mmu_layernorm_fwd_f32 (bf16 operand)
   H  = gelu(A W1^T + b1)                      mmu_gemm  EPI_BIAS_GELU (saves Z = gelu'(.), bf16)
-  S2 = A32 + dropout(H W2^T + b2)             mmu_gemm  EPI_BIAS_DROP_RES, f32
-  Y, Y32 = LN2(S2)                            mmu_layernorm_fwd_f32
-The hidden state travels as a PAIR: bf16 X (the next GEMM's operand) and f32 X32 (the
-residual).  The residual adds and LN inputs stay f32, as in the reference's fp32 layer:
+  S2 = LN1(S1)_f32 + dropout(H W2^T + b2)     mmu_gemm  EPI_BIAS_DROP_RES, f32, the residual LN1(S1)
+                                              recomputed from S1 in the epilogue (res_ln)
+  Y = LN2(S2)                                 mmu_layernorm_fwd_f32
+The hidden state travels as bf16 X (the next GEMM's operand) plus its f32 residual R: the
+embeddings' f32 rows for layer 0, then the previous layer's S2 with its LN statistics (the
+f32 LayerNorm output is recomputed where it is added, never written).  The residual adds
+and LN inputs stay f32, as in the reference's fp32 layer:
 with the stream rounded to bf16 at each of the 48 LN / residual points of 12 layers the
 logits drift by up to 1.6 % of their scale (CPU emulation of the rounding points,
 DESIGN.md §4), with it f32 by 0.5 %.
@@ -66,8 +69,14 @@ class LayerWeights:
         return self.anchor.requires_grad
 
 
-def layer_forward(lw, X, X32, keymask, B, L, p_attn, p_hid, seeds, save):
-    """(X bf16, X32 f32) [M, 768] -> (Y bf16, Y32 f32, saved)"""
+def layer_forward(lw, X, R, keymask, B, L, p_attn, p_hid, seeds, save, res_ln=None, out32=False):
+    """X bf16 [M, 768] and its f32 residual -> (Y bf16, S2, mean2, rstd2, saved, Y32).
+
+    The f32 residual is ``R`` itself (res_ln None: the embeddings' f32 rows) or the previous
+    layer's output LayerNorm recomputed in the GEMM epilogue from its f32 input ``R`` = S2
+    and ``res_ln`` = (mean2, rstd2, gamma, beta): the LayerNorms write only their bf16 output
+    (the next GEMM operand), never an f32 copy, except Y32 when ``out32`` (the last layer's
+    hidden state for the pooler / the encoder API)."""
     M = B * L
     dev = X.device
     f32 = torch.float32
@@ -79,26 +88,44 @@ def layer_forward(lw, X, X32, keymask, B, L, p_attn, p_hid, seeds, save):
     K.attention_fwd(qkv, keymask, O, lse, B, L, HEADS, p_attn, seeds[0], dmask)
     S1 = torch.empty(M, HID, dtype=f32, device=dev)
     K.gemm(O, HID, True, lw.wo16, HID, True, S1, HID, M, HID, HID,
-           epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw.bo, residual=X32, drop_p=p_hid, seed=seeds[1]))
+           epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw.bo, residual=R, drop_p=p_hid, seed=seeds[1], res_ln=res_ln))
     A = torch.empty(M, HID, dtype=bf16, device=dev)
-    A32 = torch.empty(M, HID, dtype=f32, device=dev)
     mean1 = torch.empty(M, dtype=f32, device=dev)
     rstd1 = torch.empty(M, dtype=f32, device=dev)
-    K.layernorm_fwd_f32(S1, lw.ln1w, lw.ln1b, A, A32, mean1, rstd1)
+    K.layernorm_fwd_f32(S1, lw.ln1w, lw.ln1b, A, None, mean1, rstd1)
     Z = torch.empty(M, FFN, dtype=bf16, device=dev) if save else None  # gelu'(A W1^T + b1), for the backward
     Hh = torch.empty(M, FFN, dtype=bf16, device=dev)
     K.gemm(A, HID, True, lw.w116, HID, True, Hh, FFN, M, FFN, HID, epi=K.epilogue(K.EPI_BIAS_GELU, bias=lw.b1, aux=Z))
     S2 = torch.empty(M, HID, dtype=f32, device=dev)
     K.gemm(Hh, FFN, True, lw.w216, FFN, True, S2, HID, M, HID, FFN,
-           epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw.b2, residual=A32, drop_p=p_hid, seed=seeds[2]))
-    del A32
+           epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw.b2, residual=S1, drop_p=p_hid, seed=seeds[2],
+                          res_ln=(mean1, rstd1, lw.ln1w, lw.ln1b)))
     Y = torch.empty(M, HID, dtype=bf16, device=dev)
-    Y32 = torch.empty(M, HID, dtype=f32, device=dev)
+    Y32 = torch.empty(M, HID, dtype=f32, device=dev) if out32 else None
     mean2 = torch.empty(M, dtype=f32, device=dev)
     rstd2 = torch.empty(M, dtype=f32, device=dev)
     K.layernorm_fwd_f32(S2, lw.ln2w, lw.ln2b, Y, Y32, mean2, rstd2)
     saved = (X, qkv, O, lse, dmask, S1, mean1, rstd1, A, Z, Hh, S2, mean2, rstd2) if save else None
-    return Y, Y32, saved
+    return Y, S2, mean2, rstd2, saved, Y32
+
+
+def encoder_stack(lws, X, X32, keymask, B, L, p_attn, p_hid, seeds_of, need_grad, hook=None, all_layers=False):
+    """Run the fused layers over (X bf16, X32 f32 embedding rows); returns the f32 hidden
+    state of the last layer, or of every layer (all_layers)."""
+    R, rln, outs = X32, None, []
+    n = len(lws)
+    for i, lw in enumerate(lws):
+        out32 = all_layers or i == n - 1
+        if need_grad:
+            X, R, mu, rs, Y32 = BertLayerFunction.apply(X, R, lw.anchor, lw, keymask, B, L, p_attn, p_hid,
+                                                        seeds_of(i), hook, rln, out32)
+        else:
+            X, R, mu, rs, _, Y32 = layer_forward(lw, X, R, keymask, B, L, p_attn, p_hid, seeds_of(i), False, rln,
+                                                 out32)
+        rln = (mu, rs, lw.ln2w, lw.ln2b)
+        if out32:
+            outs.append(Y32)
+    return outs if all_layers else outs[-1]
 
 
 def _reduce(part, out):
@@ -222,31 +249,38 @@ def _mark():
 
 
 class BertLayerFunction(torch.autograd.Function):
-    """One fused BertLayer; (X bf16, X32 f32) [B*L, 768] -> (Y, Y32).  The layer's whole
-    input gradient is returned for X (X and X32 hold the same values; X32 gets None);
-    the output gradient arrives on Y from the next layer or on Y32 from the pooler.
-    ``anchor`` (the layer's query weight) only makes autograd run backward when the layer
-    is trainable."""
+    """One fused BertLayer: X bf16 [B*L, 768] + its f32 residual (R, res_ln: see
+    layer_forward) -> (Y, S2, mean2, rstd2, Y32).  S2 / mean2 / rstd2 (the next layer's
+    residual source) are non-differentiable; the layer's whole input gradient is returned
+    for X.  The output gradient arrives on Y from the next layer or on Y32 (out32: the last
+    layer) from the pooler.  ``anchor`` (the layer's query weight) only makes autograd run
+    backward when the layer is trainable."""
 
     @staticmethod
-    def forward(ctx, X, X32, anchor, lw, keymask, B, L, p_attn, p_hid, seeds, on_grads_ready):
+    def forward(ctx, X, R, anchor, lw, keymask, B, L, p_attn, p_hid, seeds, on_grads_ready, res_ln=None,
+                out32=True):
         ctx.set_materialize_grads(False)
         e0 = _mark()
-        Y, Y32, saved = layer_forward(lw, X, X32, keymask, B, L, p_attn, p_hid, seeds, save=True)
+        Y, S2, mean2, rstd2, saved, Y32 = layer_forward(lw, X, R, keymask, B, L, p_attn, p_hid, seeds, True,
+                                                        res_ln, out32)
         if e0 is not None:
             _block_events.append((e0, _mark()))
         ctx.saved_bufs = saved
         ctx.meta = (lw, keymask, B, L, p_attn, p_hid, seeds, on_grads_ready)
-        return Y, Y32
+        ctx.mark_non_differentiable(S2, mean2, rstd2)
+        if Y32 is None:
+            Y32 = Y.new_empty(0, dtype=torch.float32)
+            ctx.mark_non_differentiable(Y32)
+        return Y, S2, mean2, rstd2, Y32
 
     @staticmethod
-    def backward(ctx, dY, dY32):
+    def backward(ctx, dY, _dS2, _dmean2, _drstd2, dY32):
         lw, keymask, B, L, p_attn, p_hid, seeds, hook = ctx.meta
         wgrad = lw.trainable()
-        if dY32 is not None:
+        if dY32 is not None and dY32.numel():
             dY = dY32.to(bf16) if dY is None else dY + dY32.to(bf16)
         if dY is None:
-            return (None,) * 11
+            return (None,) * 13
         e0 = _mark()
         dX, side = layer_backward(lw, ctx.saved_bufs, dY.contiguous(), keymask, B, L, p_attn, p_hid, seeds, wgrad)
         if e0 is not None:
@@ -259,7 +293,7 @@ class BertLayerFunction(torch.autograd.Function):
             _join_side_at_end(side)
         elif wgrad and hook is not None:
             hook(lw)
-        return dX, None, None, None, None, None, None, None, None, None, None
+        return (dX,) + (None,) * 12
 
 
 _pending_join = set()

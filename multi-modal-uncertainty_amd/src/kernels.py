@@ -34,7 +34,9 @@ def _want(t, dtype, name):
 
 
 def epilogue(kind=EPI_STORE, bias=None, residual=None, aux=None, colsum=None, drop_p=0.0, seed=0, accumulate=False,
-             ldr=0, ldx=0, bias_bstride=0, res_bstride=0, aux_bstride=0, colsum_bstride=0):
+             ldr=0, ldx=0, bias_bstride=0, res_bstride=0, aux_bstride=0, colsum_bstride=0, res_ln=None):
+    """res_ln = (mean, rstd, w, b): with BIAS_DROP_RES into an f32 C, the residual is the LayerNorm
+    output recomputed from the f32 ``residual`` rows (the previous LayerNorm's input)."""
     e = Epilogue()
     e.kind, e.accumulate = kind, int(accumulate)
     e.bias, e.bias_bstride = _ptr(bias), bias_bstride
@@ -44,6 +46,12 @@ def epilogue(kind=EPI_STORE, bias=None, residual=None, aux=None, colsum=None, dr
     e.colsum, e.colsum_bstride = _ptr(colsum), colsum_bstride
     e.drop_p, e.seed = float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF
     e.workspace, e.workspace_floats = None, 0
+    if res_ln is not None:
+        for t in res_ln:
+            _want(t, torch.float32, "epilogue res_ln")
+            if not t.is_contiguous():
+                raise N.NativeError("epilogue res_ln tensors must be contiguous")
+        e.res_ln_mean, e.res_ln_rstd, e.res_ln_w, e.res_ln_b = (_ptr(t) for t in res_ln)
     return e
 
 

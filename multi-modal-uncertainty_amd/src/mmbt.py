@@ -22,7 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import kernels as K
-from .encoder import BertLayerFunction, LayerWeights, layer_forward
+from .encoder import LayerWeights, encoder_stack
 from .params import ParamStore
 from .resnet import StoreConv2d, resnet152_trunk
 
@@ -440,14 +440,9 @@ class MultimodalBertEncoder(nn.Module):
         p_attn, p_hid = (self.attn_dropout, self.hidden_dropout) if act else (0.0, 0.0)
         base = _seed() if act and (p_attn > 0 or p_hid > 0) else 0
         need_grad = torch.is_grad_enabled() and (X.requires_grad or any(lw.trainable() for lw in self._lw))
-        for i, lw in enumerate(self._lw):
-            seeds = (_mix(base, 3 * i), _mix(base, 3 * i + 1), _mix(base, 3 * i + 2))
-            if need_grad:
-                X, X32 = BertLayerFunction.apply(X, X32, lw.anchor, lw, km, nb, L, p_attn, p_hid, seeds,
-                                                 self._grad_ready_hook)
-            else:
-                X, X32, _ = layer_forward(lw, X, X32, km, nb, L, p_attn, p_hid, seeds, save=False)
-        return X32
+        return encoder_stack(self._lw, X, X32, km, nb, L, p_attn, p_hid,
+                             lambda i: (_mix(base, 3 * i), _mix(base, 3 * i + 1), _mix(base, 3 * i + 2)),
+                             need_grad, self._grad_ready_hook)
 
     def _pool(self, X, nb, L):
         return self.pooler(X.view(nb, L, 768))
@@ -499,15 +494,11 @@ class MultimodalBertEncoder(nn.Module):
         act = self._dropout_active()
         p_attn, p_hid = (self.attn_dropout, self.hidden_dropout) if act else (0.0, 0.0)
         base = _seed() if act else 0
-        outs = []
-        for i, lw in enumerate(self._lw):
-            seeds = (_mix(base, 3 * i), _mix(base, 3 * i + 1), _mix(base, 3 * i + 2))
-            if torch.is_grad_enabled():
-                X, X32 = BertLayerFunction.apply(X, X32, lw.anchor, lw, km, B, L, p_attn, p_hid, seeds, None)
-            else:
-                X, X32, _ = layer_forward(lw, X, X32, km, B, L, p_attn, p_hid, seeds, save=False)
-            outs.append(X32.view(B, L, H))
-        return outs if all_layers else outs[-1:]
+        outs = encoder_stack(self._lw, X, X32, km, B, L, p_attn, p_hid,
+                             lambda i: (_mix(base, 3 * i), _mix(base, 3 * i + 1), _mix(base, 3 * i + 2)),
+                             torch.is_grad_enabled(), None, all_layers=all_layers)
+        outs = outs if all_layers else [outs]
+        return [o.view(B, L, H) for o in outs]
 
     def _image_embeddings(self, proj):
         self._prepare()

@@ -267,6 +267,37 @@ def test_gemm_bias_dropout_residual_f32_stream(dev):
     assert abs((~keep).float().mean().item() - p) < 0.01
 
 
+@pytest.mark.gpu
+def test_gemm_residual_recomputed_layernorm(dev):
+    """res_ln: the f32 residual is LN(S) recomputed in the epilogue from the f32 rows S and
+    per-row mean / rstd, per-column gamma / beta -- equal to passing the materialised LN
+    output (the encoder's S2 -> next layer's residual, src/encoder.py); batched."""
+    k = K()
+    Bt, M, N, Kd = 2, 640, 768, 256
+    A, B = rnd(Bt, M, Kd, dev=dev, seed=121), rnd(Bt, N, Kd, dev=dev, seed=122, scale=0.1)
+    bias = torch.randn(Bt, N, device=dev) * 0.1
+    S = torch.randn(Bt, M, N, device=dev) * 2.0 + 0.7
+    mean = S.mean(-1).contiguous()
+    rstd = torch.rsqrt(S.var(-1, unbiased=False) + 1e-12).contiguous()
+    w, b = torch.randn(N, device=dev), torch.randn(N, device=dev)
+    R32 = (S - mean[..., None]) * rstd[..., None] * w + b
+    y = A.float() @ B.float().transpose(1, 2) + bias[:, None, :]
+    for p in (0.0, 0.1):
+        out, ref = (torch.empty(Bt, M, N, dtype=torch.float32, device=dev) for _ in range(2))
+        k.gemm(A, Kd, True, B, Kd, True, out, N, M, N, Kd, batch=Bt, sA=M * Kd, sB=N * Kd, sC=M * N,
+               epi=k.epilogue(k.EPI_BIAS_DROP_RES, bias=bias, bias_bstride=N, residual=S, res_bstride=M * N,
+                              drop_p=p, seed=5, res_ln=(mean, rstd, w, b)))
+        k.gemm(A, Kd, True, B, Kd, True, ref, N, M, N, Kd, batch=Bt, sA=M * Kd, sB=N * Kd, sC=M * N,
+               epi=k.epilogue(k.EPI_BIAS_DROP_RES, bias=bias, bias_bstride=N, residual=R32, res_bstride=M * N,
+                              drop_p=p, seed=5))
+        torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5 * R32.abs().max().item())
+        if p == 0.0:
+            torch.testing.assert_close(out, R32 + y, rtol=1e-5, atol=2e-5 * (R32.abs().max() + y.abs().max()).item())
+    with pytest.raises(Exception):  # all four LN tensors or none
+        k.gemm(A[0], Kd, True, B[0], Kd, True, out[0], N, M, N, Kd,
+               epi=k.epilogue(k.EPI_BIAS_DROP_RES, bias=bias[0], residual=S[0], res_ln=(mean[0], rstd[0], w, None)))
+
+
 def test_gemm_batched(dev):
     k = K()
     Bt, M, N, Kd = 3, 128, 128, 64
