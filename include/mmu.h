@@ -271,9 +271,12 @@ int mmu_conv3x3_wgrad(const void* dY, const void* X, float* dW, int64_t n_img, i
  * f32 accumulate; X [n_img*H*W, C] and Y [n_img*H*W, N] NHWC rows.  The forward of
  * Bottleneck.conv2 is (X = x, Wk = the channels-last filter [Cout][3][3][Cin]); its data
  * gradient is (X = dY, Wk = the flipped filter transposed to [Cin][3][3][Cout]).
- * C % 64 == 0, N % 128 == 0, N >= 256. */
+ * C % 64 == 0, N % 128 == 0, N >= 256.  `ws` (optional, ws_floats f32): when the output has
+ * too few 256x256 tiles to fill the chip (small batches: e.g. layer3 at batch 32 is 25
+ * tiles), the taps / channels are split over workgroups into f32 slabs of ws and summed in
+ * slice order into Y (deterministic). */
 int mmu_conv3x3_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W,
-                         int64_t C, int64_t N, mmu_stream_t stream);
+                         int64_t C, int64_t N, float* ws, int64_t ws_floats, mmu_stream_t stream);
 
 /* ------------------------------------------------------------------ BatchNorm (image trunk)
  * BatchNorm2d [+ residual add] [+ ReLU] of the ResNet-152 trunk (torchvision

@@ -475,26 +475,44 @@ int mmu_conv3x3_wgrad(const void* dY, const void* X, float* dW, int64_t n_img, i
 }
 
 int mmu_conv3x3_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
-                         int64_t N, mmu_stream_t stream) {
+                         int64_t N, float* ws, int64_t ws_floats, mmu_stream_t stream) {
   if (!X || !Wk || !Y) return fail("mmu_conv3x3_implicit: null pointer");
-  if (n_img <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 64 || N % 128 || N < 256)
-    return fail("mmu_conv3x3_implicit: needs C %% 64 == 0, N %% 128 == 0, N >= 256 (C=%ld N=%ld)", C, N);
+  if (n_img <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 64 || N % 64)
+    return fail("mmu_conv3x3_implicit: needs C %% 64 == 0, N %% 64 == 0 (C=%ld N=%ld)", C, N);
   const int64_t M = n_img * H * W;
   if (M < 256 || 2 * (M + 256) * C >= (1ll << 31) || 2 * (N + 256) * 9 * C >= (1ll << 31))
     return fail("mmu_conv3x3_implicit: map size out of range");
+  // 256x256 tiles (LDS-DMA gather) for N >= 256 with N % 128 == 0; 128x128 register-staged
+  // tiles for the narrow convs (N = 64 / 128 / ...)
+  const bool small = N < 256 || N % 128;
+  const int tm_ = small ? 128 : 256, tn_ = small ? 128 : 256;
   GemmParams p{};
   p.A = (const bf16*)X; p.lda = C;       // A gathered: [M pixels][9 C]
   p.B = (const bf16*)Wk; p.ldb = 9 * C;  // B K-major [N][9 C]
   p.C = Y; p.ldc = N;                    // Y [M pixels][N] bf16
   p.M = M; p.N = N; p.K = 9 * C;
   p.conv_h = (int)H; p.conv_w = (int)W; p.conv_c = (int)C;
-  p.tiles_m = (int)((M + 255) / 256);
-  p.tiles_n = (int)((N + 255) / 256);
+  p.tiles_m = (int)((M + tm_ - 1) / tm_);
+  p.tiles_n = (int)((N + tn_ - 1) / tn_);
   p.group_m = 1;
   p.kind = MMU_EPI_STORE;
   p.splitk = 1;
   p.kchunk = p.K;
-  conv3x3_implicit_launch(p, (hipStream_t)stream);
+  // split K (taps x channels) when the map has fewer tiles than half the CUs: ~512 blocks, >= 4
+  // 64-deep steps per slice, slabs bounded by the workspace
+  const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
+  if (ws && tiles < 128) {
+    int64_t want = (512 + tiles - 1) / tiles;
+    if (want > p.K / 256) want = p.K / 256;
+    if (want > ws_floats / (M * N)) want = ws_floats / (M * N);
+    if (want >= 2) {
+      const int64_t chunk = ((p.K + want - 1) / want + 63) / 64 * 64;
+      p.kchunk = chunk;
+      p.splitk = (int)((p.K + chunk - 1) / chunk);
+      p.ws = ws;
+    }
+  }
+  conv3x3_implicit_launch(p, small, (hipStream_t)stream);
   return check_launch("mmu_conv3x3_implicit");
 }
 

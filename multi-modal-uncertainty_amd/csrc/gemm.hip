@@ -399,6 +399,97 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(GemmParams p) {
   epilogue_block<EPI, OUT_F32, 4>(p, z, slice, m0 + 64 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
 }
 
+// ---------------------------------------------------------------- 3x3 conv, 128x128 tiles
+// The implicit-im2col forward / data-gradient product of a 3x3 / stride-1 / pad-1 conv with
+// FEW output channels (64 / 128: ResNet layer1 / layer2 conv2), on the small kernel's 128x128
+// tiles, 4 waves, register staging: the A rows (output pixels) are gathered per tap while
+// they are loaded (16 B per lane, padding and rows past M read as zero); B = the filter
+// K-major [N][9 C].  C % 64 == 0 (a 64-deep k-step lies in one tap), N % 64 == 0 (a 64-col
+// wave block is all in or all out: N = 64 runs half the tile's columns).  Split-K over
+// (tap, channel) steps into f32 slabs as the 256x256 conv kernel does.
+struct ConvRows4 {
+  int base[4], h[4], w[4];  // img * H (-1: row past M), h, w of the thread's 4 rows
+};
+static __device__ __forceinline__ void conva_g_load(uint4 (&r)[4], const bf16* __restrict__ X, const GemmParams& p,
+                                                    const ConvRows4& cr, int64_t k0, int t) {
+  const int H = p.conv_h, W = p.conv_w, C = p.conv_c;
+  const int tap = (int)(k0 / C), ci0 = (int)(k0 - (int64_t)tap * C);
+  const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+  const bool kin = k0 < p.K;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = t & 7;
+    const int hh = cr.h[i] + dh, ww = cr.w[i] + dw;
+    const bool ok = kin && cr.base[i] >= 0 && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
+    r[i] = ok ? *(const uint4*)(X + ((int64_t)(cr.base[i] + hh) * W + ww) * C + ci0 + 8 * c) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+__global__ __launch_bounds__(256) void gemm_conva_small_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * S_STAGE];
+  const int t = threadIdx.x, l = t & 63, w = t >> 6, wm = w >> 1, wn = w & 1;
+  int tm, tn, slice;
+  int64_t z;
+  block_tile(p, z, slice, tm, tn);
+  const int64_t m0 = (int64_t)tm * SBM, n0 = (int64_t)tn * SBN;
+  ConvRows4 cr;
+  {
+    const int H = p.conv_h, W = p.conv_w, HW = H * W;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t pix = m0 + (t >> 3) + 32 * i;  // g_load<true>'s row of piece i
+      const int img = (int)(pix / HW), rem = (int)(pix - (int64_t)img * HW);
+      cr.base[i] = pix < p.M ? img * H : -1;
+      cr.h[i] = rem / W;
+      cr.w[i] = rem - cr.h[i] * W;
+    }
+  }
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint4 ra[4], rb[4];
+  const int64_t kb = (int64_t)slice * p.kchunk;
+  const int64_t ke = kb + p.kchunk < p.K ? kb + p.kchunk : p.K;
+  const int nk = (int)((ke - kb + BKT - 1) / BKT);
+  conva_g_load(ra, p.A, p, cr, kb, t);
+  g_load<true>(rb, p.B, p.ldb, n0, p.N, kb, ke, t);
+  s_store<true>(smem, ra, t);
+  s_store<true>(smem + SBM * BKT * 2, rb, t);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* sa = smem + (kt & 1) * S_STAGE;
+    const char* sb = sa + SBM * BKT * 2;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      const int64_t k1 = kb + (int64_t)(kt + 1) * BKT;
+      conva_g_load(ra, p.A, p, cr, k1, t);
+      g_load<true>(rb, p.B, p.ldb, n0, p.N, k1, ke, t);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fb[4], fa[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fb[i] = s_frag<true, 256>(sb, 64 * wn + 16 * i, ks, l);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fa[j] = s_frag<true, 256>(sa, 64 * wm + 16 * j, ks, l);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      char* dst = smem + ((kt + 1) & 1) * S_STAGE;
+      s_store<true>(dst, ra, t);
+      s_store<true>(dst + SBM * BKT * 2, rb, t);
+    }
+    __syncthreads();
+  }
+  epilogue_block<MMU_EPI_STORE, false, 4>(p, z, slice, m0 + 64 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
+}
+
 // ================================================================ big: 256x256, LDS-DMA
 constexpr int BBM = 256, BBN = 256;
 constexpr int B_TILE = BBM * BKT * 2;  // 32 KiB per operand per stage
@@ -593,8 +684,31 @@ __global__ __launch_bounds__(512) void gemm_conva_kernel(GemmParams p) {
   gemm_big_body<true, true, MMU_EPI_STORE, false, 2>(p);
 }
 
-void conv3x3_implicit_launch(const GemmParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(gemm_conva_kernel, dim3(p.tiles_m * p.tiles_n, 1, 1), dim3(512), 0, s, p);
+// sum of the split-K slabs of one (M x N) product into a bf16 C (slice order: deterministic)
+__global__ __launch_bounds__(256) void splitk_reduce_bf16_kernel(const float* __restrict__ ws, bf16* __restrict__ C,
+                                                                 int64_t M, int64_t N, int64_t ldc, int splitk) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;  // 8 consecutive elements per thread
+  if (q * 8 >= M * N) return;
+  const int64_t e = q * 8, m = e / N, n = e - m * N;
+  const float* s = ws + e;
+  float4 a = *(const float4*)s, b = *(const float4*)(s + 4);
+  for (int k = 1; k < splitk; ++k) {
+    const float4 c = *(const float4*)(s + k * M * N), d = *(const float4*)(s + k * M * N + 4);
+    a.x += c.x; a.y += c.y; a.z += c.z; a.w += c.w;
+    b.x += d.x; b.y += d.y; b.z += d.z; b.w += d.w;
+  }
+  const bf16x8 o = {f2bf(a.x), f2bf(a.y), f2bf(a.z), f2bf(a.w), f2bf(b.x), f2bf(b.y), f2bf(b.z), f2bf(b.w)};
+  *(bf16x8*)(C + m * ldc + n) = o;
+}
+
+void conv3x3_implicit_launch(const GemmParams& p, bool small, hipStream_t s) {
+  if (small) hipLaunchKernelGGL(gemm_conva_small_kernel, dim3(p.tiles_m * p.tiles_n, p.splitk, 1), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(gemm_conva_kernel, dim3(p.tiles_m * p.tiles_n, p.splitk, 1), dim3(512), 0, s, p);
+  if (p.splitk > 1) {
+    const int64_t q = p.M * p.N / 8;
+    hipLaunchKernelGGL(splitk_reduce_bf16_kernel, dim3((unsigned)((q + 255) / 256)), dim3(256), 0, s, p.ws,
+                       (bf16*)p.C, p.M, p.N, p.ldc, p.splitk);
+  }
 }
 
 void conv3x3_wgrad_launch(const GemmParams& p, hipStream_t s) {

@@ -39,7 +39,7 @@ struct GemmParams {
   int conv_h, conv_w, conv_c;
 };
 void conv3x3_wgrad_launch(const GemmParams& p, hipStream_t s);
-void conv3x3_implicit_launch(const GemmParams& p, hipStream_t s);
+void conv3x3_implicit_launch(const GemmParams& p, bool small, hipStream_t s);  // small: 128x128 tiles
 
 void splitk_reduce_launch(const GemmParams& p, int batch, hipStream_t s);
 void gemm_launch(const GemmParams& p, bool a_kmajor, bool b_kmajor, bool f32out, bool big, int batch, hipStream_t s);

@@ -327,6 +327,10 @@ def row_pool_bwd(dout, n, dfmap_nhwc):
     N.call("mmu_row_pool_bwd", _ptr(dout), B, Hh, Ww, C, n, _ptr(dfmap_nhwc), _stream(dout))
 
 
+import os as _os
+_CONV_SPLITK = _os.environ.get("MMU_CONV_SPLITK", "1") != "0"  # A/B switch (tools/gpu_r3_splitk_ab.sh)
+
+
 def conv3x3_implicit(X, Wk, Y):
     """Y[p, n] = sum_{tap, c} X[p + tap shift, c] Wk[n, tap * C + c]: X [N, C, H, W] and Y
     [N, Nout, H, W] channels-last bf16, Wk bf16 contiguous with Wk.numel() == Nout * 9 * C
@@ -345,7 +349,9 @@ def conv3x3_implicit(X, Wk, Y):
     if (Y.shape != (n, nout, h, w) or Y.dtype != torch.bfloat16 or not wk_ok
             or not X.is_contiguous(memory_format=cl) or not Y.is_contiguous(memory_format=cl)):
         raise N.NativeError("conv3x3_implicit: X / Y channels-last bf16 [N, C, H, W], Wk [Nout][3][3][C] bf16")
-    N.call("mmu_conv3x3_implicit", _ptr(X), _ptr(Wk), _ptr(Y), n, h, w, c, nout, _stream(X))
+    ws = _splitk_workspace(Y.device) if _CONV_SPLITK else None  # split-K slabs for small maps (few tiles)
+    N.call("mmu_conv3x3_implicit", _ptr(X), _ptr(Wk), _ptr(Y), n, h, w, c, nout, _ptr(ws),
+           ws.numel() if ws is not None else 0, _stream(X))
 
 
 def conv3x3_wgrad(dY, X, dW, accumulate=False):
@@ -389,6 +395,29 @@ def _bn_mask_check(mask, X, what):
     _dev_check(mask, X)
 
 
+def _bn_vec_check(name, C, *ts):
+    """per-channel BatchNorm vectors: f32, contiguous, >= C elements, on the device (the kernels
+    read / write them as float[C]: a bf16 running_mean -- e.g. after module.to(bfloat16) --
+    would be written past its end)"""
+    for t in ts:
+        if t is None:
+            continue
+        _dev_check(t)
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() < C:
+            raise N.NativeError(f"{name}: per-channel tensors must be contiguous f32 with >= {C} elements; got "
+                                f"{t.dtype} {tuple(t.shape)}")
+
+
+def _bn_map_check(name, X, *ts):
+    for t in ts:
+        if t is None:
+            continue
+        _dev_check(t)
+        if t.dtype != torch.bfloat16 or t.numel() != X.numel():
+            raise N.NativeError(f"{name}: maps must be bf16 with X's {X.numel()} elements; got {t.dtype} "
+                                f"{tuple(t.shape)}")
+
+
 def batchnorm_fwd(X, Y, weight, bias, running_mean, running_var, training, momentum, eps, relu=False, skip=None,
                   num_batches_tracked=None, save_mean=None, save_invstd=None, relu_mask=None):
     """X, Y, skip: channels-last bf16 [N, C, H, W] (contiguous as [N*H*W, C]).  relu_mask
@@ -397,6 +426,10 @@ def batchnorm_fwd(X, Y, weight, bias, running_mean, running_var, training, momen
     _want(X, torch.bfloat16, "batchnorm X")
     _bn_mask_check(relu_mask, X, "batchnorm_fwd")
     C = X.shape[1]
+    _bn_vec_check("batchnorm_fwd", C, weight, bias, running_mean, running_var, save_mean, save_invstd)
+    _bn_map_check("batchnorm_fwd", X, Y, skip)
+    if num_batches_tracked is not None and (num_batches_tracked.dtype != torch.int64 or not num_batches_tracked.is_cuda):
+        raise N.NativeError("batchnorm_fwd: num_batches_tracked must be an int64 device tensor")
     rows = X.numel() // C
     ws = _bn_workspace(X.device)
     N.call("mmu_batchnorm_fwd", _ptr(X), _ptr(skip), _ptr(Y), rows, C, _ptr(weight), _ptr(bias), _ptr(running_mean),
@@ -409,8 +442,11 @@ def batchnorm_bwd(dY, Y, X, weight, save_mean, save_invstd, relu, dX, dSkip=None
                   relu_mask=None):
     """relu: g = dY * [Y > 0] from relu_mask (batchnorm_fwd's) when given, else from Y."""
     _dev_check(dY, X, dX)
+    _want(X, torch.bfloat16, "batchnorm_bwd X")
     _bn_mask_check(relu_mask, X, "batchnorm_bwd")
     C = X.shape[1]
+    _bn_vec_check("batchnorm_bwd", C, weight, save_mean, save_invstd, dweight, dbias)
+    _bn_map_check("batchnorm_bwd", X, dY, Y, dX, dSkip)
     rows = X.numel() // C
     ws = _bn_workspace(X.device)
     N.call("mmu_batchnorm_bwd", _ptr(dY), _ptr(Y), _ptr(relu_mask), _ptr(X), rows, C, _ptr(weight), _ptr(save_mean),

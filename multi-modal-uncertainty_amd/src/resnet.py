@@ -73,8 +73,11 @@ class BatchNorm2d(nn.BatchNorm2d):
 
     def forward(self, x, skip=None, relu=None, skip_sink=None):
         relu = self.fused_relu if relu is None else relu
+        # (the kernels take f32 per-channel parameters / statistics: a module cast to bf16 --
+        # module.to(torch.bfloat16) -- takes the torch path)
         hip = (x.is_cuda and x.dtype == torch.bfloat16 and (skip is None or skip.dtype == torch.bfloat16)
-               and x.shape[1] % 8 == 0)
+               and x.shape[1] % 8 == 0 and self.weight is not None and self.weight.dtype == torch.float32
+               and (self.running_mean is None or self.running_mean.dtype == torch.float32))
         if hip:
             x = x.contiguous(memory_format=torch.channels_last)
             if skip is not None:

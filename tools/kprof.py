@@ -1,7 +1,8 @@
 """Run ONE hot kernel of the bench workload a few times, for rocprofv3 PMC passes
 (counters per dispatch; no timing of its own).
 
-  python tools/kprof.py attn_fwd|attn_bwd|gemm_w1|gemm_qkv|gemm_dz|gemm_wgrad [--reps 3]
+  python tools/kprof.py attn_fwd|attn_bwd|gemm_w1|gemm_qkv|gemm_dz|gemm_wgrad|ln_fwd|ln_bwd|bn_fwd|bn_bwd
+                        [--reps 3]
 """
 import argparse
 import os
@@ -42,6 +43,38 @@ def main():
             fn = lambda: K.attention_fwd(qkv, km, O, lse, B, L, H, 0.1, 7, dm)  # noqa: E731
         else:
             fn = lambda: K.attention_bwd(qkv, km, O, dO, lse, delta, dqkv, B, L, H, 0.1, 7, dm)  # noqa: E731
+    elif a.which.startswith("ln_"):  # the encoder's output LayerNorm, forward / backward (f32 input)
+        S = torch.randn(M, HID, generator=g, device=dev)
+        w, b = torch.randn(HID, device=dev), torch.randn(HID, device=dev)
+        Y = torch.empty(M, HID, dtype=bf, device=dev)
+        mean, rstd = torch.empty(M, device=dev), torch.empty(M, device=dev)
+        K.layernorm_fwd_f32(S, w, b, Y, None, mean, rstd)
+        dY = rnd(M, HID)
+        dX, dXd = torch.empty(M, HID, dtype=bf, device=dev), torch.empty(M, HID, dtype=bf, device=dev)
+        P = K.ln_parts(M)
+        pw, pb, pbias = (torch.empty(P, HID, device=dev) for _ in range(3))
+        fn = (lambda: K.layernorm_fwd_f32(S, w, b, Y, None, mean, rstd)) if a.which == "ln_fwd" else \
+            (lambda: K.layernorm_bwd(dY, S, mean, rstd, w, dX, dXd, 0.1, 5, pw, pb, pbias))  # noqa: E731
+    elif a.which.startswith("bn_"):  # layer3 bn3 (+ skip, ReLU): [B*14*14, 1024] channels-last
+        Nb, C, H = B, 1024, 14
+        cl = torch.channels_last
+        x = torch.randn(Nb, C, H, H, generator=g, device=dev).to(bf).contiguous(memory_format=cl)
+        skip = torch.randn(Nb, C, H, H, generator=g, device=dev).to(bf).contiguous(memory_format=cl)
+        y = torch.empty_like(x)
+        w, b = torch.ones(C, device=dev), torch.zeros(C, device=dev)
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        nbt = torch.zeros((), dtype=torch.int64, device=dev)
+        sm, si = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=dev)
+        K.batchnorm_fwd(x, y, w, b, rm, rv, True, 0.1, 1e-5, relu=True, skip=skip, num_batches_tracked=nbt,
+                        save_mean=sm, save_invstd=si, relu_mask=mask)
+        dy = torch.randn(Nb, C, H, H, generator=g, device=dev).to(bf).contiguous(memory_format=cl)
+        dx, ds = torch.empty_like(x), torch.empty_like(x)
+        dw, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+        fn = (lambda: K.batchnorm_fwd(x, y, w, b, rm, rv, True, 0.1, 1e-5, relu=True, skip=skip,  # noqa: E731
+                                      num_batches_tracked=nbt, save_mean=sm, save_invstd=si, relu_mask=mask)) \
+            if a.which == "bn_fwd" else \
+            (lambda: K.batchnorm_bwd(dy, None, x, w, sm, si, True, dx, ds, dw, db, relu_mask=mask))  # noqa: E731
     else:
         X, A = rnd(M, HID), rnd(M, HID)
         W1, W2, Wqkv = rnd(FFN, HID), rnd(HID, FFN), rnd(3 * HID, HID)
