@@ -82,6 +82,8 @@ typedef struct mmu_epilogue {
   const float* res_ln_rstd;
   const float* res_ln_w;
   const float* res_ln_b;
+  int64_t res_ln_bstride;   /* batched products: w / b of batch item z at + z * res_ln_bstride
+                               (mean / rstd at + z * M)                                  */
 } mmu_epilogue;
 
 int mmu_gemm(const void* A, int64_t lda, int a_kmajor,

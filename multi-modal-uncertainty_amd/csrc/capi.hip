@@ -130,7 +130,7 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
     p.colsum = epi->colsum; p.colsum_bstride = epi->colsum_bstride;
     p.drop_p = epi->drop_p; p.seed = epi->seed;
     p.res_ln_mean = epi->res_ln_mean; p.res_ln_rstd = epi->res_ln_rstd;
-    p.res_ln_w = epi->res_ln_w; p.res_ln_b = epi->res_ln_b;
+    p.res_ln_w = epi->res_ln_w; p.res_ln_b = epi->res_ln_b; p.res_ln_bstride = epi->res_ln_bstride;
   }
   p.kind = kind;
   if (kind < 0 || kind > MMU_EPI_BIAS_DROP_QGELU) return fail("mmu_gemm: bad epilogue kind %d", kind);

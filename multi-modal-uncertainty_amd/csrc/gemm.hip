@@ -213,8 +213,10 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
   if (RES32) {
     float4 w0 = make_float4(1.f, 1.f, 1.f, 1.f), w1 = w0, b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
     if (res_ln) {
-      w0 = *(const float4*)(p.res_ln_w + n); w1 = *(const float4*)(p.res_ln_w + n + 4);
-      b0 = *(const float4*)(p.res_ln_b + n); b1 = *(const float4*)(p.res_ln_b + n + 4);
+      const float* lw_ = p.res_ln_w + z * p.res_ln_bstride;
+      const float* lb_ = p.res_ln_b + z * p.res_ln_bstride;
+      w0 = *(const float4*)(lw_ + n); w1 = *(const float4*)(lw_ + n + 4);
+      b0 = *(const float4*)(lb_ + n); b1 = *(const float4*)(lb_ + n + 4);
     }
     lw[0] = w0.x; lw[1] = w0.y; lw[2] = w0.z; lw[3] = w0.w; lw[4] = w1.x; lw[5] = w1.y; lw[6] = w1.z; lw[7] = w1.w;
     lb[0] = b0.x; lb[1] = b0.y; lb[2] = b0.z; lb[3] = b0.w; lb[4] = b1.x; lb[5] = b1.y; lb[6] = b1.z; lb[7] = b1.w;

@@ -29,6 +29,7 @@ struct GemmParams {
   uint64_t seed;
   // f32 residual = LN(residual rows) recomputed per element (mmu_epilogue res_ln_*)
   const float *res_ln_mean, *res_ln_rstd, *res_ln_w, *res_ln_b;
+  int64_t res_ln_bstride;
   // split-K (EPI_STORE, f32 C, no bias/colsum): grid.y slices of kchunk, slabs in ws
   int splitk;
   int64_t kchunk;

@@ -24,7 +24,7 @@ class Epilogue(ctypes.Structure):
                 ("residual", c_vp), ("ldr", c_i64), ("res_bstride", c_i64), ("aux", c_vp), ("ldx", c_i64),
                 ("aux_bstride", c_i64), ("colsum", c_vp), ("colsum_bstride", c_i64), ("drop_p", c_f32),
                 ("seed", c_u64), ("workspace", c_vp), ("workspace_floats", c_i64), ("res_ln_mean", c_vp),
-                ("res_ln_rstd", c_vp), ("res_ln_w", c_vp), ("res_ln_b", c_vp)]
+                ("res_ln_rstd", c_vp), ("res_ln_w", c_vp), ("res_ln_b", c_vp), ("res_ln_bstride", c_i64)]
 
 
 # name -> (restype, argtypes); every entry must be exported by the library (tested on CPU)

@@ -34,7 +34,8 @@ def _want(t, dtype, name):
 
 
 def epilogue(kind=EPI_STORE, bias=None, residual=None, aux=None, colsum=None, drop_p=0.0, seed=0, accumulate=False,
-             ldr=0, ldx=0, bias_bstride=0, res_bstride=0, aux_bstride=0, colsum_bstride=0, res_ln=None):
+             ldr=0, ldx=0, bias_bstride=0, res_bstride=0, aux_bstride=0, colsum_bstride=0, res_ln=None,
+             res_ln_bstride=0):
     """res_ln = (mean, rstd, w, b): with BIAS_DROP_RES into an f32 C, the residual is the LayerNorm
     output recomputed from the f32 ``residual`` rows (the previous LayerNorm's input)."""
     e = Epilogue()
@@ -52,6 +53,7 @@ def epilogue(kind=EPI_STORE, bias=None, residual=None, aux=None, colsum=None, dr
             if not t.is_contiguous():
                 raise N.NativeError("epilogue res_ln tensors must be contiguous")
         e.res_ln_mean, e.res_ln_rstd, e.res_ln_w, e.res_ln_b = (_ptr(t) for t in res_ln)
+        e.res_ln_bstride = res_ln_bstride
     return e
 
 
@@ -396,26 +398,18 @@ def _bn_mask_check(mask, X, what):
 
 
 def _bn_vec_check(name, C, *ts):
-    """per-channel BatchNorm vectors: f32, contiguous, >= C elements, on the device (the kernels
-    read / write them as float[C]: a bf16 running_mean -- e.g. after module.to(bfloat16) --
-    would be written past its end)"""
+    """per-channel BatchNorm vectors must be f32 (the kernels read / write them as float[C]: a
+    bf16 running_mean -- e.g. after module.to(bfloat16) -- would be written past its end).
+    Only the dtype is checked per call (cheap: this runs ~300 times per train step)."""
     for t in ts:
-        if t is None:
-            continue
-        _dev_check(t)
-        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() < C:
-            raise N.NativeError(f"{name}: per-channel tensors must be contiguous f32 with >= {C} elements; got "
-                                f"{t.dtype} {tuple(t.shape)}")
+        if t is not None and t.dtype != torch.float32:
+            raise N.NativeError(f"{name}: per-channel tensors must be f32 (got {t.dtype} {tuple(t.shape)})")
 
 
 def _bn_map_check(name, X, *ts):
     for t in ts:
-        if t is None:
-            continue
-        _dev_check(t)
-        if t.dtype != torch.bfloat16 or t.numel() != X.numel():
-            raise N.NativeError(f"{name}: maps must be bf16 with X's {X.numel()} elements; got {t.dtype} "
-                                f"{tuple(t.shape)}")
+        if t is not None and t.dtype != torch.bfloat16:
+            raise N.NativeError(f"{name}: maps must be bf16 (got {t.dtype} {tuple(t.shape)})")
 
 
 def batchnorm_fwd(X, Y, weight, bias, running_mean, running_var, training, momentum, eps, relu=False, skip=None,
@@ -428,8 +422,8 @@ def batchnorm_fwd(X, Y, weight, bias, running_mean, running_var, training, momen
     C = X.shape[1]
     _bn_vec_check("batchnorm_fwd", C, weight, bias, running_mean, running_var, save_mean, save_invstd)
     _bn_map_check("batchnorm_fwd", X, Y, skip)
-    if num_batches_tracked is not None and (num_batches_tracked.dtype != torch.int64 or not num_batches_tracked.is_cuda):
-        raise N.NativeError("batchnorm_fwd: num_batches_tracked must be an int64 device tensor")
+    if num_batches_tracked is not None and num_batches_tracked.dtype != torch.int64:
+        raise N.NativeError("batchnorm_fwd: num_batches_tracked must be int64")
     rows = X.numel() // C
     ws = _bn_workspace(X.device)
     N.call("mmu_batchnorm_fwd", _ptr(X), _ptr(skip), _ptr(Y), rows, C, _ptr(weight), _ptr(bias), _ptr(running_mean),

@@ -47,9 +47,11 @@ class EnsembleMMBT:
         self.clf_b = torch.stack([m.clf.bias.detach() for m in self.members])
         self.hidden_dropout, self.attn_dropout = enc0.hidden_dropout, enc0.attn_dropout
 
-    def _layer(self, lw, X, X32, km, nb, L, p_attn, p_hid, seeds):
-        """(X bf16, X32 f32) [K*M, 768] -> (Y, Y32): src/encoder.py layer_forward batched over
-        the members (the same f32 hidden stream)."""
+    def _layer(self, lw, X, R, km, nb, L, p_attn, p_hid, seeds, res_ln=None, out32=False):
+        """X bf16 [K*M, 768] + its f32 residual -> (Y, S2, mean2, rstd2, Y32): src/encoder.py
+        layer_forward batched over the members (the same f32 hidden stream: R is the embeddings'
+        f32 rows, or the previous layer's S2 whose LayerNorm the epilogue recomputes from
+        res_ln = (mean, rstd, gamma [K, 768], beta [K, 768]))."""
         Km, M = self.K, nb * L
         dev = X.device
         f32 = torch.float32
@@ -61,24 +63,32 @@ class EnsembleMMBT:
         K.attention_fwd(qkv, km, O, lse, Km * nb, L, 12, p_attn, seeds[0])
         S1 = torch.empty(Km * M, HID, dtype=f32, device=dev)
         K.gemm(O, HID, True, lw["wo16"], HID, True, S1, HID, M, HID, HID, batch=Km, sA=M * HID, sB=HID * HID,
-               sC=M * HID, epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw["bo"], bias_bstride=HID, residual=X32,
-                                          res_bstride=M * HID, drop_p=p_hid, seed=seeds[1]))
+               sC=M * HID, epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw["bo"], bias_bstride=HID, residual=R,
+                                          res_bstride=M * HID, drop_p=p_hid, seed=seeds[1], res_ln=res_ln,
+                                          res_ln_bstride=HID))
+        del R
         A = torch.empty_like(O)
-        A32 = torch.empty_like(S1)
-        K.layernorm_fwd_f32(S1, lw["ln1w"], lw["ln1b"], A, A32, eps=LN_EPS, group_rows=M, param_stride=HID)
-        del S1
+        mean1 = torch.empty(Km * M, dtype=f32, device=dev)
+        rstd1 = torch.empty_like(mean1)
+        K.layernorm_fwd_f32(S1, lw["ln1w"], lw["ln1b"], A, None, mean1, rstd1, eps=LN_EPS, group_rows=M,
+                            param_stride=HID)
         Hh = torch.empty(Km * M, FFN, dtype=bf16, device=dev)
         K.gemm(A, HID, True, lw["w116"], HID, True, Hh, FFN, M, FFN, HID, batch=Km, sA=M * HID, sB=FFN * HID,
                sC=M * FFN, epi=K.epilogue(K.EPI_BIAS_GELU, bias=lw["b1"], bias_bstride=FFN))
+        del A
         S2 = torch.empty(Km * M, HID, dtype=f32, device=dev)
         K.gemm(Hh, FFN, True, lw["w216"], FFN, True, S2, HID, M, HID, FFN, batch=Km, sA=M * FFN, sB=HID * FFN,
-               sC=M * HID, epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw["b2"], bias_bstride=HID, residual=A32,
-                                          res_bstride=M * HID, drop_p=p_hid, seed=seeds[2]))
-        del A32
+               sC=M * HID, epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw["b2"], bias_bstride=HID, residual=S1,
+                                          res_bstride=M * HID, drop_p=p_hid, seed=seeds[2],
+                                          res_ln=(mean1, rstd1, lw["ln1w"], lw["ln1b"]), res_ln_bstride=HID))
+        del S1, Hh
         Y = torch.empty_like(O)
-        Y32 = torch.empty_like(S2)
-        K.layernorm_fwd_f32(S2, lw["ln2w"], lw["ln2b"], Y, Y32, eps=LN_EPS, group_rows=M, param_stride=HID)
-        return Y, Y32
+        Y32 = torch.empty_like(S2) if out32 else None
+        mean2 = torch.empty(Km * M, dtype=f32, device=dev)
+        rstd2 = torch.empty_like(mean2)
+        K.layernorm_fwd_f32(S2, lw["ln2w"], lw["ln2b"], Y, Y32, mean2, rstd2, eps=LN_EPS, group_rows=M,
+                            param_stride=HID)
+        return Y, S2, mean2, rstd2, Y32
 
     @torch.no_grad()
     def logits(self, txt, mask, segment, img, mc_samples=1, mc_dropout=None):
@@ -107,10 +117,14 @@ class EnsembleMMBT:
                         drop_txt=p_txt, drop_img=0.0, seed=_seed() if mc else 0, X32=X32[k * M:(k + 1) * M])
         p_attn, p_hid = (self.attn_dropout, self.hidden_dropout) if mc else (0.0, 0.0)
         base = _seed() if mc else 0
+        R, rln, n = X32, None, len(self.layers)
+        del X32
         for i, lw in enumerate(self.layers):
-            X, X32 = self._layer(lw, X, X32, km, nb, S, p_attn, p_hid, (_mix(base, 3 * i), _mix(base, 3 * i + 1),
-                                                                        _mix(base, 3 * i + 2)))
-        h0 = X32.view(self.K, nb, S, HID)[:, :, 0]                             # [K, nb, 768] f32
+            X, R, mu, rs, Y32 = self._layer(lw, X, R, km, nb, S, p_attn, p_hid,
+                                            (_mix(base, 3 * i), _mix(base, 3 * i + 1), _mix(base, 3 * i + 2)),
+                                            rln, out32=i == n - 1)
+            rln = (mu, rs, lw["ln2w"], lw["ln2b"])
+        h0 = Y32.view(self.K, nb, S, HID)[:, :, 0]                             # [K, nb, 768] f32
         pooled = torch.tanh(torch.baddbmm(self.pool_b.unsqueeze(1), h0, self.pool_w.transpose(1, 2)))
         out = torch.baddbmm(self.clf_b.unsqueeze(1), pooled, self.clf_w.transpose(1, 2))
         return out.view(self.K, T_mc, B, -1)
