@@ -1,5 +1,6 @@
 """Attention kernel throughput at the bench workload (B=256, L=513, 12 heads x 64):
-forward / backward with and without attention-probs dropout.
+forward / backward with and without attention-probs dropout; the backward also emits the
+Q/K/V bias-gradient column sums as the encoder's does.  MMU_LIB_PATH selects another build.
 
   python tools/attn_bench.py [--batch 256] [--len 513]
 """
@@ -19,8 +20,6 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--len", type=int, default=513)
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--var", default="MMU_ATTN_DMA", help="env switch timed at each of --vals (interleaved)")
-    ap.add_argument("--vals", default="1")
     a = ap.parse_args()
     B, L, H, dev = a.batch, a.len, 12, "cuda"
     g = torch.Generator(device=dev).manual_seed(0)
@@ -33,16 +32,15 @@ def main():
     dqkv = torch.empty(B * L, 3 * 768, dtype=torch.bfloat16, device=dev)
     delta = torch.empty(B * H, L, device=dev)
     dm = K.dropmask_empty(B, L, H, dev)
+    dbp = K.attention_dbias_parts(B, L, H, dev)
     fl_f = 4.0 * B * H * L * L * 64  # QK^T + PV
     fl_b = 2.5 * fl_f                # S, dP, dV, dK, dQ recompute + products
     for p in (0.0, 0.1):
-        for v in a.vals.split(","):
-            os.environ[a.var] = v
-            tf = timed(lambda: K.attention_fwd(qkv, km, O, lse, B, L, H, p, 7, dm if p > 0 else None), a.iters)
-            tb = timed(lambda: K.attention_bwd(qkv, km, O, dO, lse, delta, dqkv, B, L, H, p, 7,
-                                               dm if p > 0 else None), a.iters)
-            print(f"p={p:.1f} {a.var}={v}  fwd {tf:.3f} ms ({fl_f / tf / 1e9:6.1f} TF/s)   bwd {tb:.3f} ms "
-                  f"({fl_b / tb / 1e9:6.1f} TF/s)", flush=True)
+        tf = timed(lambda: K.attention_fwd(qkv, km, O, lse, B, L, H, p, 7, dm if p > 0 else None), a.iters)
+        tb = timed(lambda: K.attention_bwd(qkv, km, O, dO, lse, delta, dqkv, B, L, H, p, 7,
+                                           dm if p > 0 else None, dbp), a.iters)
+        print(f"p={p:.1f}  fwd {tf:.3f} ms ({fl_f / tf / 1e9:6.1f} TF/s)   bwd {tb:.3f} ms "
+              f"({fl_b / tb / 1e9:6.1f} TF/s)", flush=True)
 
 
 if __name__ == "__main__":
