@@ -28,7 +28,7 @@ def main():
     dev, cl = "cuda", torch.channels_last
     # (Cin, Cout, H): layer2..4 conv1 / conv3 (every stride-1 1x1 with both widths % 128 == 0)
     shapes = [(256, 64, 56), (64, 256, 56), (512, 128, 28), (128, 512, 28), (1024, 256, 14), (256, 1024, 14),
-              (2048, 512, 7), (512, 2048, 7)]
+              (2048, 512, 7), (512, 2048, 7), (64, 64, 56), (256, 128, 56), (512, 256, 28), (1024, 512, 14)]
     print(f"batch {N}; us per call (best of 10); TF/s in brackets")
     for cin, cout, H in shapes:
         x = (torch.randn(N, cin, H, H, device=dev) * 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
