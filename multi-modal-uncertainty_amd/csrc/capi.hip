@@ -151,10 +151,12 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
   // split-K for long-K / few-tile products (the weight gradients: K = tokens, M x N = a weight matrix)
   p.splitk = 1;
   p.kchunk = K;
-  if (kind == MMU_EPI_STORE && c_dtype == MMU_F32 && !p.bias && !p.colsum && epi && epi->workspace && K >= 4096) {
+  if (kind == MMU_EPI_STORE && c_dtype == MMU_F32 && !p.bias && !p.colsum && epi && epi->workspace && K >= 1024) {
     const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n * batch;
-    // slice cap 64 / minimum slice depth 1024 (profiles/r2_splitk_cap_ab.txt)
-    const int64_t max_split = 64, min_k = 1024;
+    // slice cap 64 / minimum slice depth 1024 (profiles/r2_splitk_cap_ab.txt); short reductions
+    // (the batch-32 ResNet filter gradients: K = 1.5-25 K pixels over 4-16 tiles) go down to
+    // 256-deep slices so that they still fill the chip
+    const int64_t max_split = 64, min_k = K >= 32768 ? 1024 : 256;
     int64_t want = (640 + tiles - 1) / tiles;
     if (want > K / min_k) want = K / min_k;
     if (want > max_split) want = max_split;
