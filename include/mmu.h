@@ -280,6 +280,21 @@ int mmu_conv3x3_wgrad(const void* dY, const void* X, float* dW, int64_t n_img, i
 int mmu_conv3x3_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W,
                          int64_t C, int64_t N, float* ws, int64_t ws_floats, mmu_stream_t stream);
 
+/* ResNet-152 stem convolution, 7x7 / stride 2 / pad 3, 3 -> 64 channels (torchvision resnet
+ * child 0, the image encoder's conv embed: src/mmbt.py:19-21,42), on channels-last bf16:
+ * X [n_img, H, W, 3], Wk [64][7][7][3] (the channels-last filter), Y [n_img, Ho, Wo, 64] with
+ * Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1; f32 accumulate.  One persistent kernel: tiles of
+ * 2 x 64 output pixels, the input patch in LDS, 16x16x32 bf16 MFMAs over the 3-channel taps
+ * padded to 4 (K = 224). */
+int mmu_stem_conv_fwd(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W,
+                      mmu_stream_t stream);
+/* Its filter gradient: dW f32 [64][7][7][3] (+)= sum over pixels of dY (x) im2col(X) (dY
+ * [n_img, Ho, Wo, 64] bf16), += when accumulate.  Per-block f32 partials go to ws
+ * (>= mmu_stem_conv_wgrad_ws_floats(n_img, H, W) floats) and are summed in block order. */
+int64_t mmu_stem_conv_wgrad_ws_floats(int64_t n_img, int64_t H, int64_t W);
+int mmu_stem_conv_wgrad(const void* dY, const void* X, float* dW, int64_t n_img, int64_t H, int64_t W,
+                        int accumulate, float* ws, int64_t ws_floats, mmu_stream_t stream);
+
 /* ------------------------------------------------------------------ BatchNorm (image trunk)
  * BatchNorm2d [+ residual add] [+ ReLU] of the ResNet-152 trunk (torchvision
  * Bottleneck bn1/bn2/bn3 + downsample, src/mmbt.py:19-21) on channels-last bf16

@@ -476,6 +476,43 @@ int mmu_conv3x3_wgrad(const void* dY, const void* X, float* dW, int64_t n_img, i
   return check_launch("mmu_conv3x3_wgrad");
 }
 
+static int stem_params(StemParams& p, int64_t n_img, int64_t H, int64_t W, const char* who) {
+  if (n_img <= 0 || H < 1 || W < 1 || n_img * H * W * 3 >= (1ll << 31) || n_img > (1 << 20))
+    return fail("%s: bad image batch %ld x %ld x %ld", who, n_img, H, W);
+  p.n = (int)n_img; p.H = (int)H; p.W = (int)W;
+  stem_fill_geometry(p);
+  if ((int64_t)p.n * p.Ho * p.Wo * 64 >= (1ll << 31)) return fail("%s: output too large", who);
+  return 0;
+}
+
+int mmu_stem_conv_fwd(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W,
+                      mmu_stream_t stream) {
+  if (!X || !Wk || !Y) return fail("mmu_stem_conv_fwd: null pointer");
+  StemParams p{};
+  if (stem_params(p, n_img, H, W, "mmu_stem_conv_fwd")) return 1;
+  p.X = (const bf16*)X; p.Wt = (const bf16*)Wk; p.Y = (bf16*)Y;
+  stem_fwd_launch(p, (hipStream_t)stream);
+  return check_launch("mmu_stem_conv_fwd");
+}
+
+int64_t mmu_stem_conv_wgrad_ws_floats(int64_t n_img, int64_t H, int64_t W) {
+  StemParams p{};
+  if (stem_params(p, n_img, H, W, "mmu_stem_conv_wgrad_ws_floats")) return -1;
+  return stem_wgrad_ws_floats(p.n_tiles);
+}
+
+int mmu_stem_conv_wgrad(const void* dY, const void* X, float* dW, int64_t n_img, int64_t H, int64_t W,
+                        int accumulate, float* ws, int64_t ws_floats, mmu_stream_t stream) {
+  if (!dY || !X || !dW || !ws) return fail("mmu_stem_conv_wgrad: null pointer");
+  StemParams p{};
+  if (stem_params(p, n_img, H, W, "mmu_stem_conv_wgrad")) return 1;
+  if (ws_floats < stem_wgrad_ws_floats(p.n_tiles))
+    return fail("mmu_stem_conv_wgrad: ws needs %ld floats", stem_wgrad_ws_floats(p.n_tiles));
+  p.X = (const bf16*)X; p.dY = (const bf16*)dY;
+  stem_wgrad_launch(p, dW, accumulate, ws, (hipStream_t)stream);
+  return check_launch("mmu_stem_conv_wgrad");
+}
+
 int mmu_conv3x3_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
                          int64_t N, float* ws, int64_t ws_floats, mmu_stream_t stream) {
   if (!X || !Wk || !Y) return fail("mmu_conv3x3_implicit: null pointer");

@@ -41,6 +41,18 @@ struct GemmParams {
 };
 void conv3x3_wgrad_launch(const GemmParams& p, hipStream_t s);
 void conv3x3_implicit_launch(const GemmParams& p, bool small, hipStream_t s);  // small: 128x128 tiles
+struct StemParams {  // csrc/stem.hip
+  const bf16* X;     // [n, H, W, 3]
+  const bf16* Wt;    // [64][7][7][3]
+  const bf16* dY;    // [n, Ho, Wo, 64] (filter gradient)
+  bf16* Y;           // [n, Ho, Wo, 64] (forward)
+  int n, H, W, Ho, Wo, tiles_r, tiles_c;
+  int64_t n_tiles;
+};
+void stem_fill_geometry(StemParams& p);
+int64_t stem_wgrad_ws_floats(int64_t n_tiles);
+void stem_fwd_launch(const StemParams& p, hipStream_t s);
+void stem_wgrad_launch(const StemParams& p, float* dW, int accumulate, float* ws, hipStream_t s);
 
 void splitk_reduce_launch(const GemmParams& p, int batch, hipStream_t s);
 void gemm_launch(const GemmParams& p, bool a_kmajor, bool b_kmajor, bool f32out, bool big, int batch, hipStream_t s);

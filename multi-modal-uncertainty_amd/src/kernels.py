@@ -356,6 +356,50 @@ def conv3x3_implicit(X, Wk, Y):
            ws.numel() if ws is not None else 0, _stream(X))
 
 
+def _stem_check(X, what):
+    if (X.dim() != 4 or X.dtype != torch.bfloat16 or X.shape[1] != 3
+            or not X.is_contiguous(memory_format=torch.channels_last)):
+        raise N.NativeError(f"{what}: X must be channels-last bf16 [N, 3, H, W] (got {tuple(X.shape)} {X.dtype})")
+
+
+def stem_conv_fwd(X, Wk, Y):
+    """Y = conv2d(X, Wk, stride 2, padding 3): the ResNet stem (7x7, 3 -> 64).  X [N, 3, H, W]
+    and Y [N, 64, Ho, Wo] channels-last bf16; Wk bf16 [64, 3, 7, 7] channels-last (memory
+    [64][7][7][3], the parameter store's filter copy)."""
+    _dev_check(X, Wk, Y)
+    _stem_check(X, "stem_conv_fwd")
+    n, _, h, w = X.shape
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    if (tuple(Wk.shape) != (64, 3, 7, 7) or Wk.dtype != torch.bfloat16
+            or not Wk.is_contiguous(memory_format=torch.channels_last)):
+        raise N.NativeError("stem_conv_fwd: Wk must be channels-last bf16 [64, 3, 7, 7]")
+    if (tuple(Y.shape) != (n, 64, ho, wo) or Y.dtype != torch.bfloat16
+            or not Y.is_contiguous(memory_format=torch.channels_last)):
+        raise N.NativeError(f"stem_conv_fwd: Y must be channels-last bf16 [{n}, 64, {ho}, {wo}]")
+    N.call("mmu_stem_conv_fwd", _ptr(X), _ptr(Wk), _ptr(Y), n, h, w, _stream(X))
+
+
+def stem_conv_wgrad(dY, X, dW, accumulate=False):
+    """dW (+)= the stem conv's filter gradient: dY [N, 64, Ho, Wo] and X [N, 3, H, W]
+    channels-last bf16, dW f32 [64, 3, 7, 7] channels-last."""
+    _dev_check(dY, X, dW)
+    _stem_check(X, "stem_conv_wgrad")
+    n, _, h, w = X.shape
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    if (tuple(dY.shape) != (n, 64, ho, wo) or dY.dtype != torch.bfloat16
+            or not dY.is_contiguous(memory_format=torch.channels_last)):
+        raise N.NativeError(f"stem_conv_wgrad: dY must be channels-last bf16 [{n}, 64, {ho}, {wo}]")
+    if (tuple(dW.shape) != (64, 3, 7, 7) or dW.dtype != torch.float32
+            or not dW.is_contiguous(memory_format=torch.channels_last)):
+        raise N.NativeError("stem_conv_wgrad: dW must be channels-last f32 [64, 3, 7, 7]")
+    need = N.load().mmu_stem_conv_wgrad_ws_floats(n, h, w)
+    ws = _splitk_workspace(X.device)
+    if need < 0 or ws.numel() < need:
+        raise N.NativeError(f"stem_conv_wgrad: workspace of {ws.numel()} floats, needs {need}")
+    N.call("mmu_stem_conv_wgrad", _ptr(dY), _ptr(X), _ptr(dW), n, h, w, int(bool(accumulate)), _ptr(ws), ws.numel(),
+           _stream(X))
+
+
 def conv3x3_wgrad(dY, X, dW, accumulate=False):
     """dW (+)= weight gradient of a 3x3 / stride 1 / pad 1 conv: X [N, Cin, H, W] and dY
     [N, Cout, H, W] channels-last bf16, dW f32 [Cout, Cin, 3, 3] channels-last (memory

@@ -275,7 +275,9 @@ class ImageEncoder(nn.Module):
     def trunk(self, x):
         train_params = any(p.requires_grad for p in self.model.parameters())
         grad = torch.is_grad_enabled() and (train_params or x.requires_grad)
-        x = x.contiguous(memory_format=torch.channels_last)
+        # bf16 trunk: the image is cast once here (what autocast would do inside the stem conv),
+        # so the stem runs on mmu_stem_conv_* with the store's bf16 filter copy
+        x = x.to(torch.bfloat16 if self.precision == "bf16" else x.dtype, memory_format=torch.channels_last)
         with torch.set_grad_enabled(grad), torch.autocast("cuda", dtype=torch.bfloat16,
                                                           enabled=self.precision == "bf16"):
             return self.model(x)

@@ -105,6 +105,12 @@ class BatchNorm2d(nn.BatchNorm2d):
         return torch.relu(y) if relu else y
 
 
+def _is_stem(w16, stride, padding):
+    """the ResNet stem conv (7x7, stride 2, pad 3, 3 -> 64): forward and filter gradient on
+    mmu_stem_conv_* (its data gradient is never needed: the image is a leaf input)"""
+    return (tuple(w16.shape) == (64, 3, 7, 7) and tuple(stride) == (2, 2) and tuple(padding) == (3, 3))
+
+
 class _ConvBF16(torch.autograd.Function):
     """Conv2d on the bf16 filter copy kept by the parameter store (updated by the fused
     optimizer), so no per-step autocast cast of the f32 filter; the backward adds MIOpen's
@@ -116,6 +122,12 @@ class _ConvBF16(torch.autograd.Function):
         ctx.save_for_backward(x, w16)
         ctx.w, ctx.conf, ctx.flipped = w, (stride, padding), flipped
         cout = w16.shape[0]
+        if _is_stem(w16, stride, padding):  # the 7x7 / 2 stem: mmu_stem_conv_fwd
+            n, _, h, wd = x.shape
+            y = torch.empty((n, cout, (h - 1) // 2 + 1, (wd - 1) // 2 + 1), dtype=x.dtype, device=x.device,
+                            memory_format=torch.channels_last)
+            K.stem_conv_fwd(x, w16, y)
+            return y
         if _is_3x3_s1(w16, stride, padding) and _mmu_3x3(x.shape[1], cout, x.shape[0] * x.shape[2] * x.shape[3])[0]:
             y = torch.empty((x.shape[0], cout, x.shape[2], x.shape[3]), dtype=x.dtype, device=x.device,
                             memory_format=torch.channels_last)
@@ -132,8 +144,11 @@ class _ConvBF16(torch.autograd.Function):
         cl = torch.channels_last
         # 3x3 stride-1 filter gradients: one implicit-im2col MFMA GEMM straight into the f32
         # gradient (mmu_conv3x3_wgrad) instead of MIOpen's wrw + a zero fill + an add pass
-        mmu_w = (need_w and tuple(w16.shape[2:]) == (3, 3) and tuple(stride) == (1, 1) and tuple(padding) == (1, 1)
-                 and _mmu_3x3_wgrad(x.shape[1], w16.shape[0], x.shape[0] * x.shape[2] * x.shape[3]))
+        stem = _is_stem(w16, stride, padding)
+        mmu_w = need_w and (stem or (tuple(w16.shape[2:]) == (3, 3) and tuple(stride) == (1, 1)
+                                     and tuple(padding) == (1, 1)
+                                     and _mmu_3x3_wgrad(x.shape[1], w16.shape[0], x.shape[0] * x.shape[2] * x.shape[3])))
+        wgrad = K.stem_conv_wgrad if stem else K.conv3x3_wgrad
         # its data gradient: the same implicit GEMM on dY with the flipped filter, [Cin][3][3][Cout]
         mmu_x = (need_x and _is_3x3_s1(w16, stride, padding)
                  and _mmu_3x3(x.shape[1], w16.shape[0], x.shape[0] * x.shape[2] * x.shape[3])[1])
@@ -150,10 +165,10 @@ class _ConvBF16(torch.autograd.Function):
         if mmu_w:
             g = ctx.w.grad
             if g is not None and g.dtype == torch.float32 and g.is_contiguous(memory_format=cl):
-                K.conv3x3_wgrad(dy, x, g, accumulate=True)
+                wgrad(dy, x, g, accumulate=True)
             else:
                 rw = torch.empty(w16.shape, dtype=torch.float32, device=x.device, memory_format=cl)
-                K.conv3x3_wgrad(dy, x, rw, accumulate=False)
+                wgrad(dy, x, rw, accumulate=False)
                 if g is not None:
                     g.add_(rw)
                     rw = None

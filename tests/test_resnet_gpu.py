@@ -76,6 +76,34 @@ def test_conv3x3_wgrad_matches_torch(dev, n, cin, cout, h, w):
     assert (dw2 - ref).abs().max().item() <= 1e-3 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("n,h,w", [(2, 224, 224), (3, 37, 53), (1, 7, 130), (5, 16, 16)])
+def test_stem_conv_matches_torch(dev, n, h, w):
+    """mmu_stem_conv_fwd / _wgrad (the 7x7 / stride-2 / pad-3 stem, 3 -> 64, LDS patch +
+    16x16x32 MFMAs over taps padded to 4 channels) against torch's fp32 conv and conv weight
+    gradient on the same bf16 inputs: full 224 images, odd sizes (partial column tiles, odd
+    output rows), a single output row pair; accumulate and store."""
+    from src import kernels as K
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(h * w + n)
+    x = torch.randn(n, 3, h, w, generator=g, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    wt = (torch.randn(64, 3, 7, 7, generator=g, device=dev) * 0.1).to(torch.bfloat16).contiguous(memory_format=cl)
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    y = torch.full((n, 64, ho, wo), 7.0, dtype=torch.bfloat16, device=dev).contiguous(memory_format=cl)
+    K.stem_conv_fwd(x, wt, y)
+    ref = torch.nn.functional.conv2d(x.float(), wt.float(), stride=2, padding=3)
+    assert y.shape == ref.shape
+    assert (y.float() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
+    _close(y.float(), ref, "stem fwd", frac=5e-3)
+    dy = torch.randn(n, 64, ho, wo, generator=g, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    rdw = torch.nn.grad.conv2d_weight(x.float(), (64, 3, 7, 7), dy.float(), stride=2, padding=3)
+    dw = torch.full((64, 3, 7, 7), 0.5, device=dev).contiguous(memory_format=cl)
+    K.stem_conv_wgrad(dy, x, dw, accumulate=True)
+    _close(dw - 0.5, rdw, "stem dW accumulate", frac=1e-4)
+    dw2 = torch.empty((64, 3, 7, 7), device=dev).contiguous(memory_format=cl)
+    K.stem_conv_wgrad(dy, x, dw2)
+    assert (dw2 - rdw).abs().max().item() <= 1e-3 * rdw.abs().max().item()
+
+
 @pytest.mark.parametrize("n,cin,cout,h,w", [(2, 256, 256, 14, 14), (3, 512, 512, 7, 13), (4, 64, 384, 9, 11),
                                              (16, 256, 256, 14, 14)])
 def test_conv3x3_implicit_matches_torch(dev, n, cin, cout, h, w):
@@ -158,7 +186,7 @@ def test_stem_maxpool_matches_torch(dev, shape):
 
 def test_model_grads_with_mmu_1x1_match_miopen(dev, monkeypatch):
     """Whole small MMBT (bf16 trunk, the bench precision) at batch 64: every ResNet weight
-    gradient with the 1x1 products on mmu_gemm -- through the parameter store's bf16
+    gradient with the stem conv on mmu_stem_conv_* and the 1x1 products on mmu_gemm -- through the parameter store's bf16
     filter copies and channels-last f32 gradient views (layer3/4 dW at 14x14 and 7x7,
     dX, the 28x28 forward) -- against the all-MIOpen path, both measured against the fp32 trunk (_no_worse)."""
     from oracle.weights import SMALL, make_state_dict
@@ -186,6 +214,7 @@ def test_model_grads_with_mmu_1x1_match_miopen(dev, monkeypatch):
     monkeypatch.setattr(R, "_mmu_1x1", lambda *a: (False, False, False))
     monkeypatch.setattr(R, "_mmu_3x3_wgrad", lambda *a: False)
     monkeypatch.setattr(R, "_mmu_3x3", lambda *a: (False, False))
+    monkeypatch.setattr(R, "_is_stem", lambda *a: False)
     l0, g0 = grads()
     lr, gr = grads("fp32")                          # the trunk in fp32: the truth for both
     assert abs(l1 - lr) <= 1e-2 * abs(lr)

@@ -1,7 +1,7 @@
 """Run ONE hot kernel of the bench workload a few times, for rocprofv3 PMC passes
 (counters per dispatch; no timing of its own).
 
-  python tools/kprof.py attn_fwd|attn_bwd|gemm_w1|gemm_qkv|gemm_dz|gemm_wgrad|ln_fwd|ln_bwd|bn_fwd|bn_bwd
+  python tools/kprof.py attn_fwd|attn_bwd|gemm_w1|gemm_qkv|gemm_dz|gemm_wgrad|ln_fwd|ln_bwd|bn_fwd|bn_bwd|stem_fwd|stem_wgrad
                         [--reps 3]
 """
 import argparse
@@ -55,6 +55,15 @@ def main():
         pw, pb, pbias = (torch.empty(P, HID, device=dev) for _ in range(3))
         fn = (lambda: K.layernorm_fwd_f32(S, w, b, Y, None, mean, rstd)) if a.which == "ln_fwd" else \
             (lambda: K.layernorm_bwd(dY, S, mean, rstd, w, dX, dXd, 0.1, 5, pw, pb, pbias))  # noqa: E731
+    elif a.which.startswith("stem_"):  # the ResNet stem conv (7x7 / 2, 3 -> 64) on 224 x 224 images
+        cl = torch.channels_last
+        x = torch.randn(B, 3, 224, 224, generator=g, device=dev).to(bf).contiguous(memory_format=cl)
+        wt = (torch.randn(64, 3, 7, 7, generator=g, device=dev) * 0.1).to(bf).contiguous(memory_format=cl)
+        y = torch.empty(B, 64, 112, 112, dtype=bf, device=dev).contiguous(memory_format=cl)
+        dy = torch.randn(B, 64, 112, 112, generator=g, device=dev).to(bf).contiguous(memory_format=cl)
+        dw = torch.zeros(64, 3, 7, 7, device=dev).contiguous(memory_format=cl)
+        fn = (lambda: K.stem_conv_fwd(x, wt, y)) if a.which == "stem_fwd" else \
+            (lambda: K.stem_conv_wgrad(dy, x, dw, accumulate=True))  # noqa: E731
     elif a.which.startswith("bn_"):  # layer3 bn3 (+ skip, ReLU): [B*14*14, 1024] channels-last
         Nb, C, H = B, 1024, 14
         cl = torch.channels_last

@@ -15,7 +15,8 @@ from collections import defaultdict
 CATS = [
     ("mmu GEMM (BERT layers + ResNet 1x1 / 3x3 convs)", r"mmu::gemm_|gemm_(small|big)_kernel|mmu::splitk"),
     ("mmu attention", r"mmu::attn_|mmu::seqattn_"),
-    ("mmu LayerNorm", r"mmu::ln_|ln_fwd_kernel|ln_fwd2_kernel|ln_bwd_kernel"),
+    ("mmu LayerNorm", r"mmu::ln_|ln_fwd_kernel|ln_fwd2_kernel|ln_fwd32_kernel|ln_bwd_kernel|ln_bwd_res"),
+    ("mmu stem conv (7x7 / 2)", r"mmu::stem_|stem_(fwd|wgrad)"),
     ("mmu embed / pool", r"mmu::embed|mmu::row_pool|embed_fwd_kernel|embed_bwd"),
     ("mmu BertAdam", r"mmu::adam"),
     ("mmu BatchNorm (ResNet)", r"mmu::bn_|bn_(stats|apply|bwd)"),
