@@ -280,6 +280,20 @@ int mmu_conv3x3_wgrad(const void* dY, const void* X, float* dW, int64_t n_img, i
 int mmu_conv3x3_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W,
                          int64_t C, int64_t N, float* ws, int64_t ws_floats, mmu_stream_t stream);
 
+/* The same two products for the strided convs of the ResNet-152 trunk (the first block of
+ * layer2..4: Bottleneck.conv2 3x3 / stride 2 / pad 1 and the downsample 1x1 / stride 2,
+ * src/mmbt.py:19-21): ksize 3 (pad 1) or 1 (pad 0), any stride 1..4; X [n_img*H*W, C] the
+ * input map, Y / dY [n_img*Ho*Wo, N] with Ho = (H + 2 pad - ksize) / stride + 1 (Wo alike).
+ * mmu_conv_implicit: forward (Wk [N][ksize][ksize][C]), C % 64 == 0, N % 64 == 0.
+ * mmu_conv_wgrad: filter gradient dW f32 [Cout][ksize][ksize][Cin], Cin % 256 == 0,
+ * Cout % 128 == 0.  mmu_conv3x3_* above are (ksize 3, stride 1) of these. */
+int mmu_conv_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
+                      int64_t N, int64_t ksize, int64_t stride, float* ws, int64_t ws_floats,
+                      mmu_stream_t stream);
+int mmu_conv_wgrad(const void* dY, const void* X, float* dW, int64_t n_img, int64_t H, int64_t W, int64_t Cin,
+                   int64_t Cout, int64_t ksize, int64_t stride, int accumulate, float* ws, int64_t ws_floats,
+                   mmu_stream_t stream);
+
 /* ResNet-152 stem convolution, 7x7 / stride 2 / pad 3, 3 -> 64 channels (torchvision resnet
  * child 0, the image encoder's conv embed: src/mmbt.py:19-21,42), on channels-last bf16:
  * X [n_img, H, W, 3], Wk [64][7][7][3] (the channels-last filter), Y [n_img, Ho, Wo, 64] with

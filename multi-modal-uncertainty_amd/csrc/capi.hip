@@ -439,30 +439,49 @@ int mmu_row_pool_bwd(const float* dout, int64_t B, int64_t Hh, int64_t Ww, int64
   return check_launch("mmu_row_pool_bwd");
 }
 
-int mmu_conv3x3_wgrad(const void* dY, const void* X, float* dW, int64_t n_img, int64_t H, int64_t W, int64_t Cin,
-                      int64_t Cout, int accumulate, float* ws, int64_t ws_floats, mmu_stream_t stream) {
-  if (!dY || !X || !dW) return fail("mmu_conv3x3_wgrad: null pointer");
-  if (n_img <= 0 || H <= 0 || W <= 0 || Cin % 256 || Cout % 128 || Cin <= 0 || Cout <= 0)
-    return fail("mmu_conv3x3_wgrad: needs Cin %% 256 == 0, Cout %% 128 == 0 (Cin=%ld Cout=%ld)", Cin, Cout);
-  const int64_t K = n_img * H * W;
-  if (K >= (1 << 24) || 2 * (K + 64) * Cin >= (1ll << 31) || 2 * (K + 64) * Cout >= (1ll << 31))
-    return fail("mmu_conv3x3_wgrad: map too large for 32-bit buffer offsets");
+// conv geometry shared by the gathered conv products: ksize 3 (pad 1) or 1 (pad 0), stride >= 1
+static int conv_geometry(GemmParams& p, int64_t n_img, int64_t H, int64_t W, int64_t C, int64_t ks, int64_t st,
+                         int64_t& Mo, const char* who) {
+  if (n_img <= 0 || H <= 0 || W <= 0 || C <= 0 || (ks != 1 && ks != 3) || st < 1 || st > 4)
+    return fail("%s: bad geometry (n=%ld H=%ld W=%ld C=%ld ksize=%ld stride=%ld)", who, n_img, H, W, C, ks, st);
+  const int64_t pad = ks / 2, Ho = (H + 2 * pad - ks) / st + 1, Wo = (W + 2 * pad - ks) / st + 1;
+  const int64_t in_bytes = 2 * n_img * H * W * C;
+  if (in_bytes >= 0x7FFF0000ll) return fail("%s: input map too large for 32-bit buffer offsets", who);
+  p.conv_h = (int)H; p.conv_w = (int)W; p.conv_c = (int)C;
+  p.conv_ho = (int)Ho; p.conv_wo = (int)Wo; p.conv_ks = (int)ks; p.conv_s = (int)st; p.conv_pad = (int)pad;
+  p.conv_in_bytes = in_bytes;
+  Mo = n_img * Ho * Wo;
+  return 0;
+}
+
+int mmu_conv_wgrad(const void* dY, const void* X, float* dW, int64_t n_img, int64_t H, int64_t W, int64_t Cin,
+                   int64_t Cout, int64_t ksize, int64_t stride, int accumulate, float* ws, int64_t ws_floats,
+                   mmu_stream_t stream) {
+  if (!dY || !X || !dW) return fail("mmu_conv_wgrad: null pointer");
+  if (Cin % 256 || Cout % 128 || Cin <= 0 || Cout <= 0)
+    return fail("mmu_conv_wgrad: needs Cin %% 256 == 0, Cout %% 128 == 0 (Cin=%ld Cout=%ld)", Cin, Cout);
   GemmParams p{};
-  p.A = (const bf16*)dY; p.lda = Cout;  // A = dY^T: M-major [K pixels][Cout]
-  p.B = (const bf16*)X; p.ldb = Cin;    // B gathered: [K pixels][9 Cin]
-  p.C = dW; p.ldc = 9 * Cin;            // dW [Cout][3][3][Cin] f32 (channels-last filter)
-  p.M = Cout; p.N = 9 * Cin; p.K = K;
-  p.conv_h = (int)H; p.conv_w = (int)W; p.conv_c = (int)Cin;
+  int64_t K;
+  if (conv_geometry(p, n_img, H, W, Cin, ksize, stride, K, "mmu_conv_wgrad")) return 1;
+  if (K >= (1 << 24) || 2 * (K + 64) * Cout >= (1ll << 31))
+    return fail("mmu_conv_wgrad: map too large for 32-bit buffer offsets");
+  const int64_t T = ksize * ksize;
+  p.A = (const bf16*)dY; p.lda = Cout;  // A = dY^T: M-major [K out pixels][Cout]
+  p.B = (const bf16*)X; p.ldb = Cin;    // B gathered: [K out pixels][T Cin]
+  p.C = dW; p.ldc = T * Cin;            // dW [Cout][ks][ks][Cin] f32 (channels-last filter)
+  p.M = Cout; p.N = T * Cin; p.K = K;
   p.tiles_m = (int)((Cout + 255) / 256);
-  p.tiles_n = (int)(9 * Cin / 256);
+  p.tiles_n = (int)(T * Cin / 256);
   p.group_m = 1;
   p.kind = MMU_EPI_STORE;
   p.accumulate = accumulate;
   // split-K over the pixels (few output tiles): ~640 blocks, >= 1024 pixels per slice
   const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
   int64_t want = (640 + tiles - 1) / tiles;
-  if (want > K / 1024) want = K / 1024;
-  if (want > 32) want = 32;
+  // (the 2-tile 1x1 downsample, Cin 256 -> Cout 512: up to 128 slices of >= 256 pixels)
+  const bool few = tiles <= 4;
+  if (want > K / (few ? 256 : 1024)) want = K / (few ? 256 : 1024);
+  if (want > (few ? 128 : 32)) want = few ? 128 : 32;
   if (ws && want > ws_floats / (p.M * p.N)) want = ws_floats / (p.M * p.N);
   p.splitk = 1;
   p.kchunk = K;
@@ -473,7 +492,12 @@ int mmu_conv3x3_wgrad(const void* dY, const void* X, float* dW, int64_t n_img, i
     p.ws = ws;
   }
   conv3x3_wgrad_launch(p, (hipStream_t)stream);
-  return check_launch("mmu_conv3x3_wgrad");
+  return check_launch("mmu_conv_wgrad");
+}
+
+int mmu_conv3x3_wgrad(const void* dY, const void* X, float* dW, int64_t n_img, int64_t H, int64_t W, int64_t Cin,
+                      int64_t Cout, int accumulate, float* ws, int64_t ws_floats, mmu_stream_t stream) {
+  return mmu_conv_wgrad(dY, X, dW, n_img, H, W, Cin, Cout, 3, 1, accumulate, ws, ws_floats, stream);
 }
 
 static int stem_params(StemParams& p, int64_t n_img, int64_t H, int64_t W, const char* who) {
@@ -513,24 +537,25 @@ int mmu_stem_conv_wgrad(const void* dY, const void* X, float* dW, int64_t n_img,
   return check_launch("mmu_stem_conv_wgrad");
 }
 
-int mmu_conv3x3_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
-                         int64_t N, float* ws, int64_t ws_floats, mmu_stream_t stream) {
-  if (!X || !Wk || !Y) return fail("mmu_conv3x3_implicit: null pointer");
-  if (n_img <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 64 || N % 64)
-    return fail("mmu_conv3x3_implicit: needs C %% 64 == 0, N %% 64 == 0 (C=%ld N=%ld)", C, N);
-  const int64_t M = n_img * H * W;
-  if (M < 256 || 2 * (M + 256) * C >= (1ll << 31) || 2 * (N + 256) * 9 * C >= (1ll << 31))
-    return fail("mmu_conv3x3_implicit: map size out of range");
+int mmu_conv_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
+                      int64_t N, int64_t ksize, int64_t stride, float* ws, int64_t ws_floats, mmu_stream_t stream) {
+  if (!X || !Wk || !Y) return fail("mmu_conv_implicit: null pointer");
+  if (C % 64 || N % 64 || N <= 0)
+    return fail("mmu_conv_implicit: needs C %% 64 == 0, N %% 64 == 0 (C=%ld N=%ld)", C, N);
+  GemmParams p{};
+  int64_t M;
+  if (conv_geometry(p, n_img, H, W, C, ksize, stride, M, "mmu_conv_implicit")) return 1;
+  const int64_t T = ksize * ksize;
+  if (M < 256 || 2 * (M + 256) * N >= (1ll << 31) || 2 * (N + 256) * T * C >= (1ll << 31))
+    return fail("mmu_conv_implicit: map size out of range");
   // 256x256 tiles (LDS-DMA gather) for N >= 256 with N % 128 == 0; 128x128 register-staged
   // tiles for the narrow convs (N = 64 / 128 / ...)
   const bool small = N < 256 || N % 128;
   const int tm_ = small ? 128 : 256, tn_ = small ? 128 : 256;
-  GemmParams p{};
-  p.A = (const bf16*)X; p.lda = C;       // A gathered: [M pixels][9 C]
-  p.B = (const bf16*)Wk; p.ldb = 9 * C;  // B K-major [N][9 C]
+  p.A = (const bf16*)X; p.lda = C;       // A gathered: [M out pixels][T C]
+  p.B = (const bf16*)Wk; p.ldb = T * C;  // B K-major [N][T C]
   p.C = Y; p.ldc = N;                    // Y [M pixels][N] bf16
-  p.M = M; p.N = N; p.K = 9 * C;
-  p.conv_h = (int)H; p.conv_w = (int)W; p.conv_c = (int)C;
+  p.M = M; p.N = N; p.K = T * C;
   p.tiles_m = (int)((M + tm_ - 1) / tm_);
   p.tiles_n = (int)((N + tn_ - 1) / tn_);
   p.group_m = 1;
@@ -552,7 +577,12 @@ int mmu_conv3x3_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, 
     }
   }
   conv3x3_implicit_launch(p, small, (hipStream_t)stream);
-  return check_launch("mmu_conv3x3_implicit");
+  return check_launch("mmu_conv_implicit");
+}
+
+int mmu_conv3x3_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
+                         int64_t N, float* ws, int64_t ws_floats, mmu_stream_t stream) {
+  return mmu_conv_implicit(X, Wk, Y, n_img, H, W, C, N, 3, 1, ws, ws_floats, stream);
 }
 
 int64_t mmu_batchnorm_ws_bytes(int64_t C) { return batchnorm_ws_bytes(C); }

@@ -401,8 +401,8 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(GemmParams p) {
   epilogue_block<EPI, OUT_F32, 4>(p, z, slice, m0 + 64 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
 }
 
-// ---------------------------------------------------------------- 3x3 conv, 128x128 tiles
-// The implicit-im2col forward / data-gradient product of a 3x3 / stride-1 / pad-1 conv with
+// ---------------------------------------------------------------- conv, 128x128 tiles
+// The implicit-im2col forward / data-gradient product of a 3x3 or 1x1 (any stride) conv with
 // FEW output channels (64 / 128: ResNet layer1 / layer2 conv2), on the small kernel's 128x128
 // tiles, 4 waves, register staging: the A rows (output pixels) are gathered per tap while
 // they are loaded (16 B per lane, padding and rows past M read as zero); B = the filter
@@ -410,13 +410,13 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(GemmParams p) {
 // wave block is all in or all out: N = 64 runs half the tile's columns).  Split-K over
 // (tap, channel) steps into f32 slabs as the 256x256 conv kernel does.
 struct ConvRows4 {
-  int base[4], h[4], w[4];  // img * H (-1: row past M), h, w of the thread's 4 rows
+  int base[4], h[4], w[4];  // img * H (-1: row past M), input h, w of tap (0, 0) of the thread's 4 rows
 };
 static __device__ __forceinline__ void conva_g_load(uint4 (&r)[4], const bf16* __restrict__ X, const GemmParams& p,
                                                     const ConvRows4& cr, int64_t k0, int t) {
   const int H = p.conv_h, W = p.conv_w, C = p.conv_c;
   const int tap = (int)(k0 / C), ci0 = (int)(k0 - (int64_t)tap * C);
-  const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+  const int dh = tap / p.conv_ks, dw = tap - dh * p.conv_ks;
   const bool kin = k0 < p.K;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -436,14 +436,15 @@ __global__ __launch_bounds__(256) void gemm_conva_small_kernel(GemmParams p) {
   const int64_t m0 = (int64_t)tm * SBM, n0 = (int64_t)tn * SBN;
   ConvRows4 cr;
   {
-    const int H = p.conv_h, W = p.conv_w, HW = H * W;
+    const int Wo = p.conv_wo, HWo = p.conv_ho * Wo;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t pix = m0 + (t >> 3) + 32 * i;  // g_load<true>'s row of piece i
-      const int img = (int)(pix / HW), rem = (int)(pix - (int64_t)img * HW);
-      cr.base[i] = pix < p.M ? img * H : -1;
-      cr.h[i] = rem / W;
-      cr.w[i] = rem - cr.h[i] * W;
+      const int img = (int)(pix / HWo), rem = (int)(pix - (int64_t)img * HWo);
+      const int ho = rem / Wo;
+      cr.base[i] = pix < p.M ? img * p.conv_h : -1;
+      cr.h[i] = ho * p.conv_s - p.conv_pad;
+      cr.w[i] = (rem - ho * Wo) * p.conv_s - p.conv_pad;
     }
   }
   f32x4 acc[4][4];
@@ -520,14 +521,15 @@ static __device__ __forceinline__ void dma_tile(char* s, __amdgpu_buffer_rsrc_t 
   }
 }
 
-// B tile (64 k-rows = pixels x 256 n = one tap's channels ci0..ci0+255) of the 3x3 conv
+// B tile (64 k-rows = output pixels x 256 n = one tap's channels ci0..ci0+255) of the conv
 // weight gradient, gathered from the NHWC map (rsrc): pixel (img, h, w) reads the input
 // pixel (h + dh, w + dw) of the block's tap; padding (and pixels >= K) read as zero through
 // an offset past the buffer's range.  Same lane-linear LDS image as dma_tile<false>.
 static __device__ __forceinline__ void dma_tile_convb(char* s, __amdgpu_buffer_rsrc_t rsrc, const GemmParams& p,
                                                       int dh, int dw, int64_t ci0, int64_t k0, int w, int l) {
-  const int H = p.conv_h, W = p.conv_w, HW = H * W, C = p.conv_c;
-  const float rhw = 1.0f / (float)HW, rw = 1.0f / (float)W;
+  const int H = p.conv_h, W = p.conv_w, C = p.conv_c, s_ = p.conv_s;
+  const int Wo = p.conv_wo, HW = p.conv_ho * Wo;
+  const float rhw = 1.0f / (float)HW, rw = 1.0f / (float)Wo;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int piece = w * 4 + i;
@@ -539,10 +541,10 @@ static __device__ __forceinline__ void dma_tile_convb(char* s, __amdgpu_buffer_r
     int rem = pix - img * HW;
     if (rem < 0) { --img; rem += HW; } else if (rem >= HW) { ++img; rem -= HW; }
     int hh = (int)((float)rem * rw);
-    int ww = rem - hh * W;
-    if (ww < 0) { --hh; ww += W; } else if (ww >= W) { ++hh; ww -= W; }
-    hh += dh;
-    ww += dw;
+    int ww = rem - hh * Wo;
+    if (ww < 0) { --hh; ww += Wo; } else if (ww >= Wo) { ++hh; ww -= Wo; }
+    hh = hh * s_ + dh;
+    ww = ww * s_ + dw;
     const bool ok = pix < p.K && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
     const uint32_t src = ok ? (uint32_t)(((((int64_t)img * H + hh) * W + ww) * C + ci0 + 16 * b + 8 * (j & 1)) * 2)
                             : 0x7FFFFFF0u;
@@ -550,25 +552,27 @@ static __device__ __forceinline__ void dma_tile_convb(char* s, __amdgpu_buffer_r
   }
 }
 
-// A tile (256 rows = output pixels x 64 k = channels ci0..ci0+63 of one tap) of a 3x3 /
-// stride-1 / pad-1 convolution as an implicit GEMM, gathered from the NHWC map (rsrc): row
-// pixel (img, h, w) reads input pixel (h + dh, w + dw); padding and rows >= M read as zero.
+// A tile (256 rows = output pixels x 64 k = channels ci0..ci0+63 of one tap) of a 3x3 or
+// 1x1 convolution as an implicit GEMM, gathered from the NHWC map (rsrc): output pixel
+// (img, ho, wo) reads input pixel (s ho - pad + dh, s wo - pad + dw) of tap (dh, dw);
+// padding and rows >= M read as zero.
 // Each lane's 4 rows are fixed for the block (pbase / ph / pw, from conv_rows_init); only
 // the tap and channel offset move with k.  Same lane-linear LDS image as dma_tile<true>.
 struct ConvRows {
-  int base[4], h[4], w[4];  // img * H (-1: row past M), h, w of the lane's rows
+  int base[4], h[4], w[4];  // img * H (-1: row past M), input h, w of tap (0, 0) of the lane's rows
 };
 static __device__ __forceinline__ ConvRows conv_rows_init(const GemmParams& p, int64_t m0, int w, int l) {
   ConvRows r;
-  const int H = p.conv_h, W = p.conv_w, HW = H * W;
+  const int Wo = p.conv_wo, HWo = p.conv_ho * Wo;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = (w * 4 + i) * 8 + (l >> 3);
     const int64_t pix = m0 + row;
-    const int img = (int)(pix / HW), rem = (int)(pix - (int64_t)img * HW);
-    r.base[i] = pix < p.M ? img * H : -1;
-    r.h[i] = rem / W;
-    r.w[i] = rem - r.h[i] * W;
+    const int img = (int)(pix / HWo), rem = (int)(pix - (int64_t)img * HWo);
+    const int ho = rem / Wo;
+    r.base[i] = pix < p.M ? img * p.conv_h : -1;
+    r.h[i] = ho * p.conv_s - p.conv_pad;
+    r.w[i] = (rem - ho * Wo) * p.conv_s - p.conv_pad;
   }
   return r;
 }
@@ -576,7 +580,7 @@ static __device__ __forceinline__ void dma_tile_conva(char* s, __amdgpu_buffer_r
                                                       const ConvRows& r, int64_t k0, int w, int l) {
   const int H = p.conv_h, W = p.conv_w, C = p.conv_c;
   const int tap = (int)(k0 / C), ci0 = (int)(k0 - (int64_t)tap * C);
-  const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+  const int dh = tap / p.conv_ks, dw = tap - dh * p.conv_ks;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int piece = w * 4 + i;
@@ -588,8 +592,8 @@ static __device__ __forceinline__ void dma_tile_conva(char* s, __amdgpu_buffer_r
   }
 }
 
-// GATHER = 1: the 3x3 conv weight-gradient product (B gathered by dma_tile_convb);
-// GATHER = 2: the 3x3 conv forward / data-gradient product (A gathered by dma_tile_conva)
+// GATHER = 1: the conv weight-gradient product (B gathered by dma_tile_convb);
+// GATHER = 2: the conv forward / data-gradient product (A gathered by dma_tile_conva)
 template <bool AK, bool BKM, int EPI, bool OUT_F32, int GATHER>
 static __device__ __forceinline__ void gemm_big_body(const GemmParams& p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * B_STAGE];
@@ -602,8 +606,9 @@ static __device__ __forceinline__ void gemm_big_body(const GemmParams& p) {
   block_tile(p, z, slice, tm, tn);
   const int64_t m0 = (int64_t)tm * BBM, n0 = (int64_t)tn * BBN;
   // operand byte ranges: rows (K-major) or k-rows (M/N-major) beyond the operand read as zero
-  const int64_t a_bytes = (AK ? p.M * p.lda : p.K * p.lda) * 2;
-  const int64_t b_bytes = (BKM ? p.N * p.ldb : p.K * p.ldb) * 2;
+  // (gathered conv operands: the whole input map, conv_in_bytes)
+  const int64_t a_bytes = GATHER == 2 ? p.conv_in_bytes : (AK ? p.M * p.lda : p.K * p.lda) * 2;
+  const int64_t b_bytes = GATHER == 1 ? p.conv_in_bytes : (BKM ? p.N * p.ldb : p.K * p.ldb) * 2;
   // (host guarantees both spans < 4 GiB: 32-bit num_records / voffset)
   const __amdgpu_buffer_rsrc_t ra =
       __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + z * p.sA), 0, (int)(uint32_t)a_bytes, 0x00020000);
@@ -621,7 +626,8 @@ static __device__ __forceinline__ void gemm_big_body(const GemmParams& p) {
   const int nk = (int)((ke - kb + BKT - 1) / BKT);
   // conv gather: the block's tap (n0 / C: a 256-column tile lies in one tap) and channels
   const int tap = GATHER == 1 ? (int)(n0 / p.conv_c) : 0;
-  const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+  const int dh = GATHER == 1 ? tap / p.conv_ks - p.conv_pad : 0;
+  const int dw = GATHER == 1 ? tap % p.conv_ks - p.conv_pad : 0;
   const int64_t ci0 = GATHER == 1 ? n0 - (int64_t)tap * p.conv_c : 0;
   auto dma_b = [&](char* d, int64_t k) {
     if (GATHER == 1) dma_tile_convb(d, rb, p, dh, dw, ci0, k, w, l);

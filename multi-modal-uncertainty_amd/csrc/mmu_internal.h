@@ -34,10 +34,12 @@ struct GemmParams {
   int splitk;
   int64_t kchunk;
   float* ws;
-  // 3x3 / stride 1 / pad 1 convolutions on an NHWC map [img * conv_h * conv_w pixels][conv_c]:
-  // weight gradient (gemm_convw_kernel): B[pixel][tap * conv_c + ci] gathered;
-  // forward / data gradient (gemm_conva_kernel): A[pixel][tap * conv_c + c] gathered
-  int conv_h, conv_w, conv_c;
+  // conv_ks x conv_ks (3 or 1) / stride conv_s / pad conv_pad convolutions of an NHWC map
+  // [img * conv_h * conv_w pixels][conv_c] (conv_in_bytes) into conv_ho x conv_wo outputs:
+  // weight gradient (gemm_convw_kernel): B[out pixel][tap * conv_c + ci] gathered;
+  // forward / data gradient (gemm_conva_kernel): A[out pixel][tap * conv_c + c] gathered
+  int conv_h, conv_w, conv_c, conv_ho, conv_wo, conv_ks, conv_s, conv_pad;
+  int64_t conv_in_bytes;
 };
 void conv3x3_wgrad_launch(const GemmParams& p, hipStream_t s);
 void conv3x3_implicit_launch(const GemmParams& p, bool small, hipStream_t s);  // small: 128x128 tiles

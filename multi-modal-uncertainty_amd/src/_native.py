@@ -65,6 +65,10 @@ SIGNATURES = {
     "mmu_row_pool_bwd": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "mmu_conv3x3_implicit": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp]),
     "mmu_conv3x3_wgrad": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp]),
+    "mmu_conv_implicit": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64,
+                                  c_vp]),
+    "mmu_conv_wgrad": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64,
+                               c_vp]),
     "mmu_stem_conv_fwd": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
     "mmu_stem_conv_wgrad_ws_floats": (c_i64, [c_i64, c_i64, c_i64]),
     "mmu_stem_conv_wgrad": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp]),

@@ -329,31 +329,41 @@ def row_pool_bwd(dout, n, dfmap_nhwc):
     N.call("mmu_row_pool_bwd", _ptr(dout), B, Hh, Ww, C, n, _ptr(dfmap_nhwc), _stream(dout))
 
 
-import os as _os
-_CONV_SPLITK = _os.environ.get("MMU_CONV_SPLITK", "1") != "0"  # A/B switch (tools/gpu_r3_splitk_ab.sh)
+def _conv_out(h, w, ksize, stride):
+    pad = ksize // 2
+    return (h + 2 * pad - ksize) // stride + 1, (w + 2 * pad - ksize) // stride + 1
+
+
+def conv_implicit(X, Wk, Y, ksize=3, stride=1):
+    """Y[p, n] = sum_{tap, c} X[input pixel of (p, tap), c] Wk[n, tap * C + c]: a ksize x ksize
+    (3: pad 1, 1: pad 0) / stride conv as one implicit-im2col GEMM.  X [N, C, H, W] and Y
+    [N, Nout, Ho, Wo] channels-last bf16, Wk bf16 with memory [Nout][ksize][ksize][C] (a
+    channels-last [Nout, C, k, k] filter, or the flipped-transposed 3x3 one for dX)."""
+    _dev_check(X, Wk, Y)
+    _want(X, torch.bfloat16, "conv_implicit X")
+    _want(Wk, torch.bfloat16, "conv_implicit Wk")
+    n, c, h, w = X.shape
+    nout = Y.shape[1]
+    ho, wo = _conv_out(h, w, ksize, stride)
+    cl = torch.channels_last
+    # the kernel reads Wk[n][tap * C + c]: either a [Nout, k, k, C] contiguous tensor or a
+    # [Nout, C, k, k] filter whose memory is channels-last (both are [Nout][k][k][C] in memory)
+    k = ksize
+    wk_ok = Wk.dim() == 4 and (
+        (tuple(Wk.shape) == (nout, k, k, c) and Wk.is_contiguous())
+        or (tuple(Wk.shape) == (nout, c, k, k) and Wk.is_contiguous(memory_format=cl)))
+    if (Y.shape != (n, nout, ho, wo) or Y.dtype != torch.bfloat16 or not wk_ok
+            or not X.is_contiguous(memory_format=cl) or not Y.is_contiguous(memory_format=cl)):
+        raise N.NativeError(f"conv_implicit: X channels-last bf16 [N, C, H, W], Y [N, Nout, {ho}, {wo}], "
+                            f"Wk [Nout][{k}][{k}][C] bf16")
+    ws = _splitk_workspace(Y.device)  # split-K slabs for small maps (few tiles)
+    N.call("mmu_conv_implicit", _ptr(X), _ptr(Wk), _ptr(Y), n, h, w, c, nout, ksize, stride, _ptr(ws), ws.numel(),
+           _stream(X))
 
 
 def conv3x3_implicit(X, Wk, Y):
-    """Y[p, n] = sum_{tap, c} X[p + tap shift, c] Wk[n, tap * C + c]: X [N, C, H, W] and Y
-    [N, Nout, H, W] channels-last bf16, Wk bf16 contiguous with Wk.numel() == Nout * 9 * C
-    (a channels-last [Nout, C, 3, 3] filter, or the flipped-transposed one for dX)."""
-    _dev_check(X, Wk, Y)
-    _want(X, torch.bfloat16, "conv3x3_implicit X")
-    _want(Wk, torch.bfloat16, "conv3x3_implicit Wk")
-    n, c, h, w = X.shape
-    nout = Y.shape[1]
-    cl = torch.channels_last
-    # the kernel reads Wk[n][tap * C + c]: either a [Nout, 3, 3, C] contiguous tensor or a
-    # [Nout, C, 3, 3] filter whose memory is channels-last (both are [Nout][3][3][C] in memory)
-    wk_ok = Wk.dim() == 4 and (
-        (tuple(Wk.shape) == (nout, 3, 3, c) and Wk.is_contiguous())
-        or (tuple(Wk.shape) == (nout, c, 3, 3) and Wk.is_contiguous(memory_format=cl)))
-    if (Y.shape != (n, nout, h, w) or Y.dtype != torch.bfloat16 or not wk_ok
-            or not X.is_contiguous(memory_format=cl) or not Y.is_contiguous(memory_format=cl)):
-        raise N.NativeError("conv3x3_implicit: X / Y channels-last bf16 [N, C, H, W], Wk [Nout][3][3][C] bf16")
-    ws = _splitk_workspace(Y.device) if _CONV_SPLITK else None  # split-K slabs for small maps (few tiles)
-    N.call("mmu_conv3x3_implicit", _ptr(X), _ptr(Wk), _ptr(Y), n, h, w, c, nout, _ptr(ws),
-           ws.numel() if ws is not None else 0, _stream(X))
+    """the 3x3 / stride-1 / pad-1 case of conv_implicit (Y and X share H, W)"""
+    conv_implicit(X, Wk, Y, 3, 1)
 
 
 def _stem_check(X, what):
@@ -400,23 +410,30 @@ def stem_conv_wgrad(dY, X, dW, accumulate=False):
            _stream(X))
 
 
-def conv3x3_wgrad(dY, X, dW, accumulate=False):
-    """dW (+)= weight gradient of a 3x3 / stride 1 / pad 1 conv: X [N, Cin, H, W] and dY
-    [N, Cout, H, W] channels-last bf16, dW f32 [Cout, Cin, 3, 3] channels-last (memory
-    [Cout][3][3][Cin]).  Cin % 256 == 0, Cout % 128 == 0."""
+def conv_wgrad(dY, X, dW, ksize=3, stride=1, accumulate=False):
+    """dW (+)= weight gradient of a ksize x ksize (3: pad 1, 1: pad 0) / stride conv: X [N, Cin,
+    H, W] and dY [N, Cout, Ho, Wo] channels-last bf16, dW f32 [Cout, Cin, k, k] channels-last
+    (memory [Cout][k][k][Cin]).  Cin % 256 == 0, Cout % 128 == 0."""
     _dev_check(dY, X, dW)
-    _want(X, torch.bfloat16, "conv3x3_wgrad X")
-    _want(dY, torch.bfloat16, "conv3x3_wgrad dY")
+    _want(X, torch.bfloat16, "conv_wgrad X")
+    _want(dY, torch.bfloat16, "conv_wgrad dY")
     n, cin, h, w = X.shape
     cout = dY.shape[1]
+    ho, wo = _conv_out(h, w, ksize, stride)
     cl = torch.channels_last
-    if (dY.shape != (n, cout, h, w) or dW.shape != (cout, cin, 3, 3) or dW.dtype != torch.float32
+    if (dY.shape != (n, cout, ho, wo) or dW.shape != (cout, cin, ksize, ksize) or dW.dtype != torch.float32
             or not X.is_contiguous(memory_format=cl) or not dY.is_contiguous(memory_format=cl)
             or not dW.is_contiguous(memory_format=cl)):
-        raise N.NativeError("conv3x3_wgrad: X / dY channels-last bf16 [N, C, H, W], dW f32 channels-last [Cout, Cin, 3, 3]")
+        raise N.NativeError(f"conv_wgrad: X channels-last bf16 [N, C, H, W], dY [N, Cout, {ho}, {wo}], "
+                            f"dW f32 channels-last [Cout, Cin, {ksize}, {ksize}]")
     ws = _splitk_workspace(X.device)
-    N.call("mmu_conv3x3_wgrad", _ptr(dY), _ptr(X), _ptr(dW), n, h, w, cin, cout, int(bool(accumulate)), _ptr(ws),
-           ws.numel(), _stream(X))
+    N.call("mmu_conv_wgrad", _ptr(dY), _ptr(X), _ptr(dW), n, h, w, cin, cout, ksize, stride, int(bool(accumulate)),
+           _ptr(ws), ws.numel(), _stream(X))
+
+
+def conv3x3_wgrad(dY, X, dW, accumulate=False):
+    """the 3x3 / stride-1 / pad-1 case of conv_wgrad"""
+    conv_wgrad(dY, X, dW, 3, 1, accumulate)
 
 
 _bn_ws = {}

@@ -128,10 +128,14 @@ class _ConvBF16(torch.autograd.Function):
                             memory_format=torch.channels_last)
             K.stem_conv_fwd(x, w16, y)
             return y
-        if _is_3x3_s1(w16, stride, padding) and _mmu_3x3(x.shape[1], cout, x.shape[0] * x.shape[2] * x.shape[3])[0]:
-            y = torch.empty((x.shape[0], cout, x.shape[2], x.shape[3]), dtype=x.dtype, device=x.device,
-                            memory_format=torch.channels_last)
-            K.conv3x3_implicit(x, w16, y)
+        geo = _conv_geo(w16, stride, padding)
+        ctx.route = route = _mmu_conv(geo, x.shape, cout)
+        if route[0]:
+            ks, st = geo
+            n, _, h, wd = x.shape
+            ho, wo = (h + 2 * (ks // 2) - ks) // st + 1, (wd + 2 * (ks // 2) - ks) // st + 1
+            y = torch.empty((n, cout, ho, wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+            K.conv_implicit(x, w16, y, ks, st)
             return y
         return torch.ops.aten.convolution(x, w16, None, stride, padding, (1, 1), False, (0, 0), 1)
 
@@ -142,16 +146,20 @@ class _ConvBF16(torch.autograd.Function):
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         dy = dy.contiguous(memory_format=torch.channels_last)
         cl = torch.channels_last
-        # 3x3 stride-1 filter gradients: one implicit-im2col MFMA GEMM straight into the f32
-        # gradient (mmu_conv3x3_wgrad) instead of MIOpen's wrw + a zero fill + an add pass
+        # filter gradients: one implicit-im2col MFMA GEMM straight into the f32 gradient
+        # (mmu_conv_wgrad / mmu_stem_conv_wgrad) instead of MIOpen's wrw + a zero fill + an add
         stem = _is_stem(w16, stride, padding)
-        mmu_w = need_w and (stem or (tuple(w16.shape[2:]) == (3, 3) and tuple(stride) == (1, 1)
-                                     and tuple(padding) == (1, 1)
-                                     and _mmu_3x3_wgrad(x.shape[1], w16.shape[0], x.shape[0] * x.shape[2] * x.shape[3])))
-        wgrad = K.stem_conv_wgrad if stem else K.conv3x3_wgrad
-        # its data gradient: the same implicit GEMM on dY with the flipped filter, [Cin][3][3][Cout]
-        mmu_x = (need_x and _is_3x3_s1(w16, stride, padding)
-                 and _mmu_3x3(x.shape[1], w16.shape[0], x.shape[0] * x.shape[2] * x.shape[3])[1])
+        geo = None if stem else _conv_geo(w16, stride, padding)
+        route = (True, False, True) if stem else ctx.route
+        mmu_w = need_w and route[2]
+        if stem:
+            wgrad = K.stem_conv_wgrad
+        else:
+            def wgrad(dy_, x_, dw_, accumulate):
+                K.conv_wgrad(dy_, x_, dw_, geo[0], geo[1], accumulate)
+        # 3x3 / stride-1 data gradient: the same implicit GEMM on dY with the flipped filter,
+        # [Cin][3][3][Cout]
+        mmu_x = need_x and route[1]
         dx = dw = None
         if (need_x and not mmu_x) or (need_w and not mmu_w):
             dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w16, None, stride, padding, (1, 1), False, (0, 0),
@@ -194,32 +202,44 @@ def _rows(t):
     return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
 
 
-_CONV3_WGRAD = os.environ.get("MMU_CONV3_WGRAD", "1") != "0"
+def _conv_geo(w16, stride, padding):
+    """(ksize, stride) of a square 3x3 / pad 1 or 1x1 / pad 0 conv with equal strides (the
+    shapes mmu_conv_implicit / mmu_conv_wgrad take), else None"""
+    k = tuple(w16.shape[2:])
+    if k not in ((3, 3), (1, 1)) or stride[0] != stride[1] or tuple(padding) != (k[0] // 2,) * 2:
+        return None
+    return k[0], stride[0]
 
 
-_CONV3_FWD = os.environ.get("MMU_CONV3_FWD", "1") != "0"
-_CONV3_DX = os.environ.get("MMU_CONV3_DX", "1") != "0"
-
-
-def _is_3x3_s1(w16, stride, padding):
-    return tuple(w16.shape[2:]) == (3, 3) and tuple(stride) == (1, 1) and tuple(padding) == (1, 1)
-
-
-def _mmu_3x3(cin, cout, M):
-    """(forward, data gradient) of a 3x3 / stride-1 conv on mmu_conv3x3_implicit (the MFMA
-    GEMM with the im2col gather in its A-operand DMA) instead of MIOpen: the output channels
-    (Cout forward, Cin for dX) >= 256 and % 128, the reduced ones % 64 (layer3 / layer4 conv2;
-    MMU_CONV3_FWD=0 / MMU_CONV3_DX=0 keep MIOpen for A/B runs)."""
-    fwd = _CONV3_FWD and cin % 64 == 0 and cout % 128 == 0 and cout >= 256 and M >= 256
-    dx = _CONV3_DX and cout % 64 == 0 and cin % 128 == 0 and cin >= 256 and M >= 256
-    return fwd, dx
-
-
-def _mmu_3x3_wgrad(cin, cout, M):
-    """3x3 / stride-1 filter gradients on mmu_conv3x3_wgrad (the MFMA GEMM with the im2col
-    gather in its B-operand DMA) instead of MIOpen: needs Cin % 256 == 0 and Cout % 128 == 0
-    (layer3 / layer4 conv2 of ResNet-152; MMU_CONV3_WGRAD=0 keeps MIOpen for A/B runs)."""
-    return _CONV3_WGRAD and cin % 256 == 0 and cout % 128 == 0 and M >= 1024
+def _mmu_conv(geo, xshape, cout):
+    """(forward, data gradient, filter gradient) of a conv on the gathered-operand MFMA
+    products (mmu_conv_implicit / mmu_conv_wgrad) instead of MIOpen, from same-box timings
+    of both engines (profiles/r3_conv_census_b256.txt, r3_conv_strided.txt):
+      3x3 stride 1: forward for Cout >= 256 (% 128), dX for Cin >= 256 (% 128), dW for
+        Cin % 256 == 0 (layer3 / layer4 conv2);
+      strided 3x3 (layer3 / layer4 conv2 at >= 12544 output pixels: forward and dW) and the
+        1x1 / stride-2 downsample (forward and dW at 12544..50176 output pixels: layer3 /
+        layer4 at batch 256, layer2's forward at batch 32); their dX stays MIOpen's."""
+    if geo is None:
+        return False, False, False
+    ks, st = geo
+    n, cin, h, w = xshape
+    pad = ks // 2
+    M = n * ((h + 2 * pad - ks) // st + 1) * ((w + 2 * pad - ks) // st + 1)
+    if ks == 3 and st == 1:
+        fwd = cin % 64 == 0 and cout % 128 == 0 and cout >= 256 and M >= 256
+        dx = cout % 64 == 0 and cin % 128 == 0 and cin >= 256 and M >= 256
+        dw = cin % 256 == 0 and cout % 128 == 0 and M >= 1024
+        return fwd, dx, dw
+    if st == 1:  # 1x1 stride 1: _Conv1x1
+        return False, False, False
+    if ks == 3:
+        fwd = cin % 64 == 0 and cout % 128 == 0 and cout >= 256 and M >= 12544
+    else:
+        fwd = cin % 64 == 0 and cout % 128 == 0 and 12544 <= M <= 50176
+    # (the 2-tile 256 -> 512 downsample filter gradient only at batch 256's 200 k pixels)
+    dw = cin % 256 == 0 and cout % 128 == 0 and M >= 12544 and (ks == 3 or cin * cout >= 8 * 65536 or M >= 100352)
+    return fwd, False, dw
 
 
 def _mmu_1x1(cin, cout, M, H):

@@ -128,6 +128,37 @@ def test_conv3x3_implicit_matches_torch(dev, n, cin, cout, h, w):
         _close(dx.float(), rdx, "conv dX", frac=5e-3)
 
 
+@pytest.mark.parametrize("n,cin,cout,h,k,s", [(4, 128, 128, 28, 3, 2), (2, 256, 256, 28, 3, 2), (6, 512, 512, 13, 3, 2),
+                                               (8, 64, 64, 16, 3, 2), (5, 256, 512, 15, 1, 2), (16, 512, 1024, 28, 1, 2),
+                                               (8, 1024, 2048, 14, 1, 2)])
+def test_strided_conv_matches_torch(dev, n, cin, cout, h, k, s):
+    """mmu_conv_implicit / mmu_conv_wgrad on the strided convs of ResNet-152 (first block of
+    layer2..4: conv2 3x3 / stride 2 / pad 1, downsample 1x1 / stride 2) against torch's fp32
+    conv and conv weight gradient on the same bf16 inputs: the trunk's shapes, odd maps
+    (partial output rows), the narrow 128x128-tile forward (Cout < 256), split-K filter
+    gradients (many pixels) and unsplit ones (few)."""
+    from src import kernels as K
+    cl = torch.channels_last
+    pad = k // 2
+    g = torch.Generator(device=dev).manual_seed(cin * 7 + h + k)
+    x = torch.randn(n, cin, h, h, generator=g, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    wt = (torch.randn(cout, cin, k, k, generator=g, device=dev) * 0.05).to(torch.bfloat16).contiguous(memory_format=cl)
+    ref = torch.nn.functional.conv2d(x.float(), wt.float(), stride=s, padding=pad)
+    y = torch.full(ref.shape, 3.0, dtype=torch.bfloat16, device=dev).contiguous(memory_format=cl)
+    K.conv_implicit(x, wt, y, k, s)
+    _close(y.float(), ref, "strided conv fwd", frac=5e-3)
+    assert (y.float() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
+    if cin % 256 == 0 and cout % 128 == 0:
+        dy = torch.randn(ref.shape, generator=g, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+        rdw = torch.nn.grad.conv2d_weight(x.float(), wt.shape, dy.float(), stride=s, padding=pad)
+        dw = torch.full(wt.shape, 0.25, device=dev).contiguous(memory_format=cl)
+        K.conv_wgrad(dy, x, dw, k, s, accumulate=True)
+        _close(dw - 0.25, rdw, "strided conv dW accumulate", frac=1e-3)
+        dw2 = torch.empty(wt.shape, device=dev).contiguous(memory_format=cl)
+        K.conv_wgrad(dy, x, dw2, k, s)
+        _close(dw2, rdw, "strided conv dW", frac=1e-3)
+
+
 @pytest.mark.parametrize("cin,width,hw,batch", [(1024, 256, 14, 128), (256, 64, 56, 4)])
 def test_bottleneck_mmu_1x1_matches_miopen(dev, monkeypatch, cin, width, hw, batch):
     from src import resnet as R
@@ -212,8 +243,7 @@ def test_model_grads_with_mmu_1x1_match_miopen(dev, monkeypatch):
 
     l1, g1 = grads()
     monkeypatch.setattr(R, "_mmu_1x1", lambda *a: (False, False, False))
-    monkeypatch.setattr(R, "_mmu_3x3_wgrad", lambda *a: False)
-    monkeypatch.setattr(R, "_mmu_3x3", lambda *a: (False, False))
+    monkeypatch.setattr(R, "_mmu_conv", lambda *a: (False, False, False))
     monkeypatch.setattr(R, "_is_stem", lambda *a: False)
     l0, g0 = grads()
     lr, gr = grads("fp32")                          # the trunk in fp32: the truth for both

@@ -34,8 +34,8 @@ def main():
         M = a.batch * H * H  # the routing rules of src/resnet.py at the train batch
         if k == 1 and s == 1:
             f, d, w = R._mmu_1x1(C, Co, M, H)
-        elif k == 3 and s == 1:
-            (f, d), w = R._mmu_3x3(C, Co, M), R._mmu_3x3_wgrad(C, Co, M)
+        elif k in (1, 3):
+            f, d, w = R._mmu_conv((k, s), (a.batch, C, H, H), Co)
         else:
             f = d = w = False
         shapes[(C, Co, k, s, H, H, f, d, w)] += 1

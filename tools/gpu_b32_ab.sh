@@ -11,5 +11,5 @@ for b in 32 256; do
     echo "$t B=$b $(tail -1 gpurun_out/ab_${t}_$b.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["value"])')"
   done
 done
-timeout -k 10 300 python3 -u -m pytest tests/test_resnet_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t_rn.log 2>&1 || { tail -20 gpurun_out/t_rn.log; exit 1; }
-tail -1 gpurun_out/t_rn.log
+
+
