@@ -18,6 +18,8 @@ makes the compute stream wait before the optimizer step.  Mean = sum / world siz
 import torch
 import torch.distributed as dist
 
+from . import kernels as K
+
 
 class GradBucketer:
     def __init__(self, model, bucket_bytes=64 << 20, group=None):
@@ -137,7 +139,15 @@ class GradBucketer:
             return
         bk = self.buckets[b]
         view = self.store.grad[bk["start"]:bk["end"]]
-        work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        side = K.side_stream_if_any(view.device) if view.is_cuda else None
+        if side is not None:
+            # filter gradients may still be in flight on the side stream (src/resnet.py
+            # _wgrad_run): the all-reduce is issued from it, behind the main stream's work too
+            side.wait_stream(torch.cuda.current_stream(view.device))
+            with torch.cuda.stream(side):
+                work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        else:
+            work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self.pending.append(work)
         self.launched.add(b)
 

@@ -296,20 +296,7 @@ class BertLayerFunction(torch.autograd.Function):
         return (dX,) + (None,) * 12
 
 
-_pending_join = set()
-
-
 def _join_side_at_end(side):
     """Once per backward pass: the main stream waits for the weight-gradient stream when
     the autograd engine finishes, so every consumer of .grad (optimizer, tests) sees them."""
-    key = (side.main.cuda_stream, side.side.cuda_stream)
-    if key in _pending_join:
-        return
-    _pending_join.add(key)
-    main, s = side.main, side.side
-
-    def join():
-        _pending_join.discard(key)
-        main.wait_stream(s)
-
-    torch.autograd.Variable._execution_engine.queue_callback(join)
+    K.join_at_backward_end(side.main, side.side)

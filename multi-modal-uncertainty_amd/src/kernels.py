@@ -80,6 +80,29 @@ def side_stream(dev):
     return s
 
 
+def side_stream_if_any(dev):
+    """the device's side stream if one was created, else None"""
+    return _side.get(torch.device(dev))
+
+
+_pending_join = set()
+
+
+def join_at_backward_end(main, side):
+    """Once per backward pass: ``main`` waits for ``side`` when the autograd engine finishes,
+    so every consumer of .grad (optimizer, all-reduce, tests) sees the side stream's work."""
+    key = (main.cuda_stream, side.cuda_stream)
+    if key in _pending_join:
+        return
+    _pending_join.add(key)
+
+    def join():
+        _pending_join.discard(key)
+        main.wait_stream(side)
+
+    torch.autograd.Variable._execution_engine.queue_callback(join)
+
+
 def gemm(A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, M, N_, K, epi=None, batch=1, sA=0, sB=0, sC=0):
     """C[m,n] = sum_k A(m,k) B(n,k) (+ fused epilogue); see mmu_gemm in include/mmu.h."""
     _dev_check(A, B, C)

@@ -144,8 +144,11 @@ class BlockFunction(torch.autograd.Function):
         Win, Wo, W1, W2 = (t.to(bf16) for t in (win, wo, w1, w2))
         # K-major copies for the data-gradient products dX = dY W and dZ = dT W2 (B = W^T
         # K-contiguous: the GEMM's faster B path, as the BERT layers' transposed copies,
-        # DESIGN.md §2)
-        Wint, Wot, W1t, W2t = (t.t().contiguous() for t in (Win, Wo, W1, W2))
+        # DESIGN.md §2); only when a backward will run (not in no-grad inference passes)
+        if any(ctx.needs_input_grad):
+            Wint, Wot, W1t, W2t = (t.t().contiguous() for t in (Win, Wo, W1, W2))
+        else:
+            Wint = Wot = W1t = W2t = None
         qkv = torch.empty(M, 3 * E, dtype=bf16, device=dev)
         K.gemm(h1, E, True, Win, E, True, qkv, 3 * E, M, 3 * E, E, epi=K.epilogue(K.EPI_STORE, bias=bin_))
         O = torch.empty(M, E, dtype=bf16, device=dev)

@@ -30,7 +30,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, q, bucket_bytes):
+def _worker(rank, world, port, q, bucket_bytes, side=False):
     try:
         import sys
         here = os.path.dirname(os.path.abspath(__file__))
@@ -42,6 +42,9 @@ def _worker(rank, world, port, q, bucket_bytes):
         from src.mmbt import MultimodalBertClf
         from src.testing import small_args, synthetic_batch
         from oracle.weights import SMALL
+        if side:  # the trunk's filter gradients on the side stream (src/resnet.py _wgrad_run)
+            from src import resnet as R
+            R.SIDE_WGRAD_MIN_BATCH = 1
         dev = "cuda:0"
         torch.manual_seed(0)
         model = MultimodalBertClf(small_args(bert_hidden_dropout=0.0, bert_attn_dropout=0.0, dropout=0.0))
@@ -103,13 +106,13 @@ def _spawn(target, world, *extra):
     return res
 
 
-@pytest.mark.parametrize("bucket_bytes", [4 << 20, 1])
-def test_bucketer_hooks_average_real_backward(bucket_bytes):
+@pytest.mark.parametrize("bucket_bytes,side", [(4 << 20, False), (1, False), (4 << 20, True)])
+def test_bucketer_hooks_average_real_backward(bucket_bytes, side):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, bucket_bytes)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, bucket_bytes, side)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]

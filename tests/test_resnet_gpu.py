@@ -251,3 +251,35 @@ def test_model_grads_with_mmu_1x1_match_miopen(dev, monkeypatch):
     for n in g0:
         if n.endswith("weight") and g0[n].dim() == 4:
             _no_worse(g1[n], g0[n], gr[n], f"grad {n}")
+
+
+def test_model_grads_with_side_stream_wgrad(dev, monkeypatch):
+    """The trunk's filter gradients on the side stream (src/resnet.py _wgrad_run, on from
+    SIDE_WGRAD_MIN_BATCH images: forced on here) give the same gradients as the main-stream
+    order, and every one of them is complete when backward() returns (the end-of-backward join)."""
+    from oracle.weights import SMALL, make_state_dict
+    from src import resnet as R
+    from src.mmbt import MultimodalBertClf
+    from src.testing import small_args, synthetic_batch
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    x, y = synthetic_batch(8, 16, vocab=SMALL.vocab, seed=5)
+    x, y = tuple(t.to(dev) for t in x), y.to(dev)
+    sd = make_state_dict(0, SMALL)
+
+    def grads():
+        torch.manual_seed(0)
+        m = MultimodalBertClf(small_args(bert_hidden_dropout=0.0, bert_attn_dropout=0.0, dropout=0.0))
+        m.load_state_dict(sd, strict=True)
+        m = m.to(dev).train()
+        m.store.zero_grad()
+        m.compute_loss(m(*x), y).backward()
+        # no synchronize: the clones run on the main stream after the join.  The trunk's
+        # gradients only (the text embeddings' scatter-add order is not deterministic)
+        return {n: p.grad.clone() for n, p in m.named_parameters() if "img_encoder" in n}
+
+    g0 = grads()
+    monkeypatch.setattr(R, "SIDE_WGRAD_MIN_BATCH", 1)
+    g1 = grads()
+    for n in g0:
+        err = (g1[n] - g0[n]).abs().max().item()
+        assert err <= 1e-5 * g0[n].abs().max().item() + 1e-12, f"{n}: side-stream gradient differs by {err:.3e}"
