@@ -141,16 +141,21 @@ def cpu_baseline(args, L_text):
                       f"warm-up; eval forward B={B}; torch CPU {torch.get_num_threads()} threads"}
 
 
-def gemm_traffic():
+def gemm_traffic(per_rank_batch):
     """Per-launch HBM bytes of the GEMMs from the newest committed PMC summary
     (profiles/r*_gemm_traffic.json, written by tools/pmc_traffic.py from two rocprofv3
-    --pmc passes of this script: FETCH_SIZE, WRITE_SIZE; gfx950 FETCH correction applied)."""
+    --pmc passes of this script: FETCH_SIZE, WRITE_SIZE; gfx950 FETCH correction applied).
+    Those passes ran the default per-rank batch (256): at any other batch the launches move
+    other byte counts, so traffic is null there rather than a number from another workload."""
     import glob
     here = os.path.dirname(os.path.abspath(__file__))
     files = sorted(glob.glob(os.path.join(here, "profiles", "r*_gemm_traffic.json")))
     if not files:
         return {"bytes": None, "source": None}
     d = json.load(open(files[-1]))
+    if per_rank_batch != d.get("per_rank_batch", 256):
+        return {"bytes": None, "source": f"{os.path.relpath(files[-1], here)} (measured at per-rank batch "
+                                          f"{d.get('per_rank_batch', 256)}, not this one)"}
     return {"bytes": round(d["traffic_bytes_per_launch"]), "source": os.path.relpath(files[-1], here)}
 
 
@@ -473,7 +478,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
     ms_step = 1000.0 * dt / args.steps
-    traffic = gemm_traffic()
+    traffic = gemm_traffic(B)
     value = args.global_batch * args.steps / dt
     H = 768
     layer_fwd = L * (24 * H * H + 4 * L * H)
