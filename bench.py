@@ -513,6 +513,7 @@ def main():
         "model_tflops_per_step_per_rank": round(B * model_flop / 1e12, 2),
         "model_tflops_achieved": round(B * model_flop * world / (ms_step * 1e-3) / 1e12, 1),
         "final_loss": round(float(loss.item()), 4),
+        "hbm_peak_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, T)

@@ -22,7 +22,6 @@ Backward mirrors it (the gradient stream is bf16); weight gradients are written 
 gradient buffer (src/params.py) and skipped when the layer is frozen
 (src/framework.py:284-285 toggles requires_grad).
 """
-import os
 
 import torch
 
@@ -117,8 +116,9 @@ def encoder_stack(lws, X, X32, keymask, B, L, p_attn, p_hid, seeds_of, need_grad
     for i, lw in enumerate(lws):
         out32 = all_layers or i == n - 1
         if need_grad:
+            # (layer 0's backward is the encoder's last: it flushes the deferred weight gradients)
             X, R, mu, rs, Y32 = BertLayerFunction.apply(X, R, lw.anchor, lw, keymask, B, L, p_attn, p_hid,
-                                                        seeds_of(i), hook, rln, out32)
+                                                        seeds_of(i), hook, rln, out32, i == 0)
         else:
             X, R, mu, rs, _, Y32 = layer_forward(lw, X, R, keymask, B, L, p_attn, p_hid, seeds_of(i), False, rln,
                                                  out32)
@@ -132,35 +132,66 @@ def _reduce(part, out):
     K.colsum_reduce(part, out, accumulate=True)
 
 
-SIDE_STREAM = os.environ.get("MMU_SIDE_STREAM", "0") == "1"
+DEFER_WGRAD = True
+
+# per device: the weight-gradient work of the layers' backwards, deferred (DEFER_WGRAD) until
+# the encoder's data-gradient chain is enqueued, then issued on the side stream
+_deferred = {}
+
+
+def _flush_deferred(dev):
+    """Issue the deferred weight-gradient work (and the DP hooks after it) on the side stream,
+    behind everything the main stream has enqueued so far -- the whole encoder dX chain -- so
+    it runs beside what follows (embedding backward, the ResNet trunk's backward)."""
+    items = _deferred.pop(dev, None)
+    if not items:
+        return
+    main = torch.cuda.current_stream(dev)
+    side = K.side_stream(dev)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        e0 = _mark()
+        for fn, tensors in items:
+            for t in tensors:
+                t.record_stream(side)
+            fn()
+        if e0 is not None:
+            _block_extra.append((e0, _mark()))
+    K.join_at_backward_end(main, side)
+
+
+def _defer(dev, fn, tensors):
+    items = _deferred.get(dev)
+    if items is None:
+        items = _deferred[dev] = []
+
+        def at_end():  # (nothing may stay deferred past the backward)
+            if dev in _deferred:
+                _flush_deferred(dev)
+                torch.cuda.current_stream(dev).wait_stream(K.side_stream(dev))
+
+        torch.autograd.Variable._execution_engine.queue_callback(at_end)
+    items.append((fn, tensors))
 
 
 class _Side:
-    """Runs the weight-gradient work of a layer's backward (split-K dW products, LN /
-    bias column-sum reductions) on a side stream, each piece ordered after the main-stream
-    kernel that produced its inputs by an event, so it overlaps the data-gradient chain
-    (and fills the tail rounds of its GEMMs).  Tensors touched on the side stream are
-    record_stream'ed so the caching allocator does not recycle them early.
-    Opt-in (MMU_SIDE_STREAM=1): measured 210 -> 207 ms per step, but co-running kernels
-    stretch each other's event-timed durations, which the per-kernel roofline of bench.py
-    reads as a slower GEMM."""
+    """The weight-gradient work of a layer's backward (split-K dW products, LN / bias
+    column-sum reductions): with DEFER_WGRAD (CUDA) it is deferred until layer 0's backward
+    has enqueued the encoder's whole data-gradient chain, then issued on the side stream
+    (_flush_deferred), where it runs beside the embedding and ResNet-trunk backward -- a
+    chain of short, latency-bound kernels.  Same-box A/B (profiles/r3_defer_wgrad_ab.txt):
+    165.6 -> 163.3 ms per step at batch 256.  The inputs it reads stay alive until then
+    (peak HBM 75 GB at batch 256).  (Round 1 issued each piece on the side stream as soon as
+    its inputs existed: 210 -> 207 ms, an opt-in that this replaces.)"""
 
     def __init__(self, dev, on):
-        on = on and SIDE_STREAM
-        self.on = on
-        self.main = torch.cuda.current_stream(dev)
-        self.side = K.side_stream(dev) if on else None
+        self.dev = dev
+        self.defer = on and DEFER_WGRAD and dev.type == "cuda"
 
     def run(self, fn, *tensors):
-        if not self.on:
-            return fn()
-        ev = torch.cuda.Event()
-        ev.record(self.main)
-        self.side.wait_event(ev)
-        for t in tensors:
-            t.record_stream(self.side)
-        with torch.cuda.stream(self.side):
-            fn()
+        if self.defer:
+            return _defer(self.dev, fn, tensors)
+        return fn()
 
 
 def layer_backward(lw, saved, dY, keymask, B, L, p_attn, p_hid, seeds, wgrad):
@@ -223,21 +254,25 @@ def layer_backward(lw, saved, dY, keymask, B, L, p_attn, p_hid, seeds, wgrad):
 
 
 _block_events = None  # [(start, end)] HIP events around every fused-layer fwd / bwd while timing
+_block_extra = []     # ... and around the layers' deferred weight-gradient work (side stream)
 
 
 def block_timing(on):
     """Time every BertLayer forward and backward on the stream it runs on (bench.py: the
-    fused-block roofline of BASELINE's north star)."""
-    global _block_events
+    fused-block roofline of BASELINE's north star), the deferred weight-gradient work of
+    the backwards included (timed on the side stream, beside whatever it overlaps)."""
+    global _block_events, _block_extra
     _block_events = [] if on else None
+    _block_extra = []
 
 
 def block_timing_read():
     """-> (total ms, number of layer passes) since block_timing(True); synchronises."""
     if not _block_events:
         return 0.0, 0
-    _block_events[-1][1].synchronize()
-    return sum(a.elapsed_time(b) for a, b in _block_events), len(_block_events)
+    torch.cuda.synchronize()
+    ms = sum(a.elapsed_time(b) for a, b in _block_events) + sum(a.elapsed_time(b) for a, b in _block_extra)
+    return ms, len(_block_events)
 
 
 def _mark():
@@ -258,7 +293,7 @@ class BertLayerFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, X, R, anchor, lw, keymask, B, L, p_attn, p_hid, seeds, on_grads_ready, res_ln=None,
-                out32=True):
+                out32=True, flush=False):
         ctx.set_materialize_grads(False)
         e0 = _mark()
         Y, S2, mean2, rstd2, saved, Y32 = layer_forward(lw, X, R, keymask, B, L, p_attn, p_hid, seeds, True,
@@ -266,7 +301,7 @@ class BertLayerFunction(torch.autograd.Function):
         if e0 is not None:
             _block_events.append((e0, _mark()))
         ctx.saved_bufs = saved
-        ctx.meta = (lw, keymask, B, L, p_attn, p_hid, seeds, on_grads_ready)
+        ctx.meta = (lw, keymask, B, L, p_attn, p_hid, seeds, on_grads_ready, flush)
         ctx.mark_non_differentiable(S2, mean2, rstd2)
         if Y32 is None:
             Y32 = Y.new_empty(0, dtype=torch.float32)
@@ -275,28 +310,24 @@ class BertLayerFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dY, _dS2, _dmean2, _drstd2, dY32):
-        lw, keymask, B, L, p_attn, p_hid, seeds, hook = ctx.meta
+        lw, keymask, B, L, p_attn, p_hid, seeds, hook, flush = ctx.meta
         wgrad = lw.trainable()
         if dY32 is not None and dY32.numel():
             dY = dY32.to(bf16) if dY is None else dY + dY32.to(bf16)
         if dY is None:
-            return (None,) * 13
+            return (None,) * 14
         e0 = _mark()
         dX, side = layer_backward(lw, ctx.saved_bufs, dY.contiguous(), keymask, B, L, p_attn, p_hid, seeds, wgrad)
         if e0 is not None:
             _block_events.append((e0, _mark()))
         ctx.saved_bufs = None
-        if wgrad and side.on:
-            if hook is not None:  # the gradient all-reduce is issued behind the side stream's work
-                with torch.cuda.stream(side.side):
-                    hook(lw)
-            _join_side_at_end(side)
+        if wgrad and side.defer:
+            if hook is not None:  # the bucket all-reduce follows the layer's deferred work
+                _defer(side.dev, lambda: hook(lw), ())
+            if flush:
+                _flush_deferred(side.dev)
         elif wgrad and hook is not None:
             hook(lw)
-        return (dX,) + (None,) * 12
+        return (dX,) + (None,) * 13
 
 
-def _join_side_at_end(side):
-    """Once per backward pass: the main stream waits for the weight-gradient stream when
-    the autograd engine finishes, so every consumer of .grad (optimizer, tests) sees them."""
-    K.join_at_backward_end(side.main, side.side)

@@ -170,7 +170,8 @@ def test_freeze_skips_weight_grads(dev):
 
 
 def test_side_stream_weight_grads_identical(dev, monkeypatch):
-    """MMU_SIDE_STREAM: the weight-gradient work on the side stream gives the same
+    """DEFER_WGRAD (the layers' weight-gradient work deferred to the end of the encoder
+    backward, then on the side stream) gives the same
     gradients (same kernels; only the float-atomic column sums may reorder) and every
     .grad is complete when backward() returns."""
     from src import encoder as E
@@ -184,8 +185,8 @@ def test_side_stream_weight_grads_identical(dev, monkeypatch):
     y = y.to(dev)
     model.train()
     grads = []
-    for on in (False, True):
-        monkeypatch.setattr(E, "SIDE_STREAM", on)
+    for defer in (False, True):
+        monkeypatch.setattr(E, "DEFER_WGRAD", defer)
         model.store.zero_grad()
         torch.manual_seed(11)  # same dropout seeds (embedding / hidden dropout draw from the torch RNG)
         model.compute_loss(model(*x), y).backward()
