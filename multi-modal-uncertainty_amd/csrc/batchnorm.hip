@@ -51,22 +51,25 @@ static __device__ __forceinline__ BnGeom bn_geom(int CH, int64_t rows, int64_t r
   return g;
 }
 
-// per-thread (a[8], b[8]) partials -> block sums per channel -> part[blockIdx.x][c] = {a, b}
+// per-thread (a[8], b[8]) partials -> block sums per channel -> part[blockIdx.x][c] = {a, b}.
+// LDS as [value][e][thread]: every write and read is one float per lane at consecutive
+// addresses (the [thread][e] layout, 8 floats per lane, was ~3.6 bank-conflict cycles per LDS
+// instruction in the step's PMC pass, profiles/r3_pmc_step_v3.txt)
 static __device__ __forceinline__ void bn_block_reduce(const BnGeom& g, int C, const float (&a)[8],
                                                        const float (&b)[8], float2* __restrict__ part) {
-  __shared__ float red[2][BN_THREADS * 8];
+  __shared__ float red[2][8][BN_THREADS];
   const int t = threadIdx.x;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) { red[0][t * 8 + e] = a[e]; red[1][t * 8 + e] = b[e]; }
+  for (int e = 0; e < 8; ++e) { red[0][e][t] = a[e]; red[1][e][t] = b[e]; }
   __syncthreads();
   if (t < g.tpr) {
     float sa[8], sb[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { sa[e] = 0.f; sb[e] = 0.f; }
     for (int r = 0; r < g.rpi; ++r) {
-      const int o = (r * g.tpr + t) * 8;
+      const int o = r * g.tpr + t;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { sa[e] += red[0][o + e]; sb[e] += red[1][o + e]; }
+      for (int e = 0; e < 8; ++e) { sa[e] += red[0][e][o]; sb[e] += red[1][e][o]; }
     }
     float2* dst = part + (int64_t)blockIdx.x * C + g.c0;
 #pragma unroll
