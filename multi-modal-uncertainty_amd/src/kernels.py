@@ -20,8 +20,13 @@ def _dev_check(*ts):
                                 f"{tuple(t.shape)} {t.dtype}")
 
 
+_raw_stream = torch._C._cuda_getCurrentRawStream  # (device index) -> the current hipStream_t as an int
+
+
 def _stream(t):
-    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+    # the raw handle, without building a torch.cuda.Stream object: this runs once per kernel
+    # launch, ~800 times per training step
+    return _raw_stream(t.get_device())
 
 
 def _ptr(t):
@@ -63,7 +68,7 @@ _side = {}
 
 
 def _splitk_workspace(dev):
-    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    key = (dev, _raw_stream(dev.index if dev.index is not None else torch.cuda.current_device()))
     t = _ws.get(key)
     if t is None:
         t = _ws[key] = torch.empty(SPLITK_WS_FLOATS, dtype=torch.float32, device=dev)

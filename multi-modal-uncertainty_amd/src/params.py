@@ -35,6 +35,7 @@ class ParamStore:
         self._tcopies = {}
         self._fcopies = {}  # conv filter name -> flipped, transposed bf16 copy [Cin, 3, 3, Cout]
         self._tjobs = None
+        self._cviews = {}  # name -> compute_of view (rebuilt with the buffers)
         self.build()
         STORES.add(self)
 
@@ -69,6 +70,7 @@ class ParamStore:
             self.offsets[n] = off
             off += k
         self.flat, self.grad = flat, grad
+        self._cviews = {}
         ctot = sum(self.params[n].numel() for n in self.compute_names)
         self.compute = torch.empty(ctot, dtype=torch.bfloat16, device=device)
         off = 0
@@ -187,17 +189,19 @@ class ParamStore:
             if all(self.params[n].grad is not None and
                    self.params[n].grad.data_ptr() == base + 4 * self.offsets[n] for n in ends):
                 return
+        params, offsets = self.params, self.offsets
         for n in names:
-            p = self.params[n]
-            o = self.offsets[n]
-            view = self._shaped(self.grad, o, p)
+            p = params[n]
+            o = offsets[n]
             g = p.grad
+            if g is not None and g.data_ptr() == base + 4 * o:
+                continue  # (the common case: no view to build)
+            view = self._shaped(self.grad, o, p)
             if g is None:
                 view.zero_()
-                p.grad = view
-            elif g.data_ptr() != base + 4 * o:
+            else:
                 view.copy_(g)
-                p.grad = view
+            p.grad = view
 
     def zero_grad(self):
         self.ensure_grads()
@@ -218,8 +222,12 @@ class ParamStore:
         self.sync_transposed()
 
     def compute_of(self, name):
-        """bf16 copy of one tensor, shaped like the parameter (conv weights channels-last)."""
-        return self._shaped(self.compute, self.coffsets[name], self.params[name])
+        """bf16 copy of one tensor, shaped like the parameter (conv weights channels-last);
+        the view is cached until the buffers are rebuilt (build())."""
+        v = self._cviews.get(name)
+        if v is None:
+            v = self._cviews[name] = self._shaped(self.compute, self.coffsets[name], self.params[name])
+        return v
 
     def maybe_sync_compute(self):
         """bf16 copies follow the masters; only an out-of-band write (version bump) needs a resync."""
@@ -228,6 +236,9 @@ class ParamStore:
 
     def check_views(self):
         """True if every parameter still aliases the flat buffer (Module._apply breaks this)."""
-        base = self.flat.data_ptr()
-        return all(self.params[n].data_ptr() == base + 4 * self.offsets[n] and self.params[n].device == self.device
-                   for n in self.names)
+        flat = self.flat
+        base, dev, params, offsets = flat.data_ptr(), flat.device, self.params, self.offsets
+        # (a data pointer inside the flat buffer's allocation implies its device; the device is
+        # compared for one tensor to catch a store whose buffer moved)
+        return params[self.names[0]].device == dev and all(
+            params[n].data_ptr() == base + 4 * offsets[n] for n in self.names)
