@@ -114,6 +114,11 @@ def _is_stem(w16, stride, padding):
 SIDE_WGRAD_MIN_BATCH = 128
 
 
+def _side_wgrad(t):
+    """filter gradients of this [N, C, H, W] map's conv go to the side stream (_wgrad_run)"""
+    return t.is_cuda and t.shape[0] >= SIDE_WGRAD_MIN_BATCH
+
+
 def _wgrad_run(fn, *tensors):
     """Run a filter-gradient product (off the backward's data-gradient chain) on the device's
     side stream, ordered after everything the main stream has enqueued so far; the tensors it
@@ -125,7 +130,7 @@ def _wgrad_run(fn, *tensors):
     per conv, and at batch 32 the step is bound by kernel issue -- measured 167.7 -> 165.6 ms
     at batch 256, but 41.7 -> 46.7 ms at batch 32 without the gate (profiles/r3_side_wgrad_ab.txt)."""
     dev = tensors[0].device
-    if not (dev.type == "cuda" and tensors[0].shape[0] >= SIDE_WGRAD_MIN_BATCH):
+    if not _side_wgrad(tensors[0]):
         fn()
         return
     main = torch.cuda.current_stream(dev)
@@ -188,6 +193,14 @@ class _ConvBF16(torch.autograd.Function):
         # [Cin][3][3][Cout]
         mmu_x = need_x and route[1]
         dx = rw = None
+        g = ctx.w.grad
+        store_g = need_w and g is not None and g.dtype == torch.float32 and g.is_contiguous(memory_format=cl)
+        if need_x and not mmu_x and store_g and not mmu_w and not _side_wgrad(dy):
+            # both products on MIOpen, both on this stream: one call (its host cost is ~30 us)
+            dx, gw, _ = torch.ops.aten.convolution_backward(dy, x, w16, None, stride, padding, (1, 1), False, (0, 0),
+                                                            1, (True, True, False))
+            g.add_(gw)
+            return dx, None, None, None, None, None
         if need_x and not mmu_x:
             dx = torch.ops.aten.convolution_backward(dy, x, w16, None, stride, padding, (1, 1), False, (0, 0), 1,
                                                      (True, False, False))[0]
@@ -196,8 +209,7 @@ class _ConvBF16(torch.autograd.Function):
             # the store's flipped copy (refreshed with the bf16 filters), else one made here
             wf = ctx.flipped() if ctx.flipped is not None else w16.flip(2, 3).permute(1, 2, 3, 0).contiguous()
             K.conv3x3_implicit(dy, wf, dx)
-        g = ctx.w.grad
-        if need_w and g is not None and g.dtype == torch.float32 and g.is_contiguous(memory_format=cl):
+        if store_g:
             # straight into the gradient store, on the side stream
             def dw_side():
                 if mmu_w:
@@ -328,9 +340,13 @@ class _Conv1x1(torch.autograd.Function):
                 K.gemm(_rows(dy), Co, 1, w16.view(Co, C), C, 0, _rows(dx), C, M, C, Co, epi=epi)
                 skip = None
             elif need_x:
-                gx = torch.ops.aten.convolution_backward(dy, x, w16, None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1,
-                                                         (True, False, False))[0]
+                both = need_w and not use_w and ctx.w.grad is not None and not _side_wgrad(dy)
+                gx, gw, _ = torch.ops.aten.convolution_backward(dy, x, w16, None, (1, 1), (0, 0), (1, 1), False,
+                                                                (0, 0), 1, (True, both, False))
                 dx = gx if skip is None else gx + skip
+                if both:  # (one MIOpen call for both products when neither goes elsewhere)
+                    ctx.w.grad.add_(gw)
+                    return dx, None, None, None
             if need_w:
                 g = ctx.w.grad
                 if g is None:
