@@ -290,11 +290,13 @@ def _mmu_1x1(cin, cout, M, H):
     MIOpen, from profiles/r1_conv1x1_b256.txt / _b32.txt (same-box timings, both engines):
     dX always for the reducing convs (cin > cout) and for M >= 12544; the forward for
     25088 <= M <= 50176 (and not the widening 14x14 product at batch 256); the weight
-    gradient for 12544 <= M <= 50176 at H <= 14.  mmu_gemm needs N % 128 == 0 for its
-    output columns (and M-major A rows % 128 for dW)."""
+    gradient for M <= 50176 at H <= 14 (layer3 / layer4; below M = 12544 -- the batch-32 to
+    batch-128 ranks of config 4 -- since the short-K split-K of profiles/r3_wgrad_shortk_ab.txt
+    brought it level with MIOpen's wrw, which also pays a bf16 -> f32 add into the store).
+    mmu_gemm needs N % 128 == 0 for its output columns (and M-major A rows % 128 for dW)."""
     fwd = cout % 128 == 0 and cin % 64 == 0 and 25088 <= M <= 50176 and (cin > cout or M < 50176)
     dx = cin % 128 == 0 and cout % 64 == 0 and (cin > cout or M >= 12544)
-    dw = cin % 128 == 0 and cout % 128 == 0 and 12544 <= M <= 50176 and H <= 14
+    dw = cin % 128 == 0 and cout % 128 == 0 and M <= 50176 and H <= 14
     return fwd, dx, dw
 
 
