@@ -316,8 +316,11 @@ struct BnGrid {
 // pairs fit BN_MAX_PART_ELEMS.  (A fixed 64 K elements per block left the trunk's small
 // tensors on 24-200 blocks -- e.g. layer3's 256-channel 14x14 maps at batch 32 -- i.e. on
 // a tenth of the CUs, latency-bound.)
+// The 8 K-element floor (was 4 K) halves the block partials the finalize sums on the small
+// maps: batch-32 BN 6.08 -> 5.41-5.47 ms per step, batch 256 unchanged
+// (profiles/r3_bn_grid_sweep.txt).
 static BnGrid bn_grid(int64_t rows, int C) {
-  const int64_t target = 1024, min_elems = 4096;
+  const int64_t target = 1024, min_elems = 8192;
   BnGrid g;
   g.CH = 512;
   while (C % g.CH) g.CH >>= 1;
