@@ -12,7 +12,8 @@ Without --mmbt: the reference's FashionMNIST MIMO robustness pass (eval_robustne
 BASELINE config 1's model family): each of the 4 quarter-crop views zeroed in turn (the
 weight-sharing model sees the other 3), predictions [4, S, heads, 10] and labels written as
 <checkpoint>_predictions_robustness.npy / <checkpoint>_labels.npy.  --data_dir / --sample_size
-as in train_fashionmnist.py (images synthetic when only the label files exist).
+/ --synthetic_images as in train_fashionmnist.py (without image files the run fails unless
+--synthetic_images is given).
 """
 import argparse
 import json
@@ -44,6 +45,7 @@ FLAGS = [
     ("--bert_model", dict(type=str, default="bert-base-uncased")),
     ("--gin_file", dict(nargs="*", default=[])), ("--gin_param", dict(nargs="*", default=[])),
     ("--data_dir", dict(type=str, default=None)), ("--sample_size", dict(type=int, default=None)),
+    ("--synthetic_images", dict(action="store_true")),
 ]
 
 
@@ -107,7 +109,10 @@ def run_fmnist(args):
         raise ValueError("--checkpoint_path is required without --mmbt")
     model = build_model(args)
     _, valid, _ = dataset.get_fmnist(datapath=args.data_dir, batch_size=args.batch_size, download=True,
-                                     shuffle=True, sample_size=args.sample_size, seed=args.seed)
+                                     shuffle=True, sample_size=args.sample_size, seed=args.seed,
+                                     synthetic_images=args.synthetic_images)
+    if getattr(valid.dataset, "synthetic", False):
+        print("WARNING: FashionMNIST images are SYNTHETIC (seeded noise, real labels)")
     print("Loading Checkpoint from {}".format(args.checkpoint_path))
     _load_pretrained_model(model, args.checkpoint_path)
     dev = torch.device("cuda:{}".format(args.device)) if args.use_gpu and torch.cuda.is_available() \

@@ -464,11 +464,13 @@ class FashionMNISTQuarters(Dataset):
     ToTensor: [4, 1, 14, 14] float in [0, 1], int64 label; reference src/dataset.py:148-162).
 
     Labels come from the IDX label file under ``datapath``.  The image files are absent
-    from this offline checkout (only the label files ship): when no image file
-    is found the images are SYNTHETIC -- seeded uint8 28x28 noise per index -- and
-    ``self.synthetic`` is True."""
+    from this offline checkout (only the label files ship).  A missing image
+    file raises FileNotFoundError (the reference downloads or fails) unless the caller
+    opts in with ``synthetic_images=True``: the images are then SYNTHETIC -- seeded uint8
+    28x28 noise per index, paired with the real labels -- ``self.synthetic`` is True and a
+    warning is logged."""
 
-    def __init__(self, datapath, train=True, seed=777, sample_size=None):
+    def __init__(self, datapath, train=True, seed=777, sample_size=None, synthetic_images=False):
         pre = "train" if train else "t10k"
         lab = _find_idx(datapath, f"{pre}-labels-idx1-ubyte")
         if lab is None:
@@ -477,6 +479,14 @@ class FashionMNISTQuarters(Dataset):
         img = _find_idx(datapath, f"{pre}-images-idx3-ubyte")
         self.synthetic = img is None
         if self.synthetic:
+            if not synthetic_images:
+                raise FileNotFoundError(
+                    f"no FashionMNIST {pre}-images-idx3-ubyte[.gz] under {datapath} (there is no network to "
+                    f"download it); pass synthetic_images=True / --synthetic_images to train on seeded noise")
+            import logging
+            logging.getLogger(__name__).warning(
+                "FashionMNIST %s images missing under %s: serving SYNTHETIC seeded noise images with the real "
+                "labels (synthetic_images=True)", pre, datapath)
             g = torch.Generator().manual_seed(seed + (0 if train else 1))
             self.images = torch.randint(0, 256, (len(self.labels), 28, 28), generator=g, dtype=torch.uint8)
         else:
@@ -493,14 +503,16 @@ class FashionMNISTQuarters(Dataset):
         return torch.stack([q.unsqueeze(0) for q in quarters]), self.labels[i]
 
 
-def get_fmnist(datapath=None, batch_size=128, download=False, shuffle=True, sample_size=None, seed=777):
+def get_fmnist(datapath=None, batch_size=128, download=False, shuffle=True, sample_size=None, seed=777,
+               synthetic_images=False):
     """(train_loader, test_loader, None) of [B, 4, 1, 14, 14] quarter crops (reference
-    src/dataset.py:130-175; ``download`` is accepted and ignored: there is no network)."""
+    src/dataset.py:130-175; ``download`` is accepted and ignored: there is no network;
+    ``synthetic_images``: see FashionMNISTQuarters)."""
     if datapath is None:
         from . import DATA_DIR as datapath
     torch.manual_seed(seed)
-    training = FashionMNISTQuarters(datapath, True, seed, sample_size)
-    testing = FashionMNISTQuarters(datapath, False, seed, sample_size)
+    training = FashionMNISTQuarters(datapath, True, seed, sample_size, synthetic_images)
+    testing = FashionMNISTQuarters(datapath, False, seed, sample_size, synthetic_images)
     train_loader = torch.utils.data.DataLoader(training, batch_size=batch_size, shuffle=shuffle)
     test_loader = torch.utils.data.DataLoader(testing, batch_size=batch_size, shuffle=False)
     print("training_loader LENGTH:", len(train_loader))

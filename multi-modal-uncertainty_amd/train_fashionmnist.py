@@ -11,14 +11,17 @@ offline necessity:
   * ``scheduler_metric`` is passed to train_loop (the reference sets args.scheduler_metric
     but never passes it, and train_loop reads kwargs["scheduler_metric"]);
   * images: only the label files ship (reference fashionMNIST/FashionMNIST/*-labels-*);
-    without image files the loader serves seeded synthetic 28x28 images with the REAL
-    labels (src/dataset.FashionMNISTQuarters).  --sample_size caps the set for smoke runs;
+    without image files the loader raises unless --synthetic_images is given, which serves
+    seeded synthetic 28x28 images with the REAL labels (src/dataset.FashionMNISTQuarters;
+    recorded as ``synthetic_images`` in <save_path>/run_meta.json).  --sample_size caps the
+    set for smoke runs;
   * gin front end: --gin_file / --gin_param bindings (configs/training.gin's ``train.*``
     scope) map onto the flags (src/gin.py).
 The ResNet runs on the CPU by default (the config is CPU plumbing); ``--transformer``
 selects MIMOTransfomer, whose fusion blocks are the HIP kernels (needs --use_gpu).
 """
 import argparse
+import json
 import logging
 import os
 import sys
@@ -62,6 +65,8 @@ def get_args(parser):
     # additions
     parser.add_argument("--data_dir", type=str, default=None, help="FashionMNIST root (default $DATA_DIR)")
     parser.add_argument("--sample_size", type=int, default=None)
+    parser.add_argument("--synthetic_images", action="store_true",
+                        help="serve seeded noise images when the FashionMNIST image files are missing")
     parser.add_argument("--gin_file", nargs="*", default=[])
     parser.add_argument("--gin_param", nargs="*", default=[])
 
@@ -119,9 +124,15 @@ def main(argv=None):
         logger.warning("gin bindings not mapped to train_fashionmnist.py flags: %s", sorted(unused))
     model = build_model(args)
     train, valid, _ = dataset.get_fmnist(datapath=args.data_dir, batch_size=args.batch_size, download=True,
-                                         shuffle=True, sample_size=args.sample_size, seed=args.seed)
+                                         shuffle=True, sample_size=args.sample_size, seed=args.seed,
+                                         synthetic_images=args.synthetic_images)
     optimizer, scheduler = build_optimizer(args, model, len(train))
     os.makedirs(args.save_path, exist_ok=True)
+    synthetic = bool(getattr(train.dataset, "synthetic", False))
+    if synthetic:
+        print("WARNING: FashionMNIST images are SYNTHETIC (seeded noise, real labels)")
+    with open(os.path.join(args.save_path, "run_meta.json"), "w") as f:
+        json.dump({"synthetic_images": synthetic, "model_type": args.model_type, "seed": args.seed}, f)
     history_csv_path = os.path.join(args.save_path, "history.csv")
     if args.resume:
         ck = torch.load(os.path.join(args.save_path, "model_last_epoch.pt"), map_location="cpu", weights_only=True)

@@ -16,6 +16,8 @@ Run:  python -m oracle.gen_golden          (needs /root/reference; CPU only)
   and the MIMO permutations of data_forming_func_transformer (src/dataset.py:30-54).
 * robustness fixtures (A11): the eval_mmbt_robustness.py:77-93 per-batch loop over the
   reference model, [B, 3 + 2n, C] with the drawn control index sets.
+* A0 fixture: the reference's own JsonlDataset / collate_fn / numpy_seed over a committed
+  jsonl (tests/golden/a0/) -> text / segment / mask / image / label batches.
 * framework fixture: the reference ``Model_.train_loop`` (src/framework.py:213)
   with ``_construct_default_callbacks`` (src/training_loop.py:23-47) driving
   oracle/tiny_model.TinyMMBT for 2 epochs x 3 steps; history + checkpoint keys.
@@ -189,18 +191,83 @@ def gen_robustness(tag, cfg, B, T, lens, n_repeats, seed=0, wseed=0, rng_seed=20
     print(f"wrote robustness_{tag}: preds {tuple(stack.shape)}")
 
 
-def _reference_function(relpath, name):
-    """One top-level function of a reference module whose other imports are absent here
-    (src/dataset.py needs torchvision transforms, a tokenizer, ViltProcessor): the
-    function's own definition is compiled from the reference file and run in a
-    namespace holding torch.  Used to record golden outputs only."""
+def _reference_function(relpath, name, ns=None):
+    """One top-level function (or class) of a reference module whose other imports are
+    absent here (src/dataset.py needs torchvision transforms, a tokenizer, ViltProcessor):
+    the definition is compiled from the reference file and run in a namespace holding
+    torch (+ ``ns``).  Used to record golden outputs only."""
     import ast
     src_path = os.path.join(REF, relpath)
     tree = ast.parse(open(src_path).read(), filename=src_path)
-    node = next(n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == name)
-    ns = {"torch": torch}
+    node = next(n for n in tree.body if isinstance(n, (ast.FunctionDef, ast.ClassDef)) and n.name == name)
+    ns = dict({"torch": torch}, **(ns or {}))
     exec(compile(ast.Module(body=[node], type_ignores=[]), src_path, "exec"), ns)
     return ns[name]
+
+
+A0_WORDS = [f"w{i}" for i in range(40)]
+
+
+def a0_vocab_stoi():
+    """The A0 fixture's vocabulary (Vocab() specials then the words, src/dataset.py:440-460)."""
+    itos = ["[PAD]", "[UNK]", "[CLS]", "[SEP]", "[MASK]"] + A0_WORDS
+    return {w: i for i, w in enumerate(itos)}
+
+
+def a0_transform(image):
+    """The fixture's image transform: PIL bilinear resize to 8x8, uint8 CHW tensor (the
+    same PIL call on both sides; torchvision's Resize/CenterCrop/Normalize are absent here)."""
+    from PIL import Image
+    return torch.from_numpy(np.asarray(image.resize((8, 8), Image.BILINEAR), dtype=np.uint8).copy()).permute(2, 0, 1)
+
+
+def gen_a0():
+    """A0 input contract: the reference's own JsonlDataset (src/dataset.py:348-405),
+    get_labels_and_frequencies (:408-417), collate_fn (:420-438) and numpy_seed
+    (src/utils.py:167-181) over a committed jsonl (tests/golden/a0/), a str.split tokenizer,
+    a fixed vocab and a PIL resize transform; drop_img_percent 0 and 0.5; max_seq_len 12 and
+    512 with num_image_embeds 3."""
+    from contextlib import contextmanager
+    from collections import Counter
+    from PIL import Image
+    from torch.utils.data import Dataset
+    d = os.path.join(OUT, "a0")
+    os.makedirs(d, exist_ok=True)
+    rng = np.random.default_rng(7)
+    for name, hw in (("a.png", (30, 41)), ("b.png", (25, 19)), ("c.png", (16, 16))):
+        Image.fromarray(rng.integers(0, 256, hw + (3,), dtype=np.uint8)).save(os.path.join(d, name))
+    labels_pool = ["pizza", "ramen", "sushi", "tacos"]
+    rows = []
+    for i in range(10):
+        n = [0, 1, 3, 8, 9, 10, 25, 600, 5, 2][i]
+        words = [A0_WORDS[int(k)] if k < len(A0_WORDS) else "oov%d" % k for k in rng.integers(0, 46, n)]
+        rows.append({"text": " ".join(words), "img": [None, "a.png", "b.png", "c.png"][i % 4] if i != 3 else "a.png",
+                     "label": labels_pool[int(rng.integers(0, 4))]})
+    with open(os.path.join(d, "train.jsonl"), "w") as f:
+        for r in rows:
+            f.write(json.dumps(r) + "\n")
+    numpy_seed = _reference_function("src/utils.py", "numpy_seed", {"np": np, "contextmanager": contextmanager})
+    ns = {"np": np, "json": json, "os": os, "Image": Image, "Dataset": Dataset, "numpy_seed": numpy_seed,
+          "Counter": Counter}
+    JsonlDataset = _reference_function("src/dataset.py", "JsonlDataset", ns)
+    collate_fn = _reference_function("src/dataset.py", "collate_fn", ns)
+    get_labels = _reference_function("src/dataset.py", "get_labels_and_frequencies", ns)
+    path = os.path.join(d, "train.jsonl")
+    labels, freqs = get_labels(path)
+    vocab = types.SimpleNamespace(stoi=a0_vocab_stoi())
+    out = {"labels": np.array(labels), "label_counts": np.array([freqs[k] for k in labels])}
+    for tag, drop, msl in (("d0_m12", 0.0, 12), ("d50_m12", 0.5, 12), ("d50_m512", 0.5, 512)):
+        ds = JsonlDataset(path, str.split, a0_transform, vocab, len(labels), drop, msl, 3, labels)
+        out[f"{tag}_img_dropped"] = np.array([r["img"] is None for r in ds.data])
+        items = [ds[i] for i in range(len(ds))]
+        out[f"{tag}_item_lens"] = np.array([len(it[0]) for it in items])
+        for lo, hi in ((0, 4), (4, 10)):
+            (txt, seg, mask, img), tgt = collate_fn(items[lo:hi])
+            for k, v in (("text", txt), ("segment", seg), ("mask", mask), ("img", img), ("tgt", tgt)):
+                out[f"{tag}_b{lo}_{k}"] = v.numpy()
+                out[f"{tag}_b{lo}_{k}_dtype"] = np.array(str(v.dtype))
+    np.savez_compressed(os.path.join(OUT, "a0_contract.npz"), **out)
+    print("wrote a0_contract.npz", {k: v.shape for k, v in out.items() if k.endswith("_text")})
 
 
 def gen_flava(tag, cfg, B, L_img, L_txt, seed):
@@ -362,14 +429,14 @@ def gen_framework():
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="all", choices=["all", "small", "full", "framework", "flava",
-                                                       "robustness", "fmnist"])
+                                                       "robustness", "fmnist", "a0"])
     a = ap.parse_args()
     sys.path.insert(0, REPO)
     from oracle.weights import SMALL, FULL
     # each generator imports the reference fresh with its own stub config -> run each in a subprocess
     if a.what == "all":
         import subprocess
-        for w in ("small", "full", "framework", "flava", "robustness", "fmnist"):
+        for w in ("small", "full", "framework", "flava", "robustness", "fmnist", "a0"):
             subprocess.check_call([sys.executable, "-m", "oracle.gen_golden", "--what", w], cwd=REPO)
     elif a.what == "small":
         gen_mmbt("small_t16", SMALL, B=2, T=16, lens=[16, 9], seed=0)
@@ -384,5 +451,7 @@ if __name__ == "__main__":
         gen_robustness("full_t508", FULL, B=2, T=508, lens=[508, 301], n_repeats=2, seed=6)
     elif a.what == "fmnist":
         gen_fmnist()
+    elif a.what == "a0":
+        gen_a0()
     else:
         gen_framework()

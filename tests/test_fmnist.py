@@ -40,7 +40,9 @@ def test_label_files_read():
     te = dataset.read_idx(os.path.join(FM_ROOT, "FashionMNIST", "t10k-labels-idx1-ubyte.gz"))
     assert tr.shape == (60000,) and te.shape == (10000,)
     assert np.bincount(tr).tolist() == [6000] * 10 and np.bincount(te).tolist() == [1000] * 10
-    ds = dataset.FashionMNISTQuarters(FM_ROOT, train=False, seed=3, sample_size=5)
+    with pytest.raises(FileNotFoundError):  # no silent noise images without the opt-in
+        dataset.FashionMNISTQuarters(FM_ROOT, train=False, seed=3, sample_size=5)
+    ds = dataset.FashionMNISTQuarters(FM_ROOT, train=False, seed=3, sample_size=5, synthetic_images=True)
     x, y = ds[2]
     assert ds.synthetic and x.shape == (4, 1, 14, 14) and x.dtype == torch.float32 and int(y) == int(te[2])
     # quarters tile the 28x28 image: UL, UR, LL, LR
@@ -102,13 +104,15 @@ def test_train_fashionmnist_entry(tmp_path, mt):
     gf.write_text("# config-1 bindings\ntrain.batch_size = 16\ntrain.lr=0.05\nMMTM_MVCNN.num_views=2\n")
     save = tmp_path / "run"
     argv = ["--save_path", str(save), "--data_dir", FM_ROOT, "--sample_size", "48", "--n_epochs", "3",
-            "--model_type", mt, "--gin_file", str(gf)]
+            "--model_type", mt, "--synthetic_images", "--gin_file", str(gf)]
     H = mod.main(argv)
     assert H["epoch"] == [1, 2]
     for k in ("loss", "acc", "val_loss", "val_acc", "test_loss", "test_acc"):
         assert len(H[k]) == 2 and all(np.isfinite(H[k]))
     files = set(os.listdir(save))
     assert {"history.csv", "model_last_epoch.pt", "model_epoch_1.pt", "model_epoch_2.pt"} <= files
+    import json
+    assert json.load(open(save / "run_meta.json"))["synthetic_images"] is True
     H2 = mod.main(argv[:-2] + ["--n_epochs", "4", "--resume"])
     assert list(H2["epoch"]) == [1, 2, 3]
 
@@ -150,13 +154,14 @@ def test_eval_robustness_fmnist(tmp_path, mt):
     mod = _acc()
     save = tmp_path / "run"
     mod.main(["--save_path", str(save), "--data_dir", FM_ROOT, "--sample_size", "24", "--n_epochs", "2",
-              "--batch_size", "8", "--model_type", mt])
+              "--batch_size", "8", "--model_type", mt, "--synthetic_images"])
     spec = importlib.util.spec_from_file_location("eval_rob", os.path.join(PKG, "eval_robustness.py"))
     ev = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(ev)
     ck = str(save / "model_last_epoch.pt")
     outs, labels = ev.main(["--checkpoint_path", ck, "--save_path", str(tmp_path / "ev"), "--data_dir", FM_ROOT,
-                            "--sample_size", "24", "--batch_size", "8", "--model_type", mt])
+                            "--sample_size", "24", "--batch_size", "8", "--model_type", mt,
+                            "--synthetic_images"])
     heads = model_configure[mt][1] if mt != "single-model-weight-sharing" else 3
     S = 24
     assert outs.shape == (4, S, heads, 10) and np.isfinite(outs).all()
@@ -166,7 +171,7 @@ def test_eval_robustness_fmnist(tmp_path, mt):
     model = mod.build_model(type("A", (), {"transformer": False, "model_type": mt})())
     model.load_state_dict(torch.load(ck, weights_only=True)["model"])
     model.eval()
-    ds = dataset.FashionMNISTQuarters(FM_ROOT, train=False, seed=42, sample_size=24)
+    ds = dataset.FashionMNISTQuarters(FM_ROOT, train=False, seed=42, sample_size=24, synthetic_images=True)
     x = torch.stack([ds[i][0] for i in range(8)])
     with torch.no_grad():
         if mt == "single-model-weight-sharing":

@@ -115,3 +115,31 @@ def test_device_prefetcher_matches_cpu_path(dev, tmp_path):
         for a, b in ((gt, rt), (gs, rs), (gm, rm), (gy, ry)):
             assert torch.equal(a.cpu(), b)
         assert (gi.cpu() - ri).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("tag,drop,msl", [("d0_m12", 0.0, 12), ("d50_m12", 0.5, 12), ("d50_m512", 0.5, 512)])
+def test_jsonl_collate_match_reference_golden(tag, drop, msl):
+    """Bit-exact A0 pin: tests/golden/a0_contract.npz was written by oracle/gen_golden.py
+    --what a0 running the reference's OWN JsonlDataset / get_labels_and_frequencies /
+    collate_fn / numpy_seed (src/dataset.py:348-438, src/utils.py:167-181) over the committed
+    tests/golden/a0/train.jsonl (empty, 1-token, truncated and 600-word texts, OOV words,
+    missing and dropped images).  Same tokenizer (str.split), vocab and PIL transform here."""
+    import types
+    from oracle.gen_golden import a0_transform, a0_vocab_stoi
+    from src.dataset import JsonlDataset, collate_fn, get_labels_and_frequencies
+    here = os.path.dirname(os.path.abspath(__file__))
+    g = np.load(os.path.join(here, "golden", "a0_contract.npz"))
+    path = os.path.join(here, "golden", "a0", "train.jsonl")
+    labels, freqs = get_labels_and_frequencies(path)
+    assert labels == g["labels"].tolist() and [freqs[k] for k in labels] == g["label_counts"].tolist()
+    vocab = types.SimpleNamespace(stoi=a0_vocab_stoi())
+    ds = JsonlDataset(path, str.split, a0_transform, vocab, len(labels), drop, msl, 3, labels)
+    assert [r["img"] is None for r in ds.data] == g[f"{tag}_img_dropped"].tolist()
+    items = [ds[i] for i in range(len(ds))]
+    assert [len(it[0]) for it in items] == g[f"{tag}_item_lens"].tolist()
+    for lo, hi in ((0, 4), (4, 10)):
+        (txt, seg, mask, img), tgt = collate_fn(items[lo:hi])
+        for k, v in (("text", txt), ("segment", seg), ("mask", mask), ("img", img), ("tgt", tgt)):
+            want = torch.from_numpy(g[f"{tag}_b{lo}_{k}"])
+            assert str(v.dtype) == str(g[f"{tag}_b{lo}_{k}_dtype"]), (tag, lo, k, v.dtype)
+            assert torch.equal(v, want), (tag, lo, k)
