@@ -239,7 +239,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
   for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
   float m_run = NEG_INF, nml = 0.f;  // nml = -m_run * log2e
-  f32x2 lsum[2] = {{0.f, 0.f}, {0.f, 0.f}};  // row-sum partials (packed pairs)
+  // row-sum partials as scalar f32 (packed v_pk_add_f32 / v_pk_fma_f32 beside MFMAs cost more
+  // issue cycles than two scalar ops: MI355X_MICROARCH 'price of one filler beside MFMAs')
+  float lsum[4] = {0.f, 0.f, 0.f, 0.f};
 
   // per tile: waves 0,1 -> K pieces, waves 2,3 -> V pieces (4 each, rows in kperm order);
   // wave 0 also the (unpermuted) mask row
@@ -315,9 +317,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     if (__builtin_amdgcn_ballot_w64(upd)) {
       const float mnew = upd ? mx : m_run;
       const float alpha = upd ? __builtin_amdgcn_exp2f((m_run - mnew) * LOG2E) : 1.0f;  // exp2(-inf) = 0
-      const f32x2 a2 = {alpha, alpha};
-      lsum[0] *= a2;
-      lsum[1] *= a2;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) lsum[i] *= alpha;
 #pragma unroll
       for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
       m_run = mnew;
@@ -331,16 +332,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       if (s2 == 1 && !two) break;
-      // exponent arguments and the row sum as packed f32 pairs (v_pk_fma_f32 / v_pk_add_f32:
-      // half the VALU instructions of the scalar forms), two partial sums per half-wave
-      const f32x2 nml2 = {nml, nml}, lg2 = {LOG2E, LOG2E};
+      // exponent arguments and the row sum as scalar f32 (4 partial sums per lane)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const f32x2 x = f32x2{sc[s2][2 * i], sc[s2][2 * i + 1]} * lg2 + nml2;
-        const f32x2 e = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
-        sc[s2][2 * i] = e.x;
-        sc[s2][2 * i + 1] = e.y;
-        lsum[i & 1] += e;
+      for (int i = 0; i < 16; ++i) {
+        const float e = __builtin_amdgcn_exp2f(fmaf(sc[s2][i], LOG2E, nml));
+        sc[s2][i] = e;
+        lsum[i & 3] += e;
       }
       if (DROP) {
         // one full hash per (row, tile, half, half-wave); its 8 pairs' 32-bit draws come
@@ -399,7 +396,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const int rows = L - q0w < 32 ? L - q0w : 32;
     for (int i = l; i < rows * nkv; i += 64) dst[i] = kbuf[i];
   }
-  const float l_run = (lsum[0].x + lsum[0].y) + (lsum[1].x + lsum[1].y);
+  const float l_run = (lsum[0] + lsum[1]) + (lsum[2] + lsum[3]);
   const float lsum_row = l_run + __shfl_xor(l_run, 32, 64);
   const float inv = (DROP ? 1.0f / (1.0f - p.drop_p) : 1.0f) / lsum_row;
   // O rows through LDS: [32 rows][128 B] per wave, 16-B chunk c of row r at c ^ (r & 7)
@@ -562,7 +559,6 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
       // accumulators): then dS = p (keep ? dp zs : -delta) and dropped-P = keep ? p zs : 0,
       // the keep bit as an all-ones / zero mask (v_bfe_i32 of the row's keep word at this
       // lane's key) bit-selecting between the two; products as packed pairs
-      const f32x2 lg2 = {LOG2E, LOG2E}, mk2 = {mkey, mkey}, zs2 = {zs, zs};
       f32x16 sc, dp;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -576,28 +572,15 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
       }
       f32x16 pz;  // dropped P (for dV)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const f32x2 x = f32x2{sc[2 * i], sc[2 * i + 1]} * lg2 + mk2;
-        const f32x2 pr = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+      for (int r = 0; r < 16; ++r) {
+        const float pr = __builtin_amdgcn_exp2f(fmaf(sc[r], LOG2E, mkey));
         if (DROP) {
-          const f32x2 pzs = pr * zs2, y = f32x2{dp[2 * i], dp[2 * i + 1]} * zs2;
-          f32x2 v;
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const int r = 2 * i + e;
-            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)kwr[r], lane31, 1);
-            pz[r] = __uint_as_float(m & __float_as_uint(pzs[e]));
-            v[e] = __uint_as_float(bfi(m, __float_as_uint(y[e]), __float_as_uint(nd4[r >> 2][r & 3])));
-          }
-          const f32x2 d = pr * v;
-          sc[2 * i] = d.x;
-          sc[2 * i + 1] = d.y;
+          const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)kwr[r], lane31, 1);
+          pz[r] = __uint_as_float(m & __float_as_uint(pr * zs));
+          sc[r] = pr * __uint_as_float(bfi(m, __float_as_uint(dp[r] * zs), __float_as_uint(nd4[r >> 2][r & 3])));
         } else {
-          pz[2 * i] = pr.x;
-          pz[2 * i + 1] = pr.y;
-          const f32x2 d = pr * f32x2{dp[2 * i], dp[2 * i + 1]};
-          sc[2 * i] = d.x;
-          sc[2 * i + 1] = d.y;
+          pz[r] = pr;
+          sc[r] = pr * dp[r];
         }
       }
 #pragma unroll
@@ -663,7 +646,9 @@ constexpr int DQ_NS = 3;  // (the main loop below is unrolled by exactly 3)
 constexpr int DQ_TILE = 64 * 128;                         // 64 keys x 64 d bf16
 constexpr int DQ_STAGE = 2 * DQ_TILE + 256 + 4 * 256;     // K, V, mask row, 4 waves x 32 keep words
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_dq_dma_kernel(AttnParams p) {
+// 3 waves / SIMD: with the softmax math scalar (no v_pk_*_f32) the kernel needs 158 VGPRs
+// (218 with the packed pairs), under the 168 of the 3-wave budget (profiles/r4_attn_scalar_ab.txt)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void attn_dq_dma_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) char smem[DQ_NS * DQ_STAGE];
   const int t = threadIdx.x, l = t & 63, h = l >> 5;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -712,7 +697,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   const float dlt = dsum;
   const float ndz = -dlt / zs;
   const uint32_t ndl_bits = __float_as_uint(-dlt);
-  const f32x2 lg2 = {LOG2E, LOG2E}, zs2 = {zs, zs};
   f32x16 dq[2];
 #pragma unroll
   for (int i = 0; i < 16; ++i) { dq[0][i] = 0.f; dq[1][i] = 0.f; }
@@ -787,20 +771,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
         // (v_bfe_i32) that bit-selects it against -delta (without dropout kw is all ones).
         // Products as packed pairs.
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const f32x2 x = f32x2{sc[2 * i], sc[2 * i + 1]} * lg2;
-          const f32x2 pr = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
-          const f32x2 y = f32x2{dp[2 * i], dp[2 * i + 1]} * zs2;
-          f32x2 v;
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const int r = 2 * i + e, kc = (r & 3) + 8 * (r >> 2);
-            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)kw32, kc, 1);
-            v[e] = __uint_as_float(bfi(m, __float_as_uint(y[e]), ndl_bits));
-          }
-          const f32x2 d = pr * v;
-          sc[2 * i] = d.x;
-          sc[2 * i + 1] = d.y;
+        for (int r = 0; r < 16; ++r) {
+          const float pr = __builtin_amdgcn_exp2f(sc[r] * LOG2E);
+          const int kc = (r & 3) + 8 * (r >> 2);
+          const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)kw32, kc, 1);
+          sc[r] = pr * __uint_as_float(bfi(m, __float_as_uint(dp[r] * zs), ndl_bits));
         }
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {

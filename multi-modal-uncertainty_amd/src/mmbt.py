@@ -269,24 +269,31 @@ class ImageEncoder(nn.Module):
         self.pool = pool(grid)
         # the HIP row-pool covers the default (avg, N x 1 bins); other configs use torch pooling
         self._hip_pool = args.img_embed_pool_type == "avg" and grid[1] == 1
-        # "bf16": MIOpen bf16 autocast (throughput path); "fp32": exact-precision trunk for parity runs
+        # "bf16": the product / bench trunk (HIP stem, BatchNorm, implicit convs, 1x1 GEMMs, pools;
+        # MIOpen for the rest); "fp32": exact-precision torch trunk for parity runs;
+        # "torch_bf16": TEST COMPARATOR only -- the same bf16 arithmetic on PyTorch's own ops
+        # (MIOpen bf16 convs under autocast, torch batch_norm / pools), which measures the noise
+        # floor any bf16 trunk has against the fp32 reference (tests/test_mmbt_gpu.py)
         self.precision = getattr(args, "img_precision", "bf16")
+        assert self.precision in ("bf16", "fp32", "torch_bf16"), self.precision
 
     def trunk(self, x):
+        from . import resnet as R
         train_params = any(p.requires_grad for p in self.model.parameters())
         grad = torch.is_grad_enabled() and (train_params or x.requires_grad)
+        bf16 = self.precision in ("bf16", "torch_bf16")
         # bf16 trunk: the image is cast once here (what autocast would do inside the stem conv),
         # so the stem runs on mmu_stem_conv_* with the store's bf16 filter copy
-        x = x.to(torch.bfloat16 if self.precision == "bf16" else x.dtype, memory_format=torch.channels_last)
-        with torch.set_grad_enabled(grad), torch.autocast("cuda", dtype=torch.bfloat16,
-                                                          enabled=self.precision == "bf16"):
+        x = x.to(torch.bfloat16 if bf16 else x.dtype, memory_format=torch.channels_last)
+        with torch.set_grad_enabled(grad), torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16), \
+                R.torch_ops_only(self.precision == "torch_bf16"):
             return self.model(x)
 
     def forward(self, x):
         if not x.is_cuda:
             raise K.N.NativeError("ImageEncoder: the MI355X path needs the image batch on a HIP device")
         f = self.trunk(x)
-        if self._hip_pool and f.dtype == torch.bfloat16:
+        if self._hip_pool and f.dtype == torch.bfloat16 and self.precision == "bf16":
             return RowPoolFunction.apply(f, self.args.num_image_embeds)
         return torch.flatten(self.pool(f.float()), start_dim=2).transpose(1, 2).contiguous()
 

@@ -19,6 +19,23 @@ import torch.nn as nn
 from . import kernels as K
 
 
+_TORCH_ONLY = [False]
+
+
+class torch_ops_only:
+    """Context (ImageEncoder img_precision "torch_bf16", a TEST comparator): every trunk module
+    takes PyTorch's own path instead of the HIP kernels / store copies."""
+
+    def __init__(self, on=True):
+        self.on, self.prev = bool(on), None
+
+    def __enter__(self):
+        self.prev, _TORCH_ONLY[0] = _TORCH_ONLY[0], self.on or _TORCH_ONLY[0]
+
+    def __exit__(self, *exc):
+        _TORCH_ONLY[0] = self.prev
+
+
 class _BatchNormAct(torch.autograd.Function):
     """Training-mode BatchNorm2d [+ residual] [+ ReLU] on channels-last bf16 via
     mmu_batchnorm_fwd / mmu_batchnorm_bwd (batch statistics, running stats updated)."""
@@ -75,7 +92,7 @@ class BatchNorm2d(nn.BatchNorm2d):
         relu = self.fused_relu if relu is None else relu
         # (the kernels take f32 per-channel parameters / statistics: a module cast to bf16 --
         # module.to(torch.bfloat16) -- takes the torch path)
-        hip = (x.is_cuda and x.dtype == torch.bfloat16 and (skip is None or skip.dtype == torch.bfloat16)
+        hip = (not _TORCH_ONLY[0] and x.is_cuda and x.dtype == torch.bfloat16 and (skip is None or skip.dtype == torch.bfloat16)
                and x.shape[1] % 8 == 0 and self.weight is not None and self.weight.dtype == torch.float32
                and (self.running_mean is None or self.running_mean.dtype == torch.float32))
         if hip:
@@ -383,7 +400,7 @@ class StoreConv2d(nn.Conv2d):
 
     def _compute_weight(self, x):
         src = self._src
-        if (src is not None and x.is_cuda and x.dtype == torch.bfloat16 and self.bias is None and self.groups == 1
+        if (src is not None and not _TORCH_ONLY[0] and x.is_cuda and x.dtype == torch.bfloat16 and self.bias is None and self.groups == 1
                 and self.dilation == (1, 1)):
             store = src[0]()
             if store is not None:
@@ -454,7 +471,7 @@ class MaxPool2d(nn.MaxPool2d):
     channels-last bf16 maps runs the HIP kernels; anything else is PyTorch's."""
 
     def forward(self, x):
-        if (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0
+        if (not _TORCH_ONLY[0] and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0
                 and self.kernel_size in (3, (3, 3)) and self.stride in (2, (2, 2)) and self.padding in (1, (1, 1))
                 and self.dilation in (1, (1, 1)) and not self.ceil_mode and not self.return_indices):
             return _MaxPool3s2.apply(x.contiguous(memory_format=torch.channels_last))

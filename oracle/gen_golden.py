@@ -138,6 +138,28 @@ def gen_mmbt(tag, cfg, B, T, lens, seed=0, wseed=0):
                                   for _, p in model.named_parameters()])
     out["clf_weight_grad"] = model.clf.weight.grad.numpy()
     out["img_proj_bias_grad"] = model.enc.img_embeddings.img_embeddings.bias.grad.numpy()
+    # eval mode on BatchNorm running statistics fitted to this batch: momentum 1 makes one
+    # train-mode pass copy the batch mean / unbiased variance into running_mean / running_var,
+    # so the eval trunk sees normalised activations (the random-init running stats of the
+    # seeded recipe do not normalise them) and a bf16 trunk is comparable at 1e-2
+    for mod in model.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.momentum = 1.0
+    model.train()
+    with torch.no_grad():
+        model(*x)
+    out["bnfit_running_mean_sum"] = np.float64(sum(float(m.running_mean.double().sum()) for m in model.modules()
+                                                   if isinstance(m, torch.nn.BatchNorm2d)))
+    model.eval()
+    with torch.no_grad():
+        lf = model(*x)
+        out["bnfit_logits_full"] = lf.numpy()
+        out["bnfit_loss_eval"] = np.float64(model.compute_loss(lf, y, eval=True))
+        out["bnfit_logits_img_only"] = model.forward_img_only(*x).numpy()
+        out["bnfit_logits_txt_only"] = model.forward_txt_only(*x).numpy()
+        for modal in ("image", "text"):
+            torch.manual_seed(77 if modal == "image" else 78)  # the same index sets as above
+            out[f"bnfit_logits_control_{modal}"] = model.forward_control(*x, modal).numpy()
     os.makedirs(OUT, exist_ok=True)
     np.savez_compressed(os.path.join(OUT, f"mmbt_{tag}.npz"), **out)
     with open(os.path.join(OUT, f"mmbt_{tag}_keys.json"), "w") as f:

@@ -18,7 +18,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, reduce_dtype="float32"):
     try:
         import sys
         here = os.path.dirname(os.path.abspath(__file__))
@@ -32,7 +32,7 @@ def _worker(rank, world, port, q):
         model = MultimodalBertClf(small_args())
         broadcast_parameters(model)
         w_sum = float(model.store.flat.double().sum())
-        bk = GradBucketer(model, bucket_bytes=8 << 20)
+        bk = GradBucketer(model, bucket_bytes=8 << 20, reduce_dtype=getattr(torch, reduce_dtype))
         g = torch.Generator().manual_seed(rank)
         model.store.grad.copy_(torch.randn(model.store.numel(), generator=g))
         launched = []
@@ -53,12 +53,15 @@ def _worker(rank, world, port, q):
         q.put((rank, "ERR", traceback.format_exc()))
 
 
-def test_bucketed_allreduce_matches_mean():
+@pytest.mark.parametrize("reduce_dtype", ["float32", "bfloat16"])
+def test_bucketed_allreduce_matches_mean(reduce_dtype):
+    """f32 buckets: the exact mean; bf16 buckets: the mean to bf16 rounding of the inputs and
+    the sum (two roundings of 2^-9 relative)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, reduce_dtype)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
@@ -74,9 +77,15 @@ def test_bucketed_allreduce_matches_mean():
     from src.testing import small_args
     n = MultimodalBertClf(small_args()).store.numel()
     mean = sum(torch.randn(n, generator=g).double() for g in gens) / world
+    bf16 = reduce_dtype == "bfloat16"
     for rank, w_sum, gsum, head, launched, nb, tail in res:
-        assert abs(gsum - float(mean.sum())) < 1e-3 * abs(float(mean.sum())) + 1e-2
-        torch.testing.assert_close(torch.tensor(head, dtype=torch.float64), mean[:1000], rtol=1e-5, atol=1e-6)
+        assert abs(gsum - float(mean.sum())) < 1e-3 * abs(float(mean.sum())) + (1e1 if bf16 else 1e-2)
+        head = torch.tensor(head, dtype=torch.float64)
+        if bf16:
+            assert (head - mean[:1000]).abs().max() <= 2 * 2 ** -8 * 4.0  # |g| < ~4: two bf16 roundings
+            assert (head - mean[:1000]).abs().max() > 0  # the bf16 path really rounded
+        else:
+            torch.testing.assert_close(head, mean[:1000], rtol=1e-5, atol=1e-6)
         assert launched[-1] >= 1, "no bucket launched during backward"
         assert tail >= 1, "no embedding / trunk bucket launched before finish()"
     assert res[0][1] == res[1][1], "ranks start from different weights"

@@ -127,7 +127,7 @@ def test_bucketer_hooks_average_real_backward(bucket_bytes, side):
         assert n_tail >= 1, "no embedding / trunk bucket launched inside backward"
 
 
-def _parity_worker(rank, world, port, q):
+def _parity_worker(rank, world, port, q, reduce_dtype="float32"):
     try:
         import sys
         here = os.path.dirname(os.path.abspath(__file__))
@@ -170,7 +170,7 @@ def _parity_worker(rank, world, port, q):
         # two ranks, each on its half, bucketed all-reduce inside backward
         m2, o2 = make()
         broadcast_parameters(m2)
-        bk = GradBucketer(m2, bucket_bytes=1 << 20)
+        bk = GradBucketer(m2, bucket_bytes=1 << 20, reduce_dtype=getattr(torch, reduce_dtype))
         sl = slice(rank * B // world, (rank + 1) * B // world)
         for it in range(2):
             o2.zero_grad()
@@ -189,13 +189,18 @@ def _parity_worker(rank, world, port, q):
         q.put((rank, "ERR", traceback.format_exc()))
 
 
-def test_dp_two_ranks_equal_single_device_global_batch():
+@pytest.mark.parametrize("reduce_dtype", ["float32", "bfloat16"])
+def test_dp_two_ranks_equal_single_device_global_batch(reduce_dtype):
     """grads and post-step params of 2 ranks x (B/2) == 1 device x B.
-    Tolerance: the two sides run the same bf16 kernels on different row counts (the
-    weight-gradient split-K sums and MIOpen's fp32 conv algorithms depend on the batch),
-    so they agree to rounding: relative Frobenius error of the gradient <= 1e-2, and of the
-    parameter change of the BertAdam step <= 2e-2."""
-    for rank, gerr, perr, upd in _spawn(_parity_worker, 2):
+    f32 buckets: the two sides agree to f32 summation order -- relative Frobenius error of the
+    averaged gradient and of the BertAdam step's parameter change <= 1e-6 (measured ~1e-7).
+    bf16 buckets (GradBucketer reduce_dtype=torch.bfloat16): every averaged gradient is
+    rounded to 8 significant bits, so <= 1e-2 (measured ~2.4e-3 / 3.3e-3: DESIGN §6's reason
+    to keep the f32 buckets as the default).  The measured errors are printed."""
+    bound = 1e-6 if reduce_dtype == "float32" else 1e-2
+    for rank, gerr, perr, upd in _spawn(_parity_worker, 2, reduce_dtype):
+        print(f"\n[dp parity {reduce_dtype} buckets] rank {rank}: grad rel err {gerr:.3e}, "
+              f"post-step param-change rel err {perr:.3e}")
         assert upd > 0, "the optimizer step changed nothing"
-        assert gerr <= 1e-2, f"rank {rank}: averaged gradient vs global-batch gradient {gerr:.3e}"
-        assert perr <= 2e-2, f"rank {rank}: post-step parameters vs single device {perr:.3e}"
+        assert gerr <= bound, f"rank {rank}: averaged gradient vs global-batch gradient {gerr:.3e}"
+        assert perr <= bound, f"rank {rank}: post-step parameters vs single device {perr:.3e}"

@@ -81,32 +81,147 @@ def test_forward_control_draws_reference_indices(dev, small):
     assert torch.equal(a, b)
 
 
-def test_train_step_grads_match_reference_golden(dev):
-    """train mode (BN batch stats) with BERT dropout 0: loss + every per-tensor grad norm."""
-    g = np.load(os.path.join(GOLD, "mmbt_small_t16.npz"))
-    names = json.load(open(os.path.join(GOLD, "mmbt_small_t16_keys.json")))["named_parameters"]
-    model, sd, cfg = build("small", dev, bert_hidden_dropout=0.0, bert_attn_dropout=0.0)
+GRAD_REL = 1e-2  # north star: 1e-2 for bf16
+NOISE_X = 2.0    # a bf16 trunk tensor may be off by up to NOISE_X x what PyTorch's own bf16 trunk is
+
+
+def _golden_batch(g, cfg, dev):
     from src.testing import synthetic_batch
-    x, y = synthetic_batch(2, 16, lens=[16, 9], vocab=cfg.vocab, seed=0)
-    x = tuple(t.to(dev) for t in x)
+    x = tuple(torch.from_numpy(g[k]).to(dev) for k in ("text", "segment", "mask"))
+    (_, _, _, img), _ = synthetic_batch(2, g["text"].shape[1], vocab=cfg.vocab, lens=None, seed=int(g["seed"]))
+    assert abs(float(img.double().sum()) - float(g["img_sum"])) < 1e-3
+    return x + (img.to(dev),), torch.from_numpy(g["y"]).to(dev)
+
+
+def _train_step(cfgname, g, dev, prec):
+    """one train-mode forward + backward (BERT dropout 0) -> loss, {name: grad norm}, clf grad, proj bias grad"""
+    model, sd, cfg = build(cfgname, dev, bert_hidden_dropout=0.0, bert_attn_dropout=0.0, img_precision=prec)
+    x, y = _golden_batch(g, cfg, dev)
     model.train()
     model.store.zero_grad()
-    loss = model.compute_loss(model(*x), y.to(dev))
+    loss = model.compute_loss(model(*x), y)
     loss.backward()
-    assert abs(loss.item() - float(g["loss_train"])) < 1e-2 * abs(float(g["loss_train"]))
+    torch.cuda.synchronize()
+    norms = {n: p.grad.double().norm().item() for n, p in model.named_parameters()}
     got = dict(model.named_parameters())
-    bad = []
-    # floor: key biases have an exactly-zero true gradient (softmax shift invariance); the
-    # reference reads ~1e-9, bf16 arithmetic ~1e-5 -- both are noise next to the real grads
+    out = (loss.item(), norms, got["clf.weight"].grad.cpu(), got["enc.img_embeddings.img_embeddings.bias"].grad.cpu())
+    del model
+    torch.cuda.empty_cache()
+    return out
+
+
+def _rel(a, b):
+    return abs(a - b) / max(abs(b), 1e-30)
+
+
+@pytest.mark.parametrize("tag,cfgname,prec", [("small_t16", "small", "fp32"), ("small_t16", "small", "bf16"),
+                                              ("full_t508", "full", "fp32"), ("full_t508", "full", "bf16")])
+def test_train_step_grads_match_reference_golden(dev, tag, cfgname, prec):
+    """Train mode (BN batch statistics), BERT dropout 0, against the reference's own train-mode
+    loss and per-tensor gradient norms (oracle/gen_golden.py gen_mmbt).  prec "bf16" is the
+    product / bench trunk: HIP stem conv, BatchNorm(+res)(+ReLU), implicit / strided convs,
+    1x1 GEMMs, max-pool, row-pool; "fp32" routes the trunk to torch fp32 convs.  Both run the
+    full ResNet-152 + 12-layer BERT for full_t508.
+    Bar: loss within 1e-2 (relative); every per-tensor gradient norm within 1e-2 (relative)
+    above the noise floor 1e-4 * max norm (key biases have an exactly-zero true gradient:
+    softmax shift invariance; the reference reads ~1e-9, bf16 arithmetic ~1e-5).  For the
+    bf16 trunk the bar of a trunk tensor is max(1e-2, NOISE_X x the relative error of
+    PyTorch's own bf16 trunk on the same step) -- img_precision "torch_bf16", MIOpen bf16
+    convs + torch BatchNorm: the gradients of the stem / layer1 pass back through ~150 bf16
+    layers and no bf16 implementation holds them to 1e-2 (measured and printed here)."""
+    g = np.load(os.path.join(GOLD, f"mmbt_{tag}.npz"))
+    names = json.load(open(os.path.join(GOLD, f"mmbt_{tag}_keys.json")))["named_parameters"]
+    ref = dict(zip(names, (float(v) for v in g["grad_norms"])))
+    loss, norms, clf_g, proj_g = _train_step(cfgname, g, dev, prec)
+    tnorms = tproj_g = None
+    if prec == "bf16":
+        _, tnorms, _, tproj_g = _train_step(cfgname, g, dev, "torch_bf16")
+    lerr = _rel(loss, float(g["loss_train"]))
     floor = 1e-4 * float(np.max(g["grad_norms"]))
-    for n, ref_norm in zip(names, g["grad_norms"]):
-        gn = got[n].grad.double().norm().item()
-        if not abs(gn - ref_norm) <= 0.05 * ref_norm + floor:
-            bad.append((n, gn, float(ref_norm)))
-    assert not bad, f"{len(bad)} grad norms off, e.g. {bad[:5]}"
-    tol_check(got["clf.weight"].grad.cpu(), g["clf_weight_grad"], rel=3e-2, what="clf grad")
-    tol_check(got["enc.img_embeddings.img_embeddings.bias"].grad.cpu(), g["img_proj_bias_grad"], rel=5e-2,
-              what="img proj bias grad")
+    bad, rows = [], []
+    for n in names:
+        e = _rel(norms[n], ref[n])
+        bar = GRAD_REL
+        te = None
+        if tnorms is not None and "img_encoder" in n:
+            te = _rel(tnorms[n], ref[n])
+            bar = max(GRAD_REL, NOISE_X * te)
+        if ref[n] > floor:
+            rows.append((n, e, te))
+        if not abs(norms[n] - ref[n]) <= bar * ref[n] + floor:
+            bad.append((n, norms[n], ref[n], e, te))
+    rows.sort(key=lambda r: -r[1])
+    msg = (f"\n[{tag} {prec}] loss rel err {lerr:.2e}; grad-norm rel err over {len(rows)} tensors above the floor: "
+           f"max {rows[0][1]:.2e} ({rows[0][0]}), median {rows[len(rows) // 2][1]:.2e}")
+    if tnorms is not None:
+        trows = sorted((r[2] for r in rows if r[2] is not None), reverse=True)
+        hrows = sorted((r[1] for r in rows if r[2] is not None), reverse=True)
+        msg += (f"; trunk tensors: HIP max {hrows[0]:.2e} median {hrows[len(hrows) // 2]:.2e} vs torch bf16 max "
+                f"{trows[0]:.2e} median {trows[len(trows) // 2]:.2e}; > 1e-2: HIP {sum(h > GRAD_REL for h in hrows)}, "
+                f"torch {sum(t > GRAD_REL for t in trows)} of {len(trows)}")
+        # the HIP trunk as a whole no noisier than PyTorch's own bf16 trunk
+        assert hrows[len(hrows) // 2] <= NOISE_X * trows[len(trows) // 2] + 1e-3, msg
+    print(msg)
+    assert lerr < 1e-2, f"train loss {loss:.6f} vs {float(g['loss_train']):.6f}"
+    assert not bad, f"{len(bad)} of {len(names)} grad norms off: worst {sorted(bad, key=lambda r: -r[3])[:5]}"
+    tol_check(clf_g, g["clf_weight_grad"], rel=1e-2, what="clf grad")
+    # the image projection's bias gradient is the trunk features' gradient summed: it carries
+    # the trunk's noise (bar as for a trunk tensor)
+    ref_p = g["img_proj_bias_grad"]
+    prel = 2e-2
+    if tproj_g is not None:
+        prel = max(prel, NOISE_X * float(np.abs(tproj_g.numpy() - ref_p).max() / np.abs(ref_p).max()))
+    tol_check(proj_g, ref_p, rel=prel, what="img proj bias grad")
+
+
+def _bnfit_logits(cfgname, g, dev, prec):
+    model, sd, cfg = build(cfgname, dev, img_precision=prec, bert_hidden_dropout=0.0, bert_attn_dropout=0.0)
+    x, y = _golden_batch(g, cfg, dev)
+    bns = [m for m in model.modules() if isinstance(m, torch.nn.BatchNorm2d)]
+    assert bns
+    for m in bns:
+        m.momentum = 1.0
+    model.train()
+    with torch.no_grad():
+        model(*x)
+    rm = sum(float(m.running_mean.double().sum()) for m in bns)
+    model.eval()
+    out = {}
+    with torch.no_grad():
+        out["full"] = model(*x)
+        out["img_only"] = model.forward_img_only(*x)
+        out["txt_only"] = model.forward_txt_only(*x)
+        for modal in ("image", "text"):
+            idx = torch.from_numpy(g[f"indices_control_{modal}"])
+            out[f"control_{modal}"] = model.clf(model.enc._variant(*x, idx))
+        loss = model.compute_loss(out["full"], y, eval=True).item()
+    del model
+    torch.cuda.empty_cache()
+    return {k: v.float().cpu().numpy() for k, v in out.items()}, loss, rm
+
+
+@pytest.mark.parametrize("tag,cfgname", [("small_t16", "small"), ("full_t508", "full")])
+def test_bnfit_eval_variants_bf16_trunk_match_reference_golden(dev, tag, cfgname):
+    """The product-precision (bf16 HIP) trunk in eval mode, on BatchNorm running statistics
+    fitted to the batch (momentum 1, one train-mode pass: the fixture's bnfit_* entries, made
+    the same way by the reference model), so the trunk's activations are normalised: logits of
+    all 5 variants (full, image-only, text-only, both controls).  Bar per variant:
+    max(1e-2, NOISE_X x PyTorch's own bf16 trunk's error) * max|logit| (printed)."""
+    g = np.load(os.path.join(GOLD, f"mmbt_{tag}.npz"))
+    got, loss, rm = _bnfit_logits(cfgname, g, dev, "bf16")
+    tgot, _, _ = _bnfit_logits(cfgname, g, dev, "torch_bf16")
+    assert abs(rm - float(g["bnfit_running_mean_sum"])) <= 2e-2 * abs(float(g["bnfit_running_mean_sum"])) + 1e-2
+    errs = {}
+    for v in ("full", "img_only", "txt_only", "control_image", "control_text"):
+        ref = g[f"bnfit_logits_{v}"]
+        scale = np.abs(ref).max()
+        e, te = np.abs(got[v] - ref).max() / scale, np.abs(tgot[v] - ref).max() / scale
+        errs[v] = (e, te)
+    print(f"\n[{tag} bnfit] logits rel err per variant (HIP bf16 trunk, torch bf16 trunk): "
+          + ", ".join(f"{k} {e:.2e} / {te:.2e}" for k, (e, te) in errs.items()))
+    for v, (e, te) in errs.items():
+        assert e <= max(1e-2, NOISE_X * te), f"bnfit {v}: {e:.3e} (torch bf16 trunk {te:.3e})"
+    assert abs(loss - float(g["bnfit_loss_eval"])) < 1e-2 * abs(float(g["bnfit_loss_eval"]))
 
 
 def test_bertadam_fused_matches_restatement_on_model(dev, small):
