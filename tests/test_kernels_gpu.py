@@ -203,6 +203,32 @@ def test_gemm_partial_last_wave(dev, Kd):
     close(f[tl], ref[tl] + 0.25)
 
 
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, False), (False, True)])
+def test_gemm_many_tiles_every_element(dev, ak, bk):
+    """More tiles than CUs (40 x 9 = 360 tiles; batch 2 x 20 x 9 = 360 items), a ragged last
+    wave, checked on EVERY element (not just the last tile row) for a bf16 epilogue and for
+    f32 accumulate, in every operand layout."""
+    k = K()
+    M, N, Kd = 256 * 40 - 96, 2304, 320
+    Ma = M if ak else 256 * 40
+    A = rnd(Ma, Kd, dev=dev, seed=81) if ak else rnd(Kd, Ma, dev=dev, seed=81)
+    B = rnd(N, Kd, dev=dev, seed=82, scale=0.1) if bk else rnd(Kd, N, dev=dev, seed=82, scale=0.1)
+    bias = torch.randn(N, device=dev) * 0.1
+    ref = op(A, ak, Ma, Kd) @ op(B, bk, N, Kd).t()
+    out = torch.empty(Ma, N, dtype=torch.bfloat16, device=dev)
+    k.gemm(A, A.shape[1], ak, B, B.shape[1], bk, out, N, Ma, N, Kd, epi=k.epilogue(k.EPI_STORE, bias=bias))
+    close(out, ref + bias)
+    f = torch.full((Ma, N), -1.5, dtype=torch.float32, device=dev)
+    k.gemm(A, A.shape[1], ak, B, B.shape[1], bk, f, N, Ma, N, Kd, epi=k.epilogue(k.EPI_STORE, accumulate=True))
+    torch.testing.assert_close(f, ref - 1.5, rtol=1e-4, atol=5e-3)
+    if ak and bk:  # batched items
+        Bt, Mb = 2, 256 * 20
+        A2, B2 = rnd(Bt, Mb, Kd, dev=dev, seed=83), rnd(Bt, N, Kd, dev=dev, seed=84, scale=0.1)
+        C2 = torch.empty(Bt, Mb, N, dtype=torch.bfloat16, device=dev)
+        k.gemm(A2, Kd, True, B2, Kd, True, C2, N, Mb, N, Kd, batch=Bt, sA=Mb * Kd, sB=N * Kd, sC=Mb * N)
+        close(C2, A2.float() @ B2.float().transpose(1, 2))
+
+
 def test_gemm_partial_last_wave_batched(dev):
     """batch 2 x 129 tile rows x 3 column tiles = 774 tiles, per-item bias"""
     k = K()

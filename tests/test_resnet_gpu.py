@@ -105,11 +105,12 @@ def test_stem_conv_matches_torch(dev, n, h, w):
 
 
 @pytest.mark.parametrize("n,cin,cout,h,w", [(2, 256, 256, 14, 14), (3, 512, 512, 7, 13), (4, 64, 384, 9, 11),
-                                             (16, 256, 256, 14, 14)])
+                                             (16, 256, 256, 14, 14), (96, 256, 256, 28, 28)])
 def test_conv3x3_implicit_matches_torch(dev, n, cin, cout, h, w):
     """mmu_conv3x3_implicit (im2col gathered in the A-operand DMA) as the 3x3 conv forward
     (filter as stored, channels-last) and as its data gradient (flipped filter transposed to
-    [Cin][3][3][Cout]) against torch's fp32 conv on the same bf16 inputs."""
+    [Cin][3][3][Cout]) against torch's fp32 conv on the same bf16 inputs.  96 x 28 x 28:
+    294 tiles, more than one wave of tiles on 256 CUs."""
     from src import kernels as K
     cl = torch.channels_last
     g = torch.Generator(device=dev).manual_seed(cin + w)
