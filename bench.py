@@ -15,6 +15,9 @@ per rank instead ("scaling": "weak"; DESIGN.md §6 has both).
                                        (src/model.py) train step on synthetic embeddings
   python bench.py --workload uncertainty   BASELINE config 3: 5-member deep ensemble x
                                        MC-dropout T=30 evaluation (NLL / ECE) of MMBT
+  python bench.py --workload encoders  BASELINE config 5's producer: the FLAVA image + text
+                                       encoders (data/encoding_with_flava.py) on HIP kernels
+  python bench.py --workload vilt      ViLT classification inference (train.py setup_vilt model)
 
 Rank 0 prints one JSON line (see README/DESIGN for the field definitions).
 """
@@ -50,7 +53,8 @@ def parse():
                     help="samples per rank per step instead (weak scaling)")
     ap.add_argument("--text-len", type=int, default=508, help="word-pieces per sample (L = 5 + this)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", default="mmbt", choices=["mmbt", "flava", "uncertainty"])
+    ap.add_argument("--workload", default="mmbt", choices=["mmbt", "flava", "uncertainty", "encoders", "vilt"])
+    ap.add_argument("--enc-batch", type=int, default=128, help="encoders / vilt: samples per rank per step")
     ap.add_argument("--members", type=int, default=5, help="uncertainty: deep-ensemble members K")
     ap.add_argument("--mc-samples", type=int, default=30, help="uncertainty: MC-dropout passes T")
     ap.add_argument("--eval-batch", type=int, default=32, help="uncertainty: samples per rank per step")
@@ -386,6 +390,109 @@ def bench_uncertainty(args, world, rank, dev):
     return out
 
 
+def _encoder_cpu_baseline(args, run, B, what):
+    """the transformers module itself (the reference's own third-party encoder: the class it
+    loads pretrained) in fp32 on host cores, B samples, 1 warm-up + 2 timed calls"""
+    torch.set_num_threads(_cpu_threads(args))
+    with torch.no_grad():
+        run()
+        n = 2
+        t0 = time.perf_counter()
+        for _ in range(n):
+            run()
+        dt = time.perf_counter() - t0
+    return {"value": round(B * n / dt, 3), "unit": "samples/s", "cores": _cpu_threads(args), "kind": "reference",
+            "sample": f"transformers {what} fp32 forward (random init, eval), B={B}, {n} timed calls after 1 warm-up, "
+                      f"torch CPU {torch.get_num_threads()} threads"}
+
+
+def bench_encoders(args, world, rank, dev):
+    """BASELINE config 5's producer (reference data/encoding_with_flava.py:11-41): FLAVA image
+    (224^2 -> 197 tokens) + text (77 tokens) encoders of a transformers FlavaModel on the HIP
+    kernels (src/flava_encoders.py), B memes per rank per step; --workload vilt: ViLT
+    classification (train.py setup_vilt: ViltForImagesAndTextClassification, 384^2 image ->
+    145 tokens + 40 text tokens, src/vilt.py).  Random-init weights (no offline checkpoint),
+    synthetic inputs; samples shard over ranks (weak scaling, no exchange)."""
+    from src import kernels as K
+    vilt = args.workload == "vilt"
+    B = args.enc_batch
+    torch.manual_seed(1234)
+    g = torch.Generator().manual_seed(300 + rank)
+    if vilt:
+        from transformers import ViltConfig, ViltForImagesAndTextClassification
+        from src.vilt import ViltHIP
+        cfg = ViltConfig(num_images=1, num_labels=2)
+        ref = ViltForImagesAndTextClassification(cfg).eval()
+        hip = ViltHIP(ref, dev)
+        Lt = cfg.max_position_embeddings
+        ids = torch.randint(1000, cfg.vocab_size, (B, Lt), generator=g)
+        pix = torch.randn(B, 1, 3, cfg.image_size, cfg.image_size, generator=g)
+        mask = torch.ones(B, Lt, dtype=torch.long)
+        inputs = [t.to(dev) for t in (ids, mask)] + [None, pix.to(dev), None]
+        L_tok = Lt + (cfg.image_size // cfg.patch_size) ** 2 + 1
+        passes = [(L_tok, cfg.num_hidden_layers)]
+        run = lambda: hip(*inputs)  # noqa: E731
+        cpu_run = lambda: ref(input_ids=ids[:2], attention_mask=mask[:2], pixel_values=pix[:2])  # noqa: E731
+        what = "ViltForImagesAndTextClassification"
+    else:
+        from transformers import FlavaConfig, FlavaModel
+        from src.flava_encoders import FlavaEncodersHIP
+        ref = FlavaModel(FlavaConfig()).eval()
+        hip = FlavaEncodersHIP(ref, dev)
+        Lt, Li = 77, 197
+        ids = torch.randint(1000, 30000, (B, Lt), generator=g)
+        pix = torch.randn(B, 3, 224, 224, generator=g)
+        mask = torch.ones(B, Lt, dtype=torch.long)
+        inputs = (pix.to(dev), ids.to(dev), mask.to(dev))
+        passes = [(Li, ref.config.image_config.num_hidden_layers), (Lt, ref.config.text_config.num_hidden_layers)]
+        run = lambda: hip(*inputs)  # noqa: E731
+        cpu_run = lambda: (ref.image_model(pixel_values=pix[:2]), ref.text_model(input_ids=ids[:2],  # noqa: E731
+                                                                                 attention_mask=mask[:2]))
+        what = "FlavaModel image_model + text_model"
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    K.timing_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    gemm_ms, gemm_n, gemm_flop = K.timing_read()
+    K.timing_enable(False)
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    H = 768
+    # forward FLOPs per sample: sum over the encoder passes of layers * L (24 H^2 + 4 L H)
+    flop_sample = sum(n * L * (24 * H * H + 4 * L * H) for L, n in passes)
+    ms_step = 1000.0 * dt / args.steps
+    gemm_tf = gemm_flop / (gemm_ms * 1e-3) / 1e12 if gemm_ms else 0.0
+    out = {
+        "metric": ("ViLT classification inference samples/sec" if vilt else
+                   "FLAVA image+text encoding samples/sec (BASELINE config 5 producer, Hateful Memes)"),
+        "value": round(B * world * args.steps / dt, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded images / token ids; random-init weights)",
+        "config": {"workload": "vilt_classification" if vilt else "flava_encoders",
+                   "model": what, "per_rank_batch": B, "global_batch": B * world,
+                   "tokens": "+".join(str(L) for L, _ in passes), "parallelism": f"dp{world}"},
+        # every encoder-layer mmu_gemm launch bracketed by HIP events on its stream
+        "roofline": {"bound": "mfma", "achieved": round(gemm_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(gemm_tf / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "gemm_launches_timed": gemm_n, "gemm_ms_per_step": round(gemm_ms / args.steps, 3)},
+        "model_tflops_achieved": round(flop_sample * B * world / (ms_step * 1e-3) / 1e12, 1),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = _encoder_cpu_baseline(args, cpu_run, 2, what)
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -396,8 +503,10 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
-    if args.workload in ("flava", "uncertainty"):
-        out = (bench_flava if args.workload == "flava" else bench_uncertainty)(args, world, rank, dev)
+    if args.workload in ("flava", "uncertainty", "encoders", "vilt"):
+        fn = {"flava": bench_flava, "uncertainty": bench_uncertainty, "encoders": bench_encoders,
+              "vilt": bench_encoders}[args.workload]
+        out = fn(args, world, rank, dev)
         if rank == 0:
             print(json.dumps(out), flush=True)
         if world > 1:
