@@ -53,6 +53,8 @@ def parse():
                     help="samples per rank per step instead (weak scaling)")
     ap.add_argument("--text-len", type=int, default=508, help="word-pieces per sample (L = 5 + this)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sync-bn", action="store_true",
+                    help="mmbt, N > 1: the trunk's BatchNorms normalise over the whole global batch (cross-rank sums)")
     ap.add_argument("--workload", default="mmbt", choices=["mmbt", "flava", "uncertainty", "encoders", "vilt"])
     ap.add_argument("--enc-batch", type=int, default=128, help="encoders / vilt: samples per rank per step")
     ap.add_argument("--members", type=int, default=5, help="uncertainty: deep-ensemble members K")
@@ -529,7 +531,7 @@ def main():
     from src.optim import BertAdam
     from src.testing import make_args, synthetic_batch
     from src import kernels as K
-    from src.dp import GradBucketer, broadcast_parameters
+    from src.dp import GradBucketer, broadcast_parameters, convert_sync_batchnorm
     from src import encoder
 
     # MIOpen solver choice for the ResNet convs: "find" mode over the find-db shipped in
@@ -547,6 +549,8 @@ def main():
     bucketer = None
     if world > 1:
         broadcast_parameters(model)
+        if args.sync_bn:
+            convert_sync_batchnorm(model)
         bucketer = GradBucketer(model)
     x, y = synthetic_batch(B, T, seed=100 + rank, device=dev)
     model.train()
@@ -602,6 +606,7 @@ def main():
         "config": {"workload": "mmbt_train_step", "model": "MMBT bert-base-uncased + resnet152",
                    "global_batch": args.global_batch, "per_rank_batch": B, "seq_len": 512, "tokens": L,
                    "parallelism": f"dp{world}", "grad_accum": 1, "optimizer": "BertAdam (fused HIP)",
+                   "batchnorm": "whole-batch (cross-rank sums)" if (args.sync_bn and world > 1) else "per-rank batch",
                    "trainable_params": sum(p.numel() for p in model.parameters())},
         "roofline": {"bound": "mfma", "kernel": "mmu_gemm (all BERT-layer GEMMs, fwd + bwd)",
                      "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",

@@ -338,6 +338,34 @@ int mmu_batchnorm_bwd(const void* dY, const void* Y, const void* relu_mask, cons
                       void* dX, void* dSkip, float* dweight, float* dbias, void* ws, int64_t ws_bytes,
                       mmu_stream_t stream);
 
+/* Cross-rank (synchronised) BatchNorm: data-parallel training that keeps the reference's
+ * whole-batch statistics (src/mmbt.py:19-21 normalises the trunk over the full batch of one
+ * device; under DP the batch is split over ranks).  Each training pass is split at its
+ * per-channel reduction and the caller sums `sums` over the ranks between the two calls
+ * (one all-reduce of 2C+1 doubles; torch.nn.SyncBatchNorm's exchange):
+ *   sums [2C+1] f64 = {s1[0..C), s2[0..C), rows}
+ *   forward:  mmu_batchnorm_stats (s1 = sum x, s2 = sum x^2 over the local rows), exchange,
+ *             mmu_batchnorm_fwd_sums (the training forward of mmu_batchnorm_fwd with the
+ *             statistics of the exchanged sums: mean, biased variance over sums[2C] rows;
+ *             running stats from the unbiased variance of the same)
+ *   backward: mmu_batchnorm_bwd_reduce (s1 = sum g, s2 = sum g (x - mean); dweight / dbias
+ *             += this rank's dgamma = s2 * invstd, dbeta = s1, may be NULL), exchange,
+ *             mmu_batchnorm_bwd_sums (dX [, dSkip] from the exchanged sums).
+ * Arguments otherwise as mmu_batchnorm_fwd / mmu_batchnorm_bwd. */
+int mmu_batchnorm_stats(const void* X, int64_t rows, int64_t C, double* sums, void* ws, int64_t ws_bytes,
+                        mmu_stream_t stream);
+int mmu_batchnorm_fwd_sums(const void* X, const void* skip, void* Y, int64_t rows, int64_t C, const double* sums,
+                           const float* weight, const float* bias, float* running_mean, float* running_var,
+                           int64_t* num_batches_tracked, float momentum, float eps, int relu, float* save_mean,
+                           float* save_invstd, void* relu_mask, void* ws, int64_t ws_bytes, mmu_stream_t stream);
+int mmu_batchnorm_bwd_reduce(const void* dY, const void* Y, const void* relu_mask, const void* X, int64_t rows,
+                             int64_t C, const float* save_mean, const float* save_invstd, int relu, double* sums,
+                             float* dweight, float* dbias, void* ws, int64_t ws_bytes, mmu_stream_t stream);
+int mmu_batchnorm_bwd_sums(const void* dY, const void* Y, const void* relu_mask, const void* X, int64_t rows,
+                           int64_t C, const double* sums, const float* weight, const float* save_mean,
+                           const float* save_invstd, int relu, void* dX, void* dSkip, void* ws, int64_t ws_bytes,
+                           mmu_stream_t stream);
+
 /* ------------------------------------------------------------------ BertAdam
  * Fused multi-tensor BertAdam (pytorch_pretrained_bert 0.6.x, constructed at
  * train.py:142-147; stepped at src/framework.py:303): per-tensor clip

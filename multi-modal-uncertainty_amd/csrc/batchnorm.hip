@@ -17,6 +17,11 @@
 // 10.25 instead of 14 B per element (without a mask it reads Y itself).
 // Semantics of torch.nn.BatchNorm2d in training mode: biased variance normalises, the
 // running variance is updated with the unbiased one, momentum-weighted.
+// Cross-rank statistics (data-parallel training with the reference's whole-batch BatchNorm):
+// each pass splits at its finalize -- the reduce pass's block partials are summed into
+// per-channel f64 sums (+ the row count) that the caller all-reduces across ranks, and the
+// finalize + apply then run from the exchanged sums (SyncBatchNorm semantics: the weight /
+// bias gradients stay per-rank, summed by the gradient all-reduce like every other one).
 //
 // Work split: a block owns a chunk of CH <= 512 channels (grid.y) and a range of rows
 // (grid.x) sized to 4 K - 64 K elements (~1 K blocks per launch, see bn_grid); a thread owns 8 consecutive channels (16-B bf16
@@ -126,14 +131,46 @@ __global__ __launch_bounds__(BN_THREADS) void bn_stats_kernel(const bf16* __rest
 }
 
 // per channel: coef = {scale, shift}; batch (partials) or running statistics
-__global__ __launch_bounds__(BN_THREADS) void bn_fwd_finalize_kernel(
-    const float2* __restrict__ part, int nparts, int64_t rows, int C, const float* w, const float* b, float* rmean,
-    float* rvar, int training, float momentum, float eps, float* smean, float* sinvstd, int64_t* nbt,
-    float* __restrict__ coef) {
+// the two per-channel totals of a pass: from the block partials, or (gsum != nullptr) from the
+// exchanged cross-rank sums {s1[C], s2[C], rows} (then *n = their row count)
+static __device__ __forceinline__ bool bn_channel_sums(const float2* __restrict__ part, int nparts,
+                                                       const double* __restrict__ gsum, int C, int& c, double& s1,
+                                                       double& s2, double* n) {
+  if (!gsum) return bn_sum_parts(part, nparts, C, c, s1, s2);
+  if (threadIdx.x >= BN_FIN_CH) return false;
+  c = blockIdx.x * BN_FIN_CH + threadIdx.x;
+  if (c >= C) return false;
+  s1 = gsum[c];
+  s2 = gsum[C + c];
+  *n = gsum[2 * C];
+  return true;
+}
+
+// the local per-channel sums of a reduce pass for the exchange: sums = {s1[C], s2[C], rows};
+// the backward's (sinvstd != nullptr) also accumulates this rank's dweight / dbias
+__global__ __launch_bounds__(BN_THREADS) void bn_local_sums_kernel(const float2* __restrict__ part, int nparts,
+                                                                    int64_t rows, int C, double* __restrict__ sums,
+                                                                    const float* sinvstd, float* dw, float* db) {
   int c;
-  double s1 = 0.0, s2 = 0.0;
+  double s1, s2;
+  if (!bn_sum_parts(part, nparts, C, c, s1, s2)) return;
+  sums[c] = s1;
+  sums[C + c] = s2;
+  if (c == 0) sums[2 * C] = (double)rows;
+  if (sinvstd) {
+    if (dw) dw[c] += (float)(s2 * (double)sinvstd[c]);
+    if (db) db[c] += (float)s1;
+  }
+}
+
+__global__ __launch_bounds__(BN_THREADS) void bn_fwd_finalize_kernel(
+    const float2* __restrict__ part, int nparts, const double* __restrict__ gsum, int64_t rows, int C,
+    const float* w, const float* b, float* rmean, float* rvar, int training, float momentum, float eps,
+    float* smean, float* sinvstd, int64_t* nbt, float* __restrict__ coef) {
+  int c;
+  double s1 = 0.0, s2 = 0.0, n = (double)rows;
   if (training) {
-    if (!bn_sum_parts(part, nparts, C, c, s1, s2)) return;
+    if (!bn_channel_sums(part, nparts, gsum, C, c, s1, s2, &n)) return;
   } else {
     const int t = threadIdx.x;
     if (t >= BN_FIN_CH) return;
@@ -142,8 +179,8 @@ __global__ __launch_bounds__(BN_THREADS) void bn_fwd_finalize_kernel(
   }
   double mean, var;
   if (training) {
-    mean = s1 / (double)rows;
-    var = s2 / (double)rows - mean * mean;
+    mean = s1 / n;
+    var = s2 / n - mean * mean;
     if (var < 0.0) var = 0.0;
   } else {
     mean = rmean[c];
@@ -158,7 +195,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_fwd_finalize_kernel(
     if (smean) { smean[c] = (float)mean; sinvstd[c] = invstd; }
     if (rmean) {
       rmean[c] = (1.0f - momentum) * rmean[c] + momentum * (float)mean;
-      rvar[c] = (1.0f - momentum) * rvar[c] + momentum * (float)(var * (double)rows / (double)(rows - 1));
+      rvar[c] = (1.0f - momentum) * rvar[c] + momentum * (float)(var * n / (n - 1.0));
     }
     if (nbt && c == 0) *nbt += 1;
   }
@@ -251,17 +288,18 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_reduce_kernel(const bf16* _
 }
 
 // coef = {k1, k2, k0}: dx = k1*g + k2*x + k0 ; dweight += dgamma, dbias += dbeta
+// (gsum: the exchanged cross-rank sums; dweight / dbias were accumulated from the local ones)
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_finalize_kernel(const float2* __restrict__ part, int nparts,
+                                                                      const double* __restrict__ gsum,
                                                                       int64_t rows, int C, const float* w,
                                                                       const float* smean, const float* sinvstd,
                                                                       float* dw, float* db, float* __restrict__ coef) {
   int c;
-  double dbeta, sgx;
-  if (!bn_sum_parts(part, nparts, C, c, dbeta, sgx)) return;
+  double dbeta, sgx, n = (double)rows;
+  if (!bn_channel_sums(part, nparts, gsum, C, c, dbeta, sgx, &n)) return;
   const double invstd = sinvstd[c], mean = smean[c];
   const double dgamma = sgx * invstd;
   const double a = (w ? (double)w[c] : 1.0) * invstd;
-  const double n = (double)rows;
   const double k2 = -a * invstd * dgamma / n;
   coef[c] = (float)a;
   coef[C + c] = (float)k2;
@@ -343,9 +381,15 @@ void batchnorm_fwd_launch(const BnFwdParams& q, hipStream_t s) {
   const int nparts = (int)G.grid.x;
   float* coef = (float*)q.ws;
   float2* part = (float2*)(coef + ((3 * q.C + 3) & ~3));
-  if (q.training)
+  const dim3 fin((q.C + BN_FIN_CH - 1) / BN_FIN_CH);
+  if (q.training && !q.gsum)
     hipLaunchKernelGGL(bn_stats_kernel, G.grid, dim3(BN_THREADS), 0, s, q.X, q.rows, q.C, G.CH, G.rpb, part);
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((q.C + BN_FIN_CH - 1) / BN_FIN_CH), dim3(BN_THREADS), 0, s, part, nparts, q.rows, q.C,
+  if (q.lsum) {  // cross-rank statistics, first half: the local sums for the exchange
+    hipLaunchKernelGGL(bn_local_sums_kernel, fin, dim3(BN_THREADS), 0, s, part, nparts, q.rows, q.C, q.lsum,
+                       nullptr, nullptr, nullptr);
+    return;
+  }
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, fin, dim3(BN_THREADS), 0, s, part, nparts, q.gsum, q.rows, q.C,
                      q.w, q.b, q.rmean, q.rvar, q.training, q.momentum, q.eps, q.smean, q.sinvstd, q.nbt, coef);
   const bool sk = q.skip != nullptr, mk = q.relu && q.mask != nullptr;
 #define BN_APPLY(SK, RL, MK)                                                                                    \
@@ -366,15 +410,23 @@ void batchnorm_bwd_launch(const BnBwdParams& q, hipStream_t s) {
   float* coef = (float*)q.ws;
   float2* part = (float2*)(coef + ((3 * q.C + 3) & ~3));
   const bool mk = q.relu && q.mask != nullptr;
+  const dim3 fin((q.C + BN_FIN_CH - 1) / BN_FIN_CH);
+  if (!q.gsum) {
 #define BN_BREDUCE(RL, MK)                                                                                   \
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<RL, MK>), G.grid, dim3(BN_THREADS), 0, s, q.dY, q.Y, q.mask, q.X, \
                      q.rows, q.C, G.CH, G.rpb, q.smean, part)
-  if (mk) BN_BREDUCE(true, true);
-  else if (q.relu) BN_BREDUCE(true, false);
-  else BN_BREDUCE(false, false);
+    if (mk) BN_BREDUCE(true, true);
+    else if (q.relu) BN_BREDUCE(true, false);
+    else BN_BREDUCE(false, false);
 #undef BN_BREDUCE
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((q.C + BN_FIN_CH - 1) / BN_FIN_CH), dim3(BN_THREADS), 0, s, part, nparts, q.rows, q.C,
-                     q.w, q.smean, q.sinvstd, q.dw, q.db, coef);
+  }
+  if (q.lsum) {  // cross-rank statistics, first half: local sums (+ this rank's dweight / dbias)
+    hipLaunchKernelGGL(bn_local_sums_kernel, fin, dim3(BN_THREADS), 0, s, part, nparts, q.rows, q.C, q.lsum,
+                       q.sinvstd, q.dw, q.db);
+    return;
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, fin, dim3(BN_THREADS), 0, s, part, nparts, q.gsum, q.rows, q.C,
+                     q.w, q.smean, q.sinvstd, q.gsum ? nullptr : q.dw, q.gsum ? nullptr : q.db, coef);
   const bool ds = q.dS != nullptr;
 #define BN_BAPPLY(RL, MK, DS)                                                                                     \
   hipLaunchKernelGGL((bn_bwd_apply_kernel<RL, MK, DS>), G.grid, dim3(BN_THREADS), 0, s, q.dY, q.Y, q.mask, q.X,  \

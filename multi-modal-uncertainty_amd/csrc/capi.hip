@@ -630,6 +630,65 @@ int mmu_batchnorm_bwd(const void* dY, const void* Y, const void* relu_mask, cons
   return check_launch("mmu_batchnorm_bwd");
 }
 
+int mmu_batchnorm_stats(const void* X, int64_t rows, int64_t C, double* sums, void* ws, int64_t ws_bytes,
+                        mmu_stream_t stream) {
+  if (!X || !sums) return fail("mmu_batchnorm_stats: null pointer");
+  if (bn_common(rows, C, ws, ws_bytes, "mmu_batchnorm_stats")) return 1;
+  BnFwdParams q{};
+  q.X = (const bf16*)X; q.rows = rows; q.C = (int)C; q.training = 1; q.ws = ws; q.lsum = sums;
+  batchnorm_fwd_launch(q, (hipStream_t)stream);
+  return check_launch("mmu_batchnorm_stats");
+}
+
+int mmu_batchnorm_fwd_sums(const void* X, const void* skip, void* Y, int64_t rows, int64_t C, const double* sums,
+                           const float* weight, const float* bias, float* running_mean, float* running_var,
+                           int64_t* num_batches_tracked, float momentum, float eps, int relu, float* save_mean,
+                           float* save_invstd, void* relu_mask, void* ws, int64_t ws_bytes, mmu_stream_t stream) {
+  if (!X || !Y || !sums) return fail("mmu_batchnorm_fwd_sums: null pointer");
+  if (relu_mask && !relu) return fail("mmu_batchnorm_fwd_sums: relu_mask needs relu");
+  if (bn_common(rows, C, ws, ws_bytes, "mmu_batchnorm_fwd_sums")) return 1;
+  if ((running_mean == nullptr) != (running_var == nullptr))
+    return fail("mmu_batchnorm_fwd_sums: running_mean / running_var must both be given or NULL");
+  if ((save_mean == nullptr) != (save_invstd == nullptr))
+    return fail("mmu_batchnorm_fwd_sums: save_mean / save_invstd must both be given or NULL");
+  BnFwdParams q{};
+  q.X = (const bf16*)X; q.skip = (const bf16*)skip; q.Y = (bf16*)Y; q.rows = rows; q.C = (int)C;
+  q.w = weight; q.b = bias; q.rmean = running_mean; q.rvar = running_var; q.nbt = num_batches_tracked;
+  q.training = 1; q.relu = relu; q.momentum = momentum; q.eps = eps;
+  q.smean = save_mean; q.sinvstd = save_invstd; q.ws = ws; q.mask = (uint8_t*)relu_mask; q.gsum = sums;
+  batchnorm_fwd_launch(q, (hipStream_t)stream);
+  return check_launch("mmu_batchnorm_fwd_sums");
+}
+
+int mmu_batchnorm_bwd_reduce(const void* dY, const void* Y, const void* relu_mask, const void* X, int64_t rows,
+                             int64_t C, const float* save_mean, const float* save_invstd, int relu, double* sums,
+                             float* dweight, float* dbias, void* ws, int64_t ws_bytes, mmu_stream_t stream) {
+  if (!dY || !X || !sums || !save_mean || !save_invstd) return fail("mmu_batchnorm_bwd_reduce: null pointer");
+  if (relu && !Y && !relu_mask) return fail("mmu_batchnorm_bwd_reduce: relu needs the forward output Y or its relu_mask");
+  if (bn_common(rows, C, ws, ws_bytes, "mmu_batchnorm_bwd_reduce")) return 1;
+  BnBwdParams q{};
+  q.dY = (const bf16*)dY; q.Y = (const bf16*)Y; q.X = (const bf16*)X; q.rows = rows; q.C = (int)C;
+  q.smean = save_mean; q.sinvstd = save_invstd; q.relu = relu; q.dw = dweight; q.db = dbias; q.ws = ws;
+  q.mask = (const uint8_t*)relu_mask; q.lsum = sums;
+  batchnorm_bwd_launch(q, (hipStream_t)stream);
+  return check_launch("mmu_batchnorm_bwd_reduce");
+}
+
+int mmu_batchnorm_bwd_sums(const void* dY, const void* Y, const void* relu_mask, const void* X, int64_t rows,
+                           int64_t C, const double* sums, const float* weight, const float* save_mean,
+                           const float* save_invstd, int relu, void* dX, void* dSkip, void* ws, int64_t ws_bytes,
+                           mmu_stream_t stream) {
+  if (!dY || !X || !dX || !sums || !save_mean || !save_invstd) return fail("mmu_batchnorm_bwd_sums: null pointer");
+  if (relu && !Y && !relu_mask) return fail("mmu_batchnorm_bwd_sums: relu needs the forward output Y or its relu_mask");
+  if (bn_common(rows, C, ws, ws_bytes, "mmu_batchnorm_bwd_sums")) return 1;
+  BnBwdParams q{};
+  q.dY = (const bf16*)dY; q.Y = (const bf16*)Y; q.X = (const bf16*)X; q.rows = rows; q.C = (int)C; q.w = weight;
+  q.smean = save_mean; q.sinvstd = save_invstd; q.relu = relu; q.dX = (bf16*)dX; q.dS = (bf16*)dSkip; q.ws = ws;
+  q.mask = (const uint8_t*)relu_mask; q.gsum = sums;
+  batchnorm_bwd_launch(q, (hipStream_t)stream);
+  return check_launch("mmu_batchnorm_bwd_sums");
+}
+
 int mmu_bertadam_step(float* params, const float* grads, float* m, float* v, void* bf16_copy, const int64_t* table,
                       int32_t* steps, int64_t n_tensors, int64_t n_chunks, float lr_decay, float lr_nodecay, float wd,
                       float warmup, float t_total, float b1, float b2, float eps, float max_grad_norm, float* ws,

@@ -171,6 +171,8 @@ struct BnFwdParams {
   int64_t* nbt;
   void* ws;
   uint8_t* mask;  // optional ReLU mask out ([rows][C/8] bytes, bit = Y > 0)
+  double* lsum;        // cross-rank statistics: write the local sums {s1[C], s2[C], rows} and stop
+  const double* gsum;  // cross-rank statistics: finalize + apply from the exchanged sums
 };
 void batchnorm_fwd_launch(const BnFwdParams& q, hipStream_t s);
 struct BnBwdParams {
@@ -183,6 +185,8 @@ struct BnBwdParams {
   float *dw, *db;
   void* ws;
   const uint8_t* mask;  // optional ReLU mask (read instead of Y)
+  double* lsum;        // as BnFwdParams: {sum g, sum g*(x-mean), rows} (+= dweight / dbias) and stop
+  const double* gsum;  // finalize + apply from the exchanged sums
 };
 void batchnorm_bwd_launch(const BnBwdParams& q, hipStream_t s);
 int64_t batchnorm_ws_bytes(int64_t C);

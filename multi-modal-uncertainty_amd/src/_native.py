@@ -77,6 +77,13 @@ SIGNATURES = {
                                   c_f32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "mmu_batchnorm_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp,
                                   c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "mmu_batchnorm_stats": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    "mmu_batchnorm_fwd_sums": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32,
+                                       c_f32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "mmu_batchnorm_bwd_reduce": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp,
+                                         c_vp, c_i64, c_vp]),
+    "mmu_batchnorm_bwd_sums": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp,
+                                       c_vp, c_vp, c_i64, c_vp]),
     "mmu_bertadam_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32,
                                   c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_i64, c_vp]),
     "mmu_uncertainty": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),

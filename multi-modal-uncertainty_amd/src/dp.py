@@ -42,6 +42,7 @@ class GradBucketer:
         self.launched = set()
         self.done_segs = set()
         self.enabled = True
+        self._trunk_side = False
         self._hooks = [m.register_forward_pre_hook(self._block_pre_hook(k)) for k, m in self._blocks.items()]
 
     def _plan(self):
@@ -128,6 +129,9 @@ class GradBucketer:
             x = args[0] if args else None
             if (self.enabled and self.world > 1 and torch.is_grad_enabled() and isinstance(x, torch.Tensor)
                     and x.requires_grad):
+                # the block's filter gradients go to the side stream at this batch (resnet._wgrad_run)
+                from .resnet import _side_wgrad
+                self._trunk_side = _side_wgrad(x)
                 x.register_hook(lambda g: self._on_segment(key))
         return pre
 
@@ -147,6 +151,15 @@ class GradBucketer:
         bk = self.buckets[b]
         view = self.store.grad[bk["start"]:bk["end"]]
         side = K.side_stream_if_any(view.device) if view.is_cuda else None
+        if side is not None and torch.cuda.current_stream(view.device) != side:
+            # from the main stream, a bucket goes behind the side stream's work only when some
+            # of its gradients are written there: the ResNet blocks' filter gradients at batches
+            # that put them on the side stream (the encoder layers' buckets are issued from the
+            # deferred work itself, already on the side stream); the embedding / projection
+            # buckets stay on the main stream so they do not queue behind deferred work
+            segs = bk.get("segs", ())
+            if not (self._trunk_side and any(k not in ("emb", "proj") for k in segs)):
+                side = None
 
         def reduce():
             buf = view
@@ -190,6 +203,28 @@ class GradBucketer:
         self.store.grad.mul_(1.0 / self.world)
         self.pending, self.launched, self.done_layers, self.done_segs = [], set(), set(), set()
         self._lowp = {}
+
+
+def convert_sync_batchnorm(model, group=None):
+    """Normalise the image trunk over the whole data-parallel batch, as the single-device
+    reference does (src/mmbt.py:19-21; SURVEY §8e "DP + BatchNorm"): every BatchNorm2d of
+    ``model`` exchanges its per-channel sums with the other ranks in training
+    (resnet._SyncBatchNormAct, one all-reduce of 2C+1 f64 per BN per pass: 2 x 155 small
+    collectives per step).  The exchanges run on a communicator of their own (a new group over
+    the same ranks), so they do not queue behind the gradient buckets' all-reduces.  Without
+    it every rank normalises over its own per-rank batch (the default: no collective on the
+    forward's critical path).  Returns the number of BatchNorm2d modules converted."""
+    from .resnet import BatchNorm2d
+    if dist.get_world_size(group) == 1:
+        return 0
+    ranks = dist.get_process_group_ranks(group) if group is not None else list(range(dist.get_world_size()))
+    sync = dist.new_group(ranks=ranks)
+    n = 0
+    for m in model.modules():
+        if isinstance(m, BatchNorm2d):
+            m.sync_group = sync
+            n += 1
+    return n
 
 
 def average_buffers(model, group=None):

@@ -133,10 +133,22 @@ def _reduce(part, out):
 
 
 DEFER_WGRAD = True
+# the deferred closures keep their input tensors (dY2, Hh, dZ, A, dAo, O, dqkv, X: ~3 GB per layer
+# at batch 256, L = 513) alive until the flush; above this many retained bytes the work deferred
+# so far is flushed early (issued on the side stream at once), so larger batches / sequences do
+# not run out of memory.  None: a quarter of the device memory.
+DEFER_MAX_BYTES = None
 
 # per device: the weight-gradient work of the layers' backwards, deferred (DEFER_WGRAD) until
 # the encoder's data-gradient chain is enqueued, then issued on the side stream
 _deferred = {}
+_deferred_bytes = {}
+
+
+def _defer_budget(dev):
+    if DEFER_MAX_BYTES is not None:
+        return DEFER_MAX_BYTES
+    return torch.cuda.get_device_properties(dev).total_memory // 4
 
 
 def _flush_deferred(dev):
@@ -144,6 +156,7 @@ def _flush_deferred(dev):
     behind everything the main stream has enqueued so far -- the whole encoder dX chain -- so
     it runs beside what follows (embedding backward, the ResNet trunk's backward)."""
     items = _deferred.pop(dev, None)
+    _deferred_bytes.pop(dev, None)
     if not items:
         return
     main = torch.cuda.current_stream(dev)
@@ -172,6 +185,10 @@ def _defer(dev, fn, tensors):
 
         torch.autograd.Variable._execution_engine.queue_callback(at_end)
     items.append((fn, tensors))
+    held = _deferred_bytes.get(dev, 0) + sum(t.numel() * t.element_size() for t in tensors)
+    _deferred_bytes[dev] = held
+    if held > _defer_budget(dev):  # retained inputs over budget: issue what is deferred so far
+        _flush_deferred(dev)
 
 
 class _Side:
@@ -181,7 +198,8 @@ class _Side:
     (_flush_deferred), where it runs beside the embedding and ResNet-trunk backward -- a
     chain of short, latency-bound kernels.  Same-box A/B (profiles/r3_defer_wgrad_ab.txt):
     165.6 -> 163.3 ms per step at batch 256.  The inputs it reads stay alive until then
-    (peak HBM 75 GB at batch 256).  (Round 1 issued each piece on the side stream as soon as
+    (peak HBM 75 GB at batch 256), at most DEFER_MAX_BYTES of them: past that the work
+    deferred so far is flushed early.  (Round 1 issued each piece on the side stream as soon as
     its inputs existed: 210 -> 207 ms, an opt-in that this replaces.)"""
 
     def __init__(self, dev, on):

@@ -537,6 +537,78 @@ def batchnorm_bwd(dY, Y, X, weight, save_mean, save_invstd, relu, dX, dSkip=None
            ws.numel() * 4, _stream(X))
 
 
+def bn_sums_buffer(C, device):
+    """[2C+1] f64: the per-channel sums of one cross-rank BatchNorm pass + its row count"""
+    return torch.empty(2 * C + 1, dtype=torch.float64, device=device)
+
+
+def batchnorm_stats(X, sums):
+    """cross-rank BatchNorm, forward first half: sums = {sum x, sum x^2, rows} over X's rows"""
+    _dev_check(X, sums)
+    _want(X, torch.bfloat16, "batchnorm_stats X")
+    C = X.shape[1]
+    _bn_sums_check("batchnorm_stats", sums, C)
+    _bn_map_check("batchnorm_stats", X)
+    ws = _bn_workspace(X.device)
+    N.call("mmu_batchnorm_stats", _ptr(X), X.numel() // C, C, _ptr(sums), _ptr(ws), ws.numel() * 4, _stream(X))
+
+
+def batchnorm_fwd_sums(X, Y, sums, weight, bias, running_mean, running_var, momentum, eps, relu=False, skip=None,
+                       num_batches_tracked=None, save_mean=None, save_invstd=None, relu_mask=None):
+    """cross-rank BatchNorm, forward second half: batchnorm_fwd (training) with the statistics
+    of the exchanged sums"""
+    _dev_check(X, Y, sums)
+    _want(X, torch.bfloat16, "batchnorm X")
+    _bn_mask_check(relu_mask, X, "batchnorm_fwd_sums")
+    C = X.shape[1]
+    _bn_sums_check("batchnorm_fwd_sums", sums, C)
+    _bn_vec_check("batchnorm_fwd_sums", C, weight, bias, running_mean, running_var, save_mean, save_invstd)
+    _bn_map_check("batchnorm_fwd_sums", X, Y, skip)
+    if num_batches_tracked is not None and num_batches_tracked.dtype != torch.int64:
+        raise N.NativeError("batchnorm_fwd_sums: num_batches_tracked must be int64")
+    ws = _bn_workspace(X.device)
+    N.call("mmu_batchnorm_fwd_sums", _ptr(X), _ptr(skip), _ptr(Y), X.numel() // C, C, _ptr(sums), _ptr(weight),
+           _ptr(bias), _ptr(running_mean), _ptr(running_var), _ptr(num_batches_tracked), float(momentum), float(eps),
+           int(bool(relu)), _ptr(save_mean), _ptr(save_invstd), _ptr(relu_mask), _ptr(ws), ws.numel() * 4,
+           _stream(X))
+
+
+def batchnorm_bwd_reduce(dY, Y, X, save_mean, save_invstd, relu, sums, dweight=None, dbias=None, relu_mask=None):
+    """cross-rank BatchNorm, backward first half: sums = {sum g, sum g*(x-mean), rows};
+    dweight / dbias += this rank's"""
+    _dev_check(dY, X, sums)
+    _want(X, torch.bfloat16, "batchnorm_bwd X")
+    _bn_mask_check(relu_mask, X, "batchnorm_bwd_reduce")
+    C = X.shape[1]
+    _bn_sums_check("batchnorm_bwd_reduce", sums, C)
+    _bn_vec_check("batchnorm_bwd_reduce", C, save_mean, save_invstd, dweight, dbias)
+    _bn_map_check("batchnorm_bwd_reduce", X, dY, Y)
+    ws = _bn_workspace(X.device)
+    N.call("mmu_batchnorm_bwd_reduce", _ptr(dY), _ptr(Y), _ptr(relu_mask), _ptr(X), X.numel() // C, C,
+           _ptr(save_mean), _ptr(save_invstd), int(bool(relu)), _ptr(sums), _ptr(dweight), _ptr(dbias), _ptr(ws),
+           ws.numel() * 4, _stream(X))
+
+
+def batchnorm_bwd_sums(dY, Y, X, sums, weight, save_mean, save_invstd, relu, dX, dSkip=None, relu_mask=None):
+    """cross-rank BatchNorm, backward second half: dX (, dSkip) from the exchanged sums"""
+    _dev_check(dY, X, dX, sums)
+    _want(X, torch.bfloat16, "batchnorm_bwd X")
+    _bn_mask_check(relu_mask, X, "batchnorm_bwd_sums")
+    C = X.shape[1]
+    _bn_sums_check("batchnorm_bwd_sums", sums, C)
+    _bn_vec_check("batchnorm_bwd_sums", C, weight, save_mean, save_invstd)
+    _bn_map_check("batchnorm_bwd_sums", X, dY, Y, dX, dSkip)
+    ws = _bn_workspace(X.device)
+    N.call("mmu_batchnorm_bwd_sums", _ptr(dY), _ptr(Y), _ptr(relu_mask), _ptr(X), X.numel() // C, C, _ptr(sums),
+           _ptr(weight), _ptr(save_mean), _ptr(save_invstd), int(bool(relu)), _ptr(dX), _ptr(dSkip), _ptr(ws),
+           ws.numel() * 4, _stream(X))
+
+
+def _bn_sums_check(who, sums, C):
+    if sums.dtype != torch.float64 or sums.numel() != 2 * C + 1 or not sums.is_contiguous():
+        raise N.NativeError(f"{who}: sums must be a contiguous float64 [2C+1] = [{2 * C + 1}] tensor")
+
+
 def bertadam_step(params, grads, m, v, bf16_copy, table, steps, n_tensors, n_chunks, lr_decay, lr_nodecay, wd,
                   warmup, t_total, b1, b2, eps, max_grad_norm, ws):
     _dev_check(params, grads, m, v, table, steps, ws)

@@ -77,6 +77,99 @@ class _BatchNormAct(torch.autograd.Function):
         return dX, rw, rb, dS, None, None, None
 
 
+class _SyncBatchNormAct(torch.autograd.Function):
+    """Training-mode BatchNorm2d [+ residual] [+ ReLU] with statistics over the batch of every
+    rank of ``group`` (the reference's whole-batch normalisation, src/mmbt.py:19-21, kept under
+    data parallelism; torch.nn.SyncBatchNorm's exchange): each pass sums its per-channel
+    reductions locally, all-reduces {s1[C], s2[C], rows} (2C+1 f64), then normalises / forms
+    dX from the global sums.  The weight / bias gradients stay this rank's (the DP gradient
+    all-reduce sums them).  bf16 channels-last GPU maps run mmu_batchnorm_stats /
+    _fwd_sums / _bwd_reduce / _bwd_sums; anything else (fp32 parity runs, CPU) the same
+    arithmetic in torch ops."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, skip, bn, relu, sink, group, hip):
+        import torch.distributed as dist
+        ctx.bias_ref, ctx.sink, ctx.group, ctx.hip = bias, sink, group, hip
+        ctx.relu, ctx.has_skip = relu, skip is not None
+        C = x.shape[1]
+        if hip:
+            sums = K.bn_sums_buffer(C, x.device)
+            K.batchnorm_stats(x, sums)
+            dist.all_reduce(sums, group=group)
+            Y = torch.empty_like(x)
+            smean = torch.empty(C, dtype=torch.float32, device=x.device)
+            sinv = torch.empty_like(smean)
+            mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device) if relu else None
+            K.batchnorm_fwd_sums(x, Y, sums, weight, bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps,
+                                 relu=relu, skip=skip, num_batches_tracked=bn.num_batches_tracked, save_mean=smean,
+                                 save_invstd=sinv, relu_mask=mask)
+            ctx.save_for_backward(x, mask, weight, smean, sinv)
+            return Y
+        xd = x.double()
+        red = [0, 2, 3]
+        sums = torch.cat([xd.sum(red), (xd * xd).sum(red), xd.new_tensor([x.numel() // C])])
+        dist.all_reduce(sums, group=group)
+        n = sums[2 * C]
+        mean = sums[:C] / n
+        var = (sums[C:2 * C] / n - mean * mean).clamp_min(0)
+        invstd = (var + bn.eps).rsqrt()
+        if bn.running_mean is not None:
+            with torch.no_grad():
+                m = bn.momentum
+                bn.running_mean.mul_(1 - m).add_(m * mean.to(bn.running_mean.dtype))
+                bn.running_var.mul_(1 - m).add_(m * (var * n / (n - 1)).to(bn.running_var.dtype))
+                bn.num_batches_tracked.add_(1)
+        shape = (1, C, 1, 1)
+        scale = invstd * (weight.double() if weight is not None else 1.0)
+        shift = (bias.double() if bias is not None else 0.0) - mean * scale
+        y = (xd * scale.view(shape) + shift.view(shape)).to(x.dtype)
+        if skip is not None:
+            y = y + skip
+        if relu:
+            y = torch.relu(y)
+        ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dY):
+        import torch.distributed as dist
+        x, saved, weight, mean, invstd = ctx.saved_tensors
+        C = x.shape[1]
+        want_w, want_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        bias = ctx.bias_ref
+        if ctx.hip:
+            dY = dY.contiguous(memory_format=torch.channels_last)
+            dw = (weight.grad if weight.grad is not None else torch.zeros_like(weight)) if want_w else None
+            db = (bias.grad if bias.grad is not None else torch.zeros_like(bias)) if want_b else None
+            sums = K.bn_sums_buffer(C, x.device)
+            K.batchnorm_bwd_reduce(dY, None, x, mean, invstd, ctx.relu, sums, dw, db, relu_mask=saved)
+            dist.all_reduce(sums, group=ctx.group)
+            dX = torch.empty_like(x)
+            dS = torch.empty_like(x) if ctx.has_skip and ctx.needs_input_grad[3] else None
+            K.batchnorm_bwd_sums(dY, None, x, sums, weight, mean, invstd, ctx.relu, dX, dS, relu_mask=saved)
+            rw = dw if (want_w and weight.grad is None) else None
+            rb = db if (want_b and bias.grad is None) else None
+        else:
+            g = dY * (saved > 0) if ctx.relu else dY
+            gd = g.double()
+            red = [0, 2, 3]
+            shape = (1, C, 1, 1)
+            xmu = x.double() - mean.view(shape)
+            sums = torch.cat([gd.sum(red), (gd * xmu).sum(red), gd.new_tensor([x.numel() // C])])
+            rw = (sums[C:2 * C] * invstd).to(weight.dtype) if want_w else None
+            rb = sums[:C].to(bias.dtype) if want_b else None
+            dist.all_reduce(sums, group=ctx.group)
+            n = sums[2 * C]
+            a = invstd * (weight.double() if weight is not None else 1.0)
+            dX = (a.view(shape) * (gd - (sums[:C] / n).view(shape)
+                                    - xmu * (invstd * invstd * sums[C:2 * C] / n).view(shape))).to(x.dtype)
+            dS = g if ctx.has_skip and ctx.needs_input_grad[3] else None
+        if ctx.sink is not None and dS is not None:  # conv1's dX GEMM adds it (EPI_ADD_RES)
+            ctx.sink.g, dS = dS, None
+        return dX, rw, rb, dS, None, None, None, None, None
+
+
 class BatchNorm2d(nn.BatchNorm2d):
     """BatchNorm2d with the activation fused in (state_dict / semantics of torch's).
     ``forward(x, skip=None, relu=None)`` computes act(BN(x) [+ skip]); ``relu`` defaults
@@ -87,6 +180,7 @@ class BatchNorm2d(nn.BatchNorm2d):
 
     fused_relu = False
     MIOPEN_MIN_BATCH = 8
+    sync_group = None  # a process group: training statistics over all its ranks' batches (src/dp.py)
 
     def forward(self, x, skip=None, relu=None, skip_sink=None):
         relu = self.fused_relu if relu is None else relu
@@ -95,6 +189,12 @@ class BatchNorm2d(nn.BatchNorm2d):
         hip = (not _TORCH_ONLY[0] and x.is_cuda and x.dtype == torch.bfloat16 and (skip is None or skip.dtype == torch.bfloat16)
                and x.shape[1] % 8 == 0 and self.weight is not None and self.weight.dtype == torch.float32
                and (self.running_mean is None or self.running_mean.dtype == torch.float32))
+        if self.sync_group is not None and self.training and self.track_running_stats:
+            if hip:
+                x = x.contiguous(memory_format=torch.channels_last)
+                if skip is not None:
+                    skip = skip.contiguous(memory_format=torch.channels_last)
+            return _SyncBatchNormAct.apply(x, self.weight, self.bias, skip, self, relu, skip_sink, self.sync_group, hip)
         if hip:
             x = x.contiguous(memory_format=torch.channels_last)
             if skip is not None:

@@ -57,6 +57,9 @@ FLAGS = [
     ("--img_embed_pool_type", dict(type=str, default="avg", choices=["max", "avg"])),
     ("--img_hidden_sz", dict(type=int, default=2048)), ("--include_bn", dict(type=int, default=True)),
     ("--max_seq_len", dict(type=int, default=512)), ("--n_workers", dict(type=int, default=0)),
+    ("--sync_bn", dict(type=int, default=0, help="data parallel: the image trunk's BatchNorms normalise over the "
+                                                 "whole batch of all ranks (the single-device reference's "
+                                                 "statistics; src/dp.convert_sync_batchnorm)")),
     ("--gpu_normalize", dict(type=int, default=1, help="Food-101: workers ship uint8 crops, ToTensor + Normalize "
                                                       "run on the GPU one batch ahead (src/dataset.py)")),
     ("--num_image_embeds", dict(type=int, default=3)), ("--warmup", dict(type=float, default=0.1)),
@@ -195,10 +198,12 @@ def food101_data(args, rank=0, world=1):
                                sampler=sampler)
 
 
-def _dp_wrap(model, optimizer, accum):
+def _dp_wrap(model, optimizer, accum, sync_bn=False):
     """Hook the RCCL bucketer between backward and BertAdam; all-reduce only on update micro-batches."""
-    from src.dp import GradBucketer, broadcast_parameters, sync_buffers_on_eval
+    from src.dp import GradBucketer, broadcast_parameters, convert_sync_batchnorm, sync_buffers_on_eval
     broadcast_parameters(model)
+    if sync_bn:
+        convert_sync_batchnorm(model)
     sync_buffers_on_eval(model)  # BatchNorm running stats averaged over ranks before eval / checkpoints
     bucketer = GradBucketer(model)
     state = {"micro": 0}
@@ -278,7 +283,7 @@ def main(argv=None):
         raise RuntimeError("the MMBT / FLAVA paths run on MI355X HIP kernels: no GPU visible")
     if world > 1:
         if mmbt:
-            _dp_wrap(model, optimizer, args.gradient_accumulation_steps)
+            _dp_wrap(model, optimizer, args.gradient_accumulation_steps, bool(getattr(args, "sync_bn", 0)))
         else:
             _dp_wrap_flat(model, optimizer)
         # evaluation sharded over the ranks, sample-weighted sums combined in eval_loop

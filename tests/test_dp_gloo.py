@@ -229,3 +229,77 @@ def test_eval_sharded_over_ranks_equals_whole_split():
         # per-batch f32 means over differently composed batches: equal to f32 rounding
         assert abs(whole["val_loss"] - sharded["val_loss"]) < 1e-6 * max(1.0, abs(whole["val_loss"]))
         assert abs(whole["val_acc"] - sharded["val_acc"]) < 1e-6 * 100
+
+
+def _trunk_net():
+    """two torchvision Bottlenecks (identity skip + strided downsample) of src/resnet"""
+    from src.resnet import Bottleneck
+    torch.manual_seed(5)
+    net = torch.nn.Sequential(Bottleneck(16, 4, 1), Bottleneck(16, 8, 2))
+    for m in net.modules():  # non-trivial affine parameters / running statistics
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.2, 0.2)
+            m.running_mean.uniform_(-0.1, 0.1)
+    return net
+
+
+def _sync_bn_data(B):
+    g = torch.Generator().manual_seed(11)
+    return torch.randn(B, 16, 8, 8, generator=g) * 2 + 0.5, torch.randn(B, 32, 4, 4, generator=g)
+
+
+def _sync_bn_worker(rank, world, port, q, B):
+    """rank r holds samples [r*B/world, (r+1)*B/world) of the batch; the trunk's BatchNorms
+    exchange their sums (dp.convert_sync_batchnorm); loss = the per-rank mean, gradients
+    averaged over the ranks as the DP bucketer does."""
+    try:
+        import sys
+        here = os.path.dirname(os.path.abspath(__file__))
+        sys.path[:0] = [os.path.join(os.path.dirname(here), "multi-modal-uncertainty_amd"), os.path.dirname(here)]
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from src.dp import convert_sync_batchnorm
+        net = _trunk_net().train()
+        n_bn = convert_sync_batchnorm(net)
+        X, R = _sync_bn_data(B)
+        s = slice(rank * B // world, (rank + 1) * B // world)
+        x = X[s].clone().requires_grad_(True)
+        out = net(x)
+        (out * R[s]).sum().div(B // world).backward()
+        grads = torch.cat([p.grad.flatten() for p in net.parameters()])
+        dist.all_reduce(grads)
+        grads /= world
+        bufs = torch.cat([b.flatten().double() for b in net.buffers()])
+        q.put((rank, out.detach(), x.grad * (1.0 / world), grads, bufs, n_bn))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, "ERR", traceback.format_exc()))
+
+
+def test_sync_batchnorm_matches_whole_batch():
+    """Cross-rank BatchNorm (resnet._SyncBatchNormAct, torch-op arithmetic on the CPU) over 2
+    ranks x 4 samples reproduces the single-device 8-sample step of the reference's whole-batch
+    BatchNorm (torch.nn.BatchNorm2d): outputs, input gradients, the DP-averaged parameter
+    gradients and every rank's running statistics."""
+    B, world = 8, 2
+    res = _spawn(_sync_bn_worker, world, B)
+    net = _trunk_net().train()
+    X, R = _sync_bn_data(B)
+    x = X.clone().requires_grad_(True)
+    out = net(x)
+    (out * R).sum().div(B).backward()
+    grads = torch.cat([p.grad.flatten() for p in net.parameters()])
+    bufs = torch.cat([b.flatten().double() for b in net.buffers()])
+    for rank, o, gx, g, bf, n_bn in res:
+        s = slice(rank * B // world, (rank + 1) * B // world)
+        assert n_bn == 7
+        torch.testing.assert_close(o, out.detach()[s], rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(gx, x.grad[s], rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(g, grads, rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(bf, bufs, rtol=1e-5, atol=1e-6)
+    # per-rank statistics (no exchange) really differ: the test discriminates
+    local = _trunk_net().train()
+    o_local = local(X[:B // world])
+    assert (o_local - out.detach()[:B // world]).abs().max() > 1e-2

@@ -127,7 +127,7 @@ def test_bucketer_hooks_average_real_backward(bucket_bytes, side):
         assert n_tail >= 1, "no embedding / trunk bucket launched inside backward"
 
 
-def _parity_worker(rank, world, port, q, reduce_dtype="float32"):
+def _parity_worker(rank, world, port, q, reduce_dtype="float32", sync_bn=None):
     try:
         import sys
         here = os.path.dirname(os.path.abspath(__file__))
@@ -135,7 +135,7 @@ def _parity_worker(rank, world, port, q, reduce_dtype="float32"):
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.backends.cudnn.deterministic = True
-        from src.dp import GradBucketer, broadcast_parameters
+        from src.dp import GradBucketer, broadcast_parameters, convert_sync_batchnorm
         from src.mmbt import MultimodalBertClf
         from src.optim import BertAdam
         from src.testing import small_args, synthetic_batch
@@ -146,8 +146,11 @@ def _parity_worker(rank, world, port, q, reduce_dtype="float32"):
         def make():
             torch.manual_seed(0)
             m = MultimodalBertClf(small_args(bert_hidden_dropout=0.0, bert_attn_dropout=0.0, dropout=0.0,
-                                             img_precision="fp32")).to(dev)
-            m.eval()  # BN on running statistics (per-sample independent), dropout off
+                                             img_precision=sync_bn or "fp32")).to(dev)
+            if sync_bn:
+                m.train()  # BN on batch statistics: the ranks exchange them (convert_sync_batchnorm)
+            else:
+                m.eval()  # BN on running statistics (per-sample independent), dropout off
             named = list(m.named_parameters())
             nd = ["bias", "LayerNorm.bias", "LayerNorm.weight"]
             groups = [{"params": [p for n, p in named if not any(k in n for k in nd)], "weight_decay": 0.01},
@@ -170,6 +173,8 @@ def _parity_worker(rank, world, port, q, reduce_dtype="float32"):
         # two ranks, each on its half, bucketed all-reduce inside backward
         m2, o2 = make()
         broadcast_parameters(m2)
+        if sync_bn:
+            assert convert_sync_batchnorm(m2) > 0
         bk = GradBucketer(m2, bucket_bytes=1 << 20, reduce_dtype=getattr(torch, reduce_dtype))
         sl = slice(rank * B // world, (rank + 1) * B // world)
         for it in range(2):
@@ -182,7 +187,12 @@ def _parity_worker(rank, world, port, q, reduce_dtype="float32"):
         torch.cuda.synchronize()
         gerr = ((g2 - g1).norm() / g1.norm()).item()
         perr = ((p2 - p1).norm() / (p1 - p0).norm()).item()
-        q.put((rank, gerr, perr, (p1 - p0).abs().max().item()))
+        if sync_bn:  # the BatchNorm running statistics after the two steps
+            b1 = torch.cat([b.double().flatten() for b in m1.buffers() if b.is_floating_point()])
+            b2 = torch.cat([b.double().flatten() for b in m2.buffers() if b.is_floating_point()])
+            q.put((rank, gerr, perr, (p1 - p0).abs().max().item(), ((b2 - b1).norm() / b1.norm()).item()))
+        else:
+            q.put((rank, gerr, perr, (p1 - p0).abs().max().item()))
         dist.destroy_process_group()
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
@@ -204,3 +214,20 @@ def test_dp_two_ranks_equal_single_device_global_batch(reduce_dtype):
         assert upd > 0, "the optimizer step changed nothing"
         assert gerr <= bound, f"rank {rank}: averaged gradient vs global-batch gradient {gerr:.3e}"
         assert perr <= bound, f"rank {rank}: post-step parameters vs single device {perr:.3e}"
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_dp_sync_batchnorm_two_ranks_equal_single_device_train_mode(precision):
+    """The reference's whole-batch BatchNorm under DP (src/mmbt.py:19-21): in
+    TRAINING mode (batch statistics) 2 ranks x (B/2) with the trunk's BatchNorms exchanging
+    their sums (dp.convert_sync_batchnorm) == 1 device x B: averaged gradients, post-step
+    parameters and BN running statistics.  precision "bf16" is the bench trunk (HIP convs +
+    mmu_batchnorm_stats / _fwd_sums / _bwd_reduce / _bwd_sums), "fp32" the torch-op exchange.
+    Bars: fp32 1e-5 (summation order); bf16 1e-2 (bf16 maps: a per-sample conv on 4 vs 8 images
+    and the weight-gradient batch sums round differently).  Measured errors printed."""
+    bound = 1e-5 if precision == "fp32" else 1e-2
+    for rank, gerr, perr, upd, berr in _spawn(_parity_worker, 2, "float32", precision):
+        print(f"\n[dp sync-bn {precision} trunk] rank {rank}: grad rel err {gerr:.3e}, "
+              f"post-step param-change rel err {perr:.3e}, running-stats rel err {berr:.3e}")
+        assert upd > 0, "the optimizer step changed nothing"
+        assert gerr <= bound and perr <= bound and berr <= bound, (gerr, perr, berr)

@@ -458,6 +458,44 @@ def test_attention_dropout_multiword(dev, B, L):
         close(dqkv[:, 768 * part:768 * (part + 1)], g[:, 768 * part:768 * (part + 1)], atol_frac=3e-2)
 
 
+def test_attention_dropout_joint_statistics(dev):
+    """Higher-order statistics of the attention-probs dropout draws: the 16 keep decisions of a
+    half-wave's 16 consecutive keys come from ONE 32-bit hash (attention.hip pair_draw: 24-bit
+    multiplies of rotated windows), so beyond the per-key rate the JOINT behaviour of a group is
+    tested on the forward's own keep words (1.6 M groups of 16 at B = 8, L = 513, p = 0.1):
+    the kept count per group against Binomial(16, 0.9), and the 16 patterns of every aligned
+    4-bit sub-group against their product probabilities -- chi-square at alpha = 1e-6."""
+    from scipy import stats
+    k = K()
+    B, L, p = 8, 513, 0.1
+    qkv, km = make_attn_inputs(dev, B, L, pad=False, seed=21, scale=1.0)
+    O = torch.empty(B * L, 768, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(B * 12, L, device=dev)
+    dm = k.dropmask_empty(B, L, 12, dev)
+    k.attention_fwd(qkv, km, O, lse, B, L, drop_p=p, seed=97, dropmask=dm)
+    words = dm[:, :, : L // 64].reshape(-1)  # full 64-key tiles only (the last one holds 1 key)
+    groups = torch.stack([(words >> (16 * g)) & 0xFFFF for g in range(4)], 1).reshape(-1).cpu().numpy()
+    n = groups.size
+    kept = np.unpackbits(groups.astype(">u2").view(np.uint8)).reshape(n, 16).sum(1)
+    obs = np.bincount(kept, minlength=17).astype(np.float64)
+    exp = n * stats.binom.pmf(np.arange(17), 16, 1 - p)
+    lo = np.nonzero(exp >= 20)[0][0]  # pool the sparse low-count bins
+    o2 = np.concatenate([[obs[:lo].sum()], obs[lo:]])
+    e2 = np.concatenate([[exp[:lo].sum()], exp[lo:]])
+    chi_count = float(((o2 - e2) ** 2 / e2).sum())
+    crit_count = stats.chi2.ppf(1 - 1e-6, len(o2) - 1)
+    nib = np.concatenate([(groups >> (4 * s)) & 0xF for s in range(4)])
+    obs4 = np.bincount(nib, minlength=16).astype(np.float64)
+    ones = np.array([bin(v).count("1") for v in range(16)])
+    exp4 = nib.size * (1 - p) ** ones * p ** (4 - ones)
+    chi_nib = float(((obs4 - exp4) ** 2 / exp4).sum())
+    crit_nib = stats.chi2.ppf(1 - 1e-6, 15)
+    print(f"\n[dropout joint] {n} groups: kept-count chi2 {chi_count:.1f} (crit {crit_count:.1f}), "
+          f"4-bit pattern chi2 {chi_nib:.1f} (crit {crit_nib:.1f}), drop rate {1 - kept.mean() / 16:.5f}")
+    assert abs(1 - kept.mean() / 16 - p) < 2e-3
+    assert chi_count < crit_count and chi_nib < crit_nib
+
+
 @pytest.mark.parametrize("B,L", [(2, 200), (1, 513)])
 def test_attention_dropout_inference_matches_training_forward(dev, B, L):
     """MC-dropout inference (no dropmask: the forward kernel that stores no keep bits) drops
@@ -731,6 +769,78 @@ def test_batchnorm_train_fwd_bwd(dev, N, C, H, W, skip, relu):
     torch.testing.assert_close(db + 0.5, grads[2], rtol=2e-2, atol=2e-2 * grads[2].abs().max().item() + 1e-3)
     if skip:
         close(dS, grads[3], atol_frac=1e-2)
+
+
+@pytest.mark.parametrize("C,skip,relu", [(64, False, True), (256, True, True), (2048, False, False)])
+def test_batchnorm_cross_rank_sums_equal_whole_batch(dev, C, skip, relu):
+    """mmu_batchnorm_stats / _fwd_sums / _bwd_reduce / _bwd_sums over two halves of a batch,
+    their sums added (the all-reduce two ranks would do), reproduce mmu_batchnorm_fwd / _bwd on
+    the whole batch: outputs, saved statistics, running statistics, dX, dSkip and the two
+    halves' dweight / dbias summing to the whole batch's."""
+    k = K()
+    g = torch.Generator(device=dev).manual_seed(C)
+    cl = torch.channels_last
+    N, H, W = 6, 7, 5
+    x = (torch.randn(N, C, H, W, generator=g, device=dev) * 2 + 0.7).to(torch.bfloat16).contiguous(memory_format=cl)
+    s = torch.randn(N, C, H, W, generator=g, device=dev).to(torch.bfloat16).contiguous(memory_format=cl) if skip else None
+    dY = torch.randn(N, C, H, W, generator=g, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    w, b = torch.rand(C, generator=g, device=dev) + 0.5, torch.randn(C, generator=g, device=dev) * 0.1
+    rm0, rv0 = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
+    # whole batch
+    rm, rv = rm0.clone(), rv0.clone()
+    Y, sm, si = torch.empty_like(x), torch.empty(C, device=dev), torch.empty(C, device=dev)
+    mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=dev) if relu else None
+    k.batchnorm_fwd(x, Y, w, b, rm, rv, True, 0.1, 1e-5, relu=relu, skip=s, save_mean=sm, save_invstd=si,
+                    relu_mask=mask)
+    dX, dS = torch.empty_like(x), torch.empty_like(x) if skip else None
+    dw, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    k.batchnorm_bwd(dY, None, x, w, sm, si, relu, dX, dS, dw, db, relu_mask=mask)
+    # two "ranks"
+    halves = [slice(0, 4), slice(4, N)]  # ragged: 4 + 2 images
+    part = lambda t, h: None if t is None else t[h].contiguous(memory_format=cl)
+    sums = [k.bn_sums_buffer(C, dev) for _ in halves]
+    for h, sm_ in zip(halves, sums):
+        k.batchnorm_stats(part(x, h), sm_)
+    assert [int(t[2 * C]) for t in sums] == [4 * H * W, 2 * H * W]
+    tot = sums[0] + sums[1]
+    outs = []
+    for h in halves:
+        rm_h, rv_h = rm0.clone(), rv0.clone()
+        nbt = torch.zeros((), dtype=torch.int64, device=dev)
+        xh = part(x, h)
+        Yh, smh, sih = torch.empty_like(xh), torch.empty(C, device=dev), torch.empty(C, device=dev)
+        mh = torch.empty(xh.numel() // 8, dtype=torch.uint8, device=dev) if relu else None
+        k.batchnorm_fwd_sums(xh, Yh, tot, w, b, rm_h, rv_h, 0.1, 1e-5, relu=relu, skip=part(s, h),
+                             num_batches_tracked=nbt, save_mean=smh, save_invstd=sih, relu_mask=mh)
+        assert int(nbt) == 1
+        torch.testing.assert_close(rm_h, rm, rtol=1e-6, atol=1e-7)
+        torch.testing.assert_close(rv_h, rv, rtol=1e-6, atol=1e-7)
+        torch.testing.assert_close(smh, sm, rtol=1e-6, atol=1e-7)
+        torch.testing.assert_close(sih, si, rtol=1e-6, atol=1e-7)
+        outs.append((xh, Yh, smh, sih, mh))
+    Yc = torch.cat([o[1] for o in outs])
+    assert (Yc.float() - Y.float()).abs().max() <= 1e-2 * Y.float().abs().max()
+    assert (Yc != Y).float().mean() < 1e-3  # bit-identical but for a rare last-bit rounding
+    bsums, dws, dbs = [k.bn_sums_buffer(C, dev) for _ in halves], [], []
+    for h, bs, (xh, Yh, smh, sih, mh) in zip(halves, bsums, outs):
+        dwh, dbh = torch.full((C,), 0.25, device=dev), torch.full((C,), -0.5, device=dev)
+        k.batchnorm_bwd_reduce(part(dY, h), None, xh, smh, sih, relu, bs, dwh, dbh, relu_mask=mh)
+        dws.append(dwh - 0.25)
+        dbs.append(dbh + 0.5)
+    torch.testing.assert_close(dws[0] + dws[1], dw, rtol=1e-4, atol=1e-4 * dw.abs().max().item())
+    torch.testing.assert_close(dbs[0] + dbs[1], db, rtol=1e-4, atol=1e-4 * db.abs().max().item())
+    btot = bsums[0] + bsums[1]
+    dXs, dSs = [], []
+    for h, (xh, Yh, smh, sih, mh) in zip(halves, outs):
+        dXh, dSh = torch.empty_like(xh), torch.empty_like(xh) if skip else None
+        k.batchnorm_bwd_sums(part(dY, h), None, xh, btot, w, smh, sih, relu, dXh, dSh, relu_mask=mh)
+        dXs.append(dXh)
+        dSs.append(dSh)
+    dXc = torch.cat(dXs)
+    assert (dXc.float() - dX.float()).abs().max() <= 1e-2 * dX.float().abs().max()
+    assert (dXc != dX).float().mean() < 1e-2
+    if skip:
+        assert torch.equal(torch.cat(dSs), dS)
 
 
 def test_batchnorm_eval_and_module(dev):
