@@ -375,7 +375,8 @@ def _mmu_conv(geo, xshape, cout):
     """(forward, data gradient, filter gradient) of a conv on the gathered-operand MFMA
     products (mmu_conv_implicit / mmu_conv_wgrad) instead of MIOpen, from same-box timings
     of both engines (profiles/r3_conv_census_b256.txt, r3_conv_strided.txt):
-      3x3 stride 1: forward for Cout >= 256 (% 128), dX for Cin >= 256 (% 128), dW for
+      3x3 stride 1: forward for Cout >= 256 (% 128), dX for Cin >= 128 (% 128: layer2's
+        128-channel dX is 117 vs 142 us at batch 256, 36 vs 41 us at batch 32), dW for
         Cin % 256 == 0 (layer3 / layer4 conv2);
       strided 3x3 (layer3 / layer4 conv2 at >= 12544 output pixels: forward and dW) and the
         1x1 / stride-2 downsample (forward and dW at 12544..50176 output pixels: layer3 /
@@ -388,7 +389,7 @@ def _mmu_conv(geo, xshape, cout):
     M = n * ((h + 2 * pad - ks) // st + 1) * ((w + 2 * pad - ks) // st + 1)
     if ks == 3 and st == 1:
         fwd = cin % 64 == 0 and cout % 128 == 0 and cout >= 256 and M >= 256
-        dx = cout % 64 == 0 and cin % 128 == 0 and cin >= 256 and M >= 256
+        dx = cout % 64 == 0 and cin % 128 == 0 and M >= 256
         dw = cin % 256 == 0 and cout % 128 == 0 and M >= 1024
         return fwd, dx, dw
     if st == 1:  # 1x1 stride 1: _Conv1x1

@@ -106,29 +106,41 @@ class ViltHIP:
         x_w = xm[:, 0].sum(dim=2)[:, 0]
         pd = self.config.image_size // self.config.patch_size
         spatial = self.pos_img[:, 1:, :].transpose(1, 2).reshape(1, H, pd, pd)
-        pos = torch.cat([F.pad(F.interpolate(spatial, size=(int(h), int(w)), mode="bilinear", align_corners=True),
-                               (0, gw - int(w), 0, gh - int(h))) for h, w in zip(x_h, x_w)], 0)
-        pos = pos.flatten(2).transpose(1, 2)  # [B, gh*gw, H]
-        xm = xm.flatten(1)                    # [B, gh*gw]
+        # one interpolated position grid per distinct valid extent (a batch of full-size
+        # images shares one), gathered per sample
+        ext = [(int(h), int(w)) for h, w in zip(x_h, x_w)]
+        uniq = sorted(set(ext))
+        grids = torch.cat([F.pad(F.interpolate(spatial, size=e, mode="bilinear", align_corners=True),
+                                 (0, gw - e[1], 0, gh - e[0])) for e in uniq], 0)
+        grids = grids.flatten(2).transpose(1, 2)  # [U, gh*gw, H]
+        xm = xm.flatten(1)                        # [B, gh*gw]
         max_len = self.config.max_image_length
         eff = x_h * x_w
         max_len = int(eff.max()) if (max_len is None or not isinstance(max_len, int) or max_len < 0) \
             else min(int(eff.max()), max_len)
-        valid = xm.nonzero(as_tuple=False)
-        nonvalid = (1 - xm).nonzero(as_tuple=False)
+        # the reference's selection, sample by sample in the same order with the same
+        # torch.multinomial draws (valid patches in row-major order: nonzero()'s order)
+        P = gh * gw
+        n_valid = xm.sum(1)
+        v_all = torch.split(xm.nonzero(as_tuple=False)[:, 1], n_valid.tolist())
+        nv_all = torch.split((1 - xm).nonzero(as_tuple=False)[:, 1], (P - n_valid).tolist())
         sel = []
-        for b in valid[:, 0].unique():
-            v, nv = valid[valid[:, 0] == b], nonvalid[nonvalid[:, 0] == b]
+        for b in range(B):
+            v, nv = v_all[b], nv_all[b]
+            if v.numel() == 0:  # (the reference iterates the samples that have a valid patch)
+                continue
             pad = max_len - v.shape[0]
             if pad <= 0:
-                sel.append(v[torch.multinomial(torch.ones(v.shape[0]).float(), max_len)])
+                pick = v[torch.multinomial(torch.ones(v.shape[0]).float(), max_len)]
             else:
-                sel.append(torch.cat([v, nv[torch.multinomial(torch.ones(nv.shape[0]).float(), pad, replacement=True)]]))
-        sel = torch.cat(sel, 0)
-        bi, pi = sel[:, 0].to(x.device), sel[:, 1].to(x.device)
-        x = x[bi, pi].view(B, -1, H)
-        pos = pos[bi, pi].view(B, -1, H)
-        mask = xm[sel[:, 0], sel[:, 1]].view(B, -1).to(x.device)
+                pick = torch.cat([v, nv[torch.multinomial(torch.ones(nv.shape[0]).float(), pad, replacement=True)]])
+            sel.append(pick + b * P)
+        flat = torch.cat(sel, 0)
+        mask = xm.flatten()[flat].view(B, -1).to(x.device)
+        flat = flat.to(x.device)
+        x = x.reshape(B * P, H)[flat].view(B, -1, H)
+        gid = torch.tensor([uniq.index(e) for e in ext], device=x.device)
+        pos = grids.reshape(-1, H)[(gid * P).repeat_interleave(max_len) + flat % P].view(B, -1, H)
         x = torch.cat([self.cls.expand(B, -1, -1), x], 1)
         pos = torch.cat([self.pos_img[:, :1].expand(B, -1, -1), pos], 1)
         mask = torch.cat([torch.ones(B, 1, dtype=mask.dtype, device=x.device), mask], 1)

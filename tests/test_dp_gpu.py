@@ -127,7 +127,7 @@ def test_bucketer_hooks_average_real_backward(bucket_bytes, side):
         assert n_tail >= 1, "no embedding / trunk bucket launched inside backward"
 
 
-def _parity_worker(rank, world, port, q, reduce_dtype="float32", sync_bn=None):
+def _parity_worker(rank, world, port, q, reduce_dtype="float32"):
     try:
         import sys
         here = os.path.dirname(os.path.abspath(__file__))
@@ -135,7 +135,7 @@ def _parity_worker(rank, world, port, q, reduce_dtype="float32", sync_bn=None):
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.backends.cudnn.deterministic = True
-        from src.dp import GradBucketer, broadcast_parameters, convert_sync_batchnorm
+        from src.dp import GradBucketer, broadcast_parameters
         from src.mmbt import MultimodalBertClf
         from src.optim import BertAdam
         from src.testing import small_args, synthetic_batch
@@ -146,11 +146,8 @@ def _parity_worker(rank, world, port, q, reduce_dtype="float32", sync_bn=None):
         def make():
             torch.manual_seed(0)
             m = MultimodalBertClf(small_args(bert_hidden_dropout=0.0, bert_attn_dropout=0.0, dropout=0.0,
-                                             img_precision=sync_bn or "fp32")).to(dev)
-            if sync_bn:
-                m.train()  # BN on batch statistics: the ranks exchange them (convert_sync_batchnorm)
-            else:
-                m.eval()  # BN on running statistics (per-sample independent), dropout off
+                                             img_precision="fp32")).to(dev)
+            m.eval()  # BN on running statistics (per-sample independent), dropout off
             named = list(m.named_parameters())
             nd = ["bias", "LayerNorm.bias", "LayerNorm.weight"]
             groups = [{"params": [p for n, p in named if not any(k in n for k in nd)], "weight_decay": 0.01},
@@ -173,8 +170,6 @@ def _parity_worker(rank, world, port, q, reduce_dtype="float32", sync_bn=None):
         # two ranks, each on its half, bucketed all-reduce inside backward
         m2, o2 = make()
         broadcast_parameters(m2)
-        if sync_bn:
-            assert convert_sync_batchnorm(m2) > 0
         bk = GradBucketer(m2, bucket_bytes=1 << 20, reduce_dtype=getattr(torch, reduce_dtype))
         sl = slice(rank * B // world, (rank + 1) * B // world)
         for it in range(2):
@@ -187,12 +182,7 @@ def _parity_worker(rank, world, port, q, reduce_dtype="float32", sync_bn=None):
         torch.cuda.synchronize()
         gerr = ((g2 - g1).norm() / g1.norm()).item()
         perr = ((p2 - p1).norm() / (p1 - p0).norm()).item()
-        if sync_bn:  # the BatchNorm running statistics after the two steps
-            b1 = torch.cat([b.double().flatten() for b in m1.buffers() if b.is_floating_point()])
-            b2 = torch.cat([b.double().flatten() for b in m2.buffers() if b.is_floating_point()])
-            q.put((rank, gerr, perr, (p1 - p0).abs().max().item(), ((b2 - b1).norm() / b1.norm()).item()))
-        else:
-            q.put((rank, gerr, perr, (p1 - p0).abs().max().item()))
+        q.put((rank, gerr, perr, (p1 - p0).abs().max().item()))
         dist.destroy_process_group()
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
@@ -216,18 +206,105 @@ def test_dp_two_ranks_equal_single_device_global_batch(reduce_dtype):
         assert perr <= bound, f"rank {rank}: post-step parameters vs single device {perr:.3e}"
 
 
+
+def _sync_bn_worker(rank, world, port, q, precision):
+    """TRAINING-mode step (batch statistics) three ways: one device on the global batch; two
+    ranks on its halves with the trunk's BatchNorms exchanging their sums; two ranks without
+    the exchange (per-rank statistics).  Gradients are compared over the flat store without
+    the BERT key biases: their gradient is analytically zero (a per-query constant added to
+    every score of a softmax row), so what they hold is rounding residue, and BertAdam's
+    normalised step turns it into O(lr) parameter changes of arbitrary sign."""
+    try:
+        import sys
+        here = os.path.dirname(os.path.abspath(__file__))
+        sys.path[:0] = [os.path.join(os.path.dirname(here), "multi-modal-uncertainty_amd"), os.path.dirname(here)]
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.backends.cudnn.deterministic = True
+        from src.dp import GradBucketer, broadcast_parameters, convert_sync_batchnorm
+        from src.mmbt import MultimodalBertClf
+        from src.optim import BertAdam
+        from src.testing import small_args, synthetic_batch
+        from oracle.weights import SMALL
+        dev, B = "cuda:0", 8
+
+        def make():
+            torch.manual_seed(0)
+            m = MultimodalBertClf(small_args(bert_hidden_dropout=0.0, bert_attn_dropout=0.0, dropout=0.0,
+                                             img_precision=precision)).to(dev).train()
+            named = list(m.named_parameters())
+            nd = ["bias", "LayerNorm.bias", "LayerNorm.weight"]
+            groups = [{"params": [p for n, p in named if not any(k in n for k in nd)], "weight_decay": 0.01},
+                      {"params": [p for n, p in named if any(k in n for k in nd)], "weight_decay": 0.0}]
+            return m, BertAdam(groups, lr=1e-3, warmup=0.1, t_total=10.0)
+
+        x, y = synthetic_batch(B, 16, lens=[16, 9, 12, 16, 5, 16, 11, 14], vocab=SMALL.vocab, seed=31)
+        x, y = tuple(t.to(dev) for t in x), y.to(dev)
+        sl = slice(rank * B // world, (rank + 1) * B // world)
+
+        perm = torch.cat([torch.arange(B // 2, B), torch.arange(0, B // 2)]).to(dev)
+
+        def run(ranks, sync, permuted=False):
+            m, o = make()
+            bk = None
+            if ranks:
+                broadcast_parameters(m)
+                if sync:
+                    assert convert_sync_batchnorm(m) > 0
+                bk = GradBucketer(m, bucket_bytes=1 << 20)
+            xs, ys = (tuple(t[sl] for t in x), y[sl]) if ranks else (x, y)
+            if permuted:  # the same global batch in another order: the same step up to summation order
+                xs, ys = tuple(t[perm] for t in xs), ys[perm]
+            for it in range(2):  # BertAdam's first step has lr 0 (warmup_linear): the second moves
+                p0 = m.store.flat.clone()
+                o.zero_grad()
+                m.compute_loss(m(*xs), ys).backward()
+                if bk is not None:
+                    bk.finish()
+                g = m.store.grad.clone()
+                o.step()
+            bufs = torch.cat([b.double().flatten() for b in m.buffers() if b.is_floating_point()])
+            torch.cuda.synchronize()
+            return m, g, m.store.flat - p0, bufs
+
+        m1, g1, d1, b1 = run(False, False)
+        keep = torch.ones_like(g1, dtype=torch.bool)
+        for n in m1.store.names:
+            if n.endswith("attention.self.key.bias"):
+                o_ = m1.store.offsets[n]
+                keep[o_:o_ + m1.store.params[n].numel()] = False
+        rel = lambda a, b: ((a - b)[keep].norm() / b[keep].norm()).item()
+        _, g0, d0, _ = run(False, False, permuted=True)
+        _, g2, d2, b2 = run(True, True)
+        _, g3, _, _ = run(True, False)
+        q.put((rank, rel(g2, g1), rel(d2, d1), ((b2 - b1).norm() / b1.norm()).item(), rel(g3, g1), rel(g0, g1),
+               rel(d0, d1)))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, "ERR", traceback.format_exc()))
+
+
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_dp_sync_batchnorm_two_ranks_equal_single_device_train_mode(precision):
     """The reference's whole-batch BatchNorm under DP (src/mmbt.py:19-21): in
-    TRAINING mode (batch statistics) 2 ranks x (B/2) with the trunk's BatchNorms exchanging
-    their sums (dp.convert_sync_batchnorm) == 1 device x B: averaged gradients, post-step
-    parameters and BN running statistics.  precision "bf16" is the bench trunk (HIP convs +
-    mmu_batchnorm_stats / _fwd_sums / _bwd_reduce / _bwd_sums), "fp32" the torch-op exchange.
-    Bars: fp32 1e-5 (summation order); bf16 1e-2 (bf16 maps: a per-sample conv on 4 vs 8 images
-    and the weight-gradient batch sums round differently).  Measured errors printed."""
-    bound = 1e-5 if precision == "fp32" else 1e-2
-    for rank, gerr, perr, upd, berr in _spawn(_parity_worker, 2, "float32", precision):
-        print(f"\n[dp sync-bn {precision} trunk] rank {rank}: grad rel err {gerr:.3e}, "
-              f"post-step param-change rel err {perr:.3e}, running-stats rel err {berr:.3e}")
-        assert upd > 0, "the optimizer step changed nothing"
-        assert gerr <= bound and perr <= bound and berr <= bound, (gerr, perr, berr)
+    TRAINING mode 2 ranks x (B/2) with the trunk's BatchNorms exchanging their sums
+    (dp.convert_sync_batchnorm) == 1 device x B.  "fp32" = the fp32 torch trunk with the
+    torch-op exchange, "bf16" = the bench trunk on mmu_batchnorm_stats / _fwd_sums /
+    _bwd_reduce / _bwd_sums; the BERT encoder is bf16 in both.
+    Bar: the single device's own summation-order noise -- the same global batch in another
+    sample order, a step identical in exact arithmetic, whose bf16 roundings land differently
+    (a 1e-7 change in the trunk's statistics flips bf16 roundings downstream, and BertAdam's
+    normalised step magnifies near-zero gradients).  The averaged gradient and the parameter
+    change after the second BertAdam step must be within 2x that noise and within the north
+    star's 1e-2 (gradient); the running statistics within 1e-5 (fp32 trunk) / 1e-3 (statistics
+    of bf16 maps); and per-rank statistics (no exchange) must be off by >= 3x more than the
+    synchronised run, so the test sees the statistics.  Measured errors printed."""
+    for rank, gerr, perr, berr, gloc, gnoise, pnoise in _spawn(_sync_bn_worker, 2, precision):
+        print(f"\n[dp sync-bn {precision} trunk] rank {rank}: grad rel err {gerr:.3e} (reordered batch {gnoise:.3e}), "
+              f"post-step param-change rel err {perr:.3e} (reordered batch {pnoise:.3e}), running-stats rel err "
+              f"{berr:.3e}; per-rank statistics: grad rel err {gloc:.3e}")
+        assert gerr <= 1e-2 and gerr <= 2 * gnoise + 1e-6, (gerr, gnoise)
+        assert perr <= 2 * pnoise + 1e-6, (perr, pnoise)
+        assert berr <= (1e-5 if precision == "fp32" else 1e-3), berr  # bf16 maps: their roundings
+        assert gloc >= 3 * max(gerr, gnoise), (gloc, gerr, gnoise)
