@@ -34,6 +34,47 @@ def _f32(t, dev):
     return t.detach().to(dev, torch.float32).contiguous()
 
 
+def patch_mask(pixel_mask, gh, gw):
+    """[B, H, W] pixel mask -> [B, gh, gw] long patch mask (nearest), on the host
+    (ViltEmbeddings.visual_embed's x_mask)"""
+    return F.interpolate(pixel_mask[:, None].float().cpu(), size=(gh, gw)).long()[:, 0]
+
+
+def image_length(xm, max_image_length):
+    """number of image tokens per sample: the largest valid extent, capped by max_image_length
+    when that is a non-negative int (visual_embed's max_image_length rule)"""
+    eff = int((xm.sum(1)[:, 0] * xm.sum(2)[:, 0]).max())
+    if max_image_length is None or not isinstance(max_image_length, int) or max_image_length < 0:
+        return eff
+    return min(eff, max_image_length)
+
+
+def select_patches(xm, max_len):
+    """ViltEmbeddings.visual_embed's patch selection on the host, sample by sample in the
+    reference's order with the same torch.multinomial draws from the global CPU generator: a
+    sample with at least max_len valid patches keeps max_len of them in random order, one with
+    fewer keeps all (in row-major order) and pads with valid-mask-0 patches drawn with
+    replacement.  xm: [B, P] long patch mask.  Returns the flat indices b * P + p of the chosen
+    patches ([B * max_len]) and their mask values [B, max_len]."""
+    B, P = xm.shape
+    n_valid = xm.sum(1)
+    v_all = torch.split(xm.nonzero(as_tuple=False)[:, 1], n_valid.tolist())
+    nv_all = torch.split((1 - xm).nonzero(as_tuple=False)[:, 1], (P - n_valid).tolist())
+    sel = []
+    for b in range(B):
+        v, nv = v_all[b], nv_all[b]
+        if v.numel() == 0:  # (the reference iterates the samples that have a valid patch)
+            continue
+        pad = max_len - v.shape[0]
+        if pad <= 0:
+            pick = v[torch.multinomial(torch.ones(v.shape[0]).float(), max_len)]
+        else:
+            pick = torch.cat([v, nv[torch.multinomial(torch.ones(nv.shape[0]).float(), pad, replacement=True)]])
+        sel.append(pick + b * P)
+    flat = torch.cat(sel, 0)
+    return flat, xm.flatten()[flat].view(B, -1)
+
+
 class ViltHIP:
     """``ViltForImagesAndTextClassification`` (or a bare ``ViltModel``) on the HIP kernels.
 
@@ -101,9 +142,9 @@ class ViltHIP:
                epi=K.epilogue(K.EPI_STORE, bias=self.b_patch))
         x = x.view(B, gh * gw, H)
         # pixel mask -> patch mask (nearest), valid extents per sample
-        xm = F.interpolate(pixel_mask[:, None].float().cpu(), size=(gh, gw)).long()
-        x_h = xm[:, 0].sum(dim=1)[:, 0]
-        x_w = xm[:, 0].sum(dim=2)[:, 0]
+        xm = patch_mask(pixel_mask, gh, gw)
+        x_h = xm.sum(1)[:, 0]
+        x_w = xm.sum(2)[:, 0]
         pd = self.config.image_size // self.config.patch_size
         spatial = self.pos_img[:, 1:, :].transpose(1, 2).reshape(1, H, pd, pd)
         # one interpolated position grid per distinct valid extent (a batch of full-size
@@ -113,30 +154,10 @@ class ViltHIP:
         grids = torch.cat([F.pad(F.interpolate(spatial, size=e, mode="bilinear", align_corners=True),
                                  (0, gw - e[1], 0, gh - e[0])) for e in uniq], 0)
         grids = grids.flatten(2).transpose(1, 2)  # [U, gh*gw, H]
-        xm = xm.flatten(1)                        # [B, gh*gw]
-        max_len = self.config.max_image_length
-        eff = x_h * x_w
-        max_len = int(eff.max()) if (max_len is None or not isinstance(max_len, int) or max_len < 0) \
-            else min(int(eff.max()), max_len)
-        # the reference's selection, sample by sample in the same order with the same
-        # torch.multinomial draws (valid patches in row-major order: nonzero()'s order)
+        max_len = image_length(xm, self.config.max_image_length)
         P = gh * gw
-        n_valid = xm.sum(1)
-        v_all = torch.split(xm.nonzero(as_tuple=False)[:, 1], n_valid.tolist())
-        nv_all = torch.split((1 - xm).nonzero(as_tuple=False)[:, 1], (P - n_valid).tolist())
-        sel = []
-        for b in range(B):
-            v, nv = v_all[b], nv_all[b]
-            if v.numel() == 0:  # (the reference iterates the samples that have a valid patch)
-                continue
-            pad = max_len - v.shape[0]
-            if pad <= 0:
-                pick = v[torch.multinomial(torch.ones(v.shape[0]).float(), max_len)]
-            else:
-                pick = torch.cat([v, nv[torch.multinomial(torch.ones(nv.shape[0]).float(), pad, replacement=True)]])
-            sel.append(pick + b * P)
-        flat = torch.cat(sel, 0)
-        mask = xm.flatten()[flat].view(B, -1).to(x.device)
+        flat, mask = select_patches(xm.flatten(1), max_len)
+        mask = mask.to(x.device)
         flat = flat.to(x.device)
         x = x.reshape(B * P, H)[flat].view(B, -1, H)
         gid = torch.tensor([uniq.index(e) for e in ext], device=x.device)
