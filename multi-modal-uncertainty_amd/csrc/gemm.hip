@@ -105,24 +105,26 @@ static __device__ __forceinline__ bf16x8 s_frag(const char* s, int row0, int ks,
 // (residual / aux loads, bf16 or f32 stores, split-K slabs) is then a 16-B-per-lane
 // access covering full 128-B lines.
 
-// one (m, n..n+7) octet: epilogue math + store; v holds acc (+ bias) on entry
+// one (m, n..n+7) octet: epilogue math + store; v holds acc (+ bias) on entry.  The row's
+// addresses arrive precomputed (epilogue_block: a per-lane base + a wave-uniform row offset, so
+// no per-row 64-bit VALU multiplies): cdst = &C[z][m][n], xdst = &aux[z][m][n], qd = the
+// dropout quad counter ((z M + m) N + n) / 4
 template <int EPI, bool OUT_F32>
-static __device__ __forceinline__ void epi_oct(const GemmParams& p, int64_t z, int64_t m, int64_t n, float (&v)[8],
-                                               const float (&in)[8], bf16* aux, float scale, uint32_t thr) {
+static __device__ __forceinline__ void epi_oct(const GemmParams& p, void* cdst, bf16* xdst, uint64_t qd,
+                                               float (&v)[8], const float (&in)[8], float scale, uint32_t thr) {
   if (EPI == MMU_EPI_BIAS_GELU) {  // C = gelu(z); aux (optional) = gelu'(z) for the backward
     float d[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) gelu_pair(v[r], v[r], d[r]);
-    if (aux) {
+    if (xdst) {
       bf16x8 o;
 #pragma unroll
       for (int r = 0; r < 8; ++r) o[r] = f2bf(d[r]);
-      *(bf16x8*)(aux + m * p.ldx + n) = o;
+      *(bf16x8*)xdst = o;
     }
   } else if (EPI == MMU_EPI_BIAS_DROP_RES) {
     if (thr) {  // counter over the whole batched output: batch item z, row m, column n (quads)
-      const uint64_t q0 = (uint64_t)((z * p.M + m) * p.N + n) >> 2;
-      const uint32_t keep = mmu_keep4(p.seed, q0, thr) | (mmu_keep4(p.seed, q0 + 1, thr) << 4);
+      const uint32_t keep = mmu_keep4(p.seed, qd, thr) | (mmu_keep4(p.seed, qd + 1, thr) << 4);
 #pragma unroll
       for (int r = 0; r < 8; ++r) v[r] = ((keep >> r) & 1) ? v[r] * scale : 0.f;
     }
@@ -130,10 +132,7 @@ static __device__ __forceinline__ void epi_oct(const GemmParams& p, int64_t z, i
     for (int r = 0; r < 8; ++r) v[r] += in[r];  // residual (f32 when C is f32: the hidden stream)
   } else if (EPI == MMU_EPI_BIAS_DROP_QGELU) {  // FLAVA mlp: u = dropout(z); C = u*sigmoid(1.702u)
     uint32_t keep = 0xFFu;                         // aux (optional) = dC/dz = keep*scale*qgelu'(u)
-    if (thr) {
-      const uint64_t q0 = (uint64_t)((z * p.M + m) * p.N + n) >> 2;
-      keep = mmu_keep4(p.seed, q0, thr) | (mmu_keep4(p.seed, q0 + 1, thr) << 4);
-    }
+    if (thr) keep = mmu_keep4(p.seed, qd, thr) | (mmu_keep4(p.seed, qd + 1, thr) << 4);
     float d[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
@@ -143,11 +142,11 @@ static __device__ __forceinline__ void epi_oct(const GemmParams& p, int64_t z, i
       v[r] = u * sg;
       d[r] = kz * fmaf(1.702f * u * sg, 1.0f - sg, sg);
     }
-    if (aux) {
+    if (xdst) {
       bf16x8 o;
 #pragma unroll
       for (int r = 0; r < 8; ++r) o[r] = f2bf(d[r]);
-      *(bf16x8*)(aux + m * p.ldx + n) = o;
+      *(bf16x8*)xdst = o;
     }
   } else if (EPI == MMU_EPI_DGELU) {  // in = aux = gelu'(z) saved by the forward epilogue
 #pragma unroll
@@ -157,7 +156,7 @@ static __device__ __forceinline__ void epi_oct(const GemmParams& p, int64_t z, i
     for (int r = 0; r < 8; ++r) v[r] += in[r];  // residual
   }
   if (OUT_F32) {
-    float4* C = (float4*)((float*)p.C + z * p.sC + m * p.ldc + n);
+    float4* C = (float4*)cdst;
     float4 lo = make_float4(v[0], v[1], v[2], v[3]), hi = make_float4(v[4], v[5], v[6], v[7]);
     if (p.accumulate) {
       const float4 c0 = C[0], c1 = C[1];
@@ -170,7 +169,7 @@ static __device__ __forceinline__ void epi_oct(const GemmParams& p, int64_t z, i
     bf16x8 o;
 #pragma unroll
     for (int r = 0; r < 8; ++r) o[r] = f2bf(v[r]);
-    *(bf16x8*)((bf16*)p.C + z * p.sC + m * p.ldc + n) = o;
+    *(bf16x8*)cdst = o;
   }
 }
 
@@ -183,7 +182,8 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
   if (nw >= p.N) return;  // (N % 128 == 0: a 64-column wave block is all in or all out)
   const int q = l & 7, rr = l >> 3;
   const int64_t n = nw + 8 * q;
-  const bool slab = p.splitk > 1;  // raw partial product -> this slice's f32 slab (splitk_reduce_kernel)
+  // raw partial product -> this slice's f32 slab (splitk_reduce_kernel); split-K is EPI_STORE only
+  const bool slab = EPI == MMU_EPI_STORE && p.splitk > 1;
   float* slab_base = slab ? p.ws + (z * p.splitk + slice) * p.M * p.N : nullptr;
   const float* bias = (!slab && p.bias && EPI != MMU_EPI_DGELU && EPI != MMU_EPI_ADD_RES)
                           ? p.bias + z * p.bias_bstride : nullptr;
@@ -207,6 +207,16 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
   const bf16* src = EPI == MMU_EPI_DGELU ? (const bf16*)aux : res;
   const float* src32 = RES32 && p.residual ? (const float*)p.residual + z * p.res_bstride : nullptr;
   const int64_t lds_ = EPI == MMU_EPI_DGELU ? p.ldx : p.ldr;
+  // the lane's row mw + rr: per-lane bases computed once; row mw + rr + d adds the wave-uniform
+  // d * ld (scalar multiplies) -- a per-row m * ld is a 64-bit VALU multiply per pointer
+  const int64_t m_l = mw + rr;
+  const int64_t in_l = m_l * lds_ + n;
+  const int64_t c_l = z * p.sC + m_l * p.ldc + n;
+  constexpr bool XST = EPI == MMU_EPI_BIAS_GELU || EPI == MMU_EPI_BIAS_DROP_QGELU;  // aux stores
+  constexpr bool DRP = EPI == MMU_EPI_BIAS_DROP_RES || EPI == MMU_EPI_BIAS_DROP_QGELU;
+  const int64_t x_l = XST ? m_l * p.ldx + n : 0;
+  const int64_t s_l = EPI == MMU_EPI_STORE ? m_l * p.N + n : 0;
+  const int64_t q_l = DRP ? (z * p.M + m_l) * p.N + n : 0;
   // residual = LN(residual rows): per-column gamma / beta here, per-row mean / rstd per pass
   const bool res_ln = RES32 && p.res_ln_w != nullptr && !slab;
   float lw[8], lb[8];
@@ -229,13 +239,15 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
     float rmu[RES32 ? 2 * PJ : 1], rrs[RES32 ? 2 * PJ : 1];
 #pragma unroll
     for (int it = 0; it < 2 * PJ; ++it) {
-      const int64_t m = mw + 16 * PJ * pass + rr + 8 * it;
+      const int d = 16 * PJ * pass + 8 * it;  // row offset from the lane's first row (uniform)
+      const int64_t m = m_l + d;
       if (RES32) {
         rmu[it] = 0.f;
         rrs[it] = 1.f;
         if (!slab && m < p.M) {
-          in32[it][0] = *(const float4*)(src32 + m * lds_ + n);
-          in32[it][1] = *(const float4*)(src32 + m * lds_ + n + 4);
+          const float* s32 = src32 + in_l + d * lds_;
+          in32[it][0] = *(const float4*)s32;
+          in32[it][1] = *(const float4*)(s32 + 4);
           if (res_ln) {
             rmu[it] = p.res_ln_mean[z * p.M + m];
             rrs[it] = p.res_ln_rstd[z * p.M + m];
@@ -244,7 +256,7 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
           in32[it][0] = in32[it][1] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
       } else if (LOADS && !slab && m < p.M) {
-        in[it] = *(const bf16x8*)(src + m * lds_ + n);
+        in[it] = *(const bf16x8*)(src + in_l + d * lds_);
       } else {
         in[it] = bf16x8{};
       }
@@ -261,14 +273,15 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
 #pragma unroll
     for (int it = 0; it < 2 * PJ; ++it) {
       const int r = rr + 8 * it;
-      const int64_t m = mw + 16 * PJ * pass + r;
+      const int d = 16 * PJ * pass + 8 * it;
+      const int64_t m = m_l + d;
       const float4 lo = *(const float4*)(ws + r * 256 + (((2 * q) ^ (r & 15)) << 4));
       const float4 hi = *(const float4*)(ws + r * 256 + (((2 * q + 1) ^ (r & 15)) << 4));
       if (m >= p.M) continue;
       if (slab) {
-        float4* d = (float4*)(slab_base + m * p.N + n);
-        d[0] = lo;
-        d[1] = hi;
+        float4* sd = (float4*)(slab_base + s_l + d * p.N);
+        sd[0] = lo;
+        sd[1] = hi;
         continue;
       }
       float v[8] = {lo.x + bv[0], lo.y + bv[1], lo.z + bv[2], lo.w + bv[3],
@@ -285,7 +298,9 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
 #pragma unroll
         for (int r = 0; r < 8; ++r) inf[r] = LOADS ? bf2f(in[RES32 ? 0 : it][r]) : 0.f;
       }
-      epi_oct<EPI, OUT_F32>(p, z, m, n, v, inf, aux, scale, thr);
+      void* cdst = OUT_F32 ? (void*)((float*)p.C + c_l + d * p.ldc) : (void*)((bf16*)p.C + c_l + d * p.ldc);
+      epi_oct<EPI, OUT_F32>(p, cdst, (XST && aux) ? aux + x_l + d * p.ldx : nullptr,
+                            DRP ? (uint64_t)(q_l + d * p.N) >> 2 : 0, v, inf, scale, thr);
       if (want_cs) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) cs[e] += v[e];

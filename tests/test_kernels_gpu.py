@@ -203,6 +203,80 @@ def test_gemm_partial_last_wave(dev, Kd):
     close(f[tl], ref[tl] + 0.25)
 
 
+def _keep_np(seed, idx, p):
+    """numpy restatement of mmu_keep4 / mmu_keep1 (csrc/mmu_common.h): the keep decision of
+    element idx of a dropout stream"""
+    import numpy as np
+    M32 = np.uint64(0xFFFFFFFF)
+
+    def lb(x):
+        x = x.astype(np.uint64) & M32
+        x ^= x >> np.uint64(16)
+        x = (x * np.uint64(0x7FEB352D)) & M32
+        x ^= x >> np.uint64(15)
+        x = (x * np.uint64(0x846CA68B)) & M32
+        x ^= x >> np.uint64(16)
+        return x
+    s32 = lb(np.uint64(seed & 0xFFFFFFFF) ^ lb(np.uint64((seed >> 32) ^ 0x68BC21EB)))
+    idx = np.asarray(idx, dtype=np.uint64)
+    quad = idx >> np.uint64(2)
+    x = (((quad << np.uint64(1)) & M32) ^ (((quad >> np.uint64(31)) * np.uint64(0x9E3779B8)) & M32)) ^ s32
+    h0, h1 = lb(x), lb(x ^ np.uint64(1))
+    e = idx & np.uint64(3)
+    draw = np.where(e == 0, h0 & np.uint64(0xFFFF), np.where(e == 1, h0 >> np.uint64(16),
+                    np.where(e == 2, h1 & np.uint64(0xFFFF), h1 >> np.uint64(16))))
+    return draw >= np.uint64(int(p * 65536.0 + 0.5))
+
+
+def test_gemm_epilogues_exact_first_and_last_tile_rows(dev):
+    """M = 256 * 257 rows x 3 column tiles = 771 tiles (3 whole rounds of 256 CUs + a partial
+    one), the epilogues' row addressing (per-lane row bases + wave-uniform row offsets) checked
+    on the first and the last tile row against torch: the f32 hidden-stream epilogue with the
+    residual LayerNorm recomputed and dropout -- keep decisions equal to a numpy restatement
+    of mmu_keep4 at the element's global index --, GELU + gelu' aux, and FLAVA's dropout +
+    QuickGELU with its derivative aux."""
+    import numpy as np
+    k = K()
+    M, N, Kd = 256 * 257, 768, 768
+    A, B = rnd(M, Kd, dev=dev, seed=131), rnd(N, Kd, dev=dev, seed=132, scale=0.1)
+    bias = torch.randn(N, device=dev) * 0.1
+    y = A.float() @ B.float().t() + bias
+    rows = [slice(0, 256), slice(M - 256, M)]
+    idx = {r.start: (np.arange(r.start, r.stop)[:, None] * N + np.arange(N)[None, :]) for r in rows}
+    # f32 hidden stream: C = LN(S) + dropout(A B^T + b)
+    S = torch.randn(M, N, device=dev) * 2.0 + 0.7
+    mean = S.mean(-1).contiguous()
+    rstd = torch.rsqrt(S.var(-1, unbiased=False) + 1e-12).contiguous()
+    w, b = torch.randn(N, device=dev), torch.randn(N, device=dev)
+    R32 = (S - mean[:, None]) * rstd[:, None] * w + b
+    p, seed = 0.1, 4242
+    out = torch.empty(M, N, dtype=torch.float32, device=dev)
+    k.gemm(A, Kd, True, B, Kd, True, out, N, M, N, Kd,
+           epi=k.epilogue(k.EPI_BIAS_DROP_RES, bias=bias, residual=S, drop_p=p, seed=seed, res_ln=(mean, rstd, w, b)))
+    for r in rows:
+        keep = torch.from_numpy(_keep_np(seed, idx[r.start], p)).to(dev)
+        want = R32[r] + torch.where(keep, y[r] / (1 - p), torch.zeros_like(y[r]))
+        torch.testing.assert_close(out[r], want, rtol=1e-5, atol=3e-5 * (R32.abs().max() + y.abs().max()).item())
+    # GELU + derivative aux
+    Z = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    H = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    k.gemm(A, Kd, True, B, Kd, True, H, N, M, N, Kd, epi=k.epilogue(k.EPI_BIAS_GELU, bias=bias, aux=Z))
+    for r in rows:
+        z = y[r].clone().requires_grad_(True)
+        g = torch.nn.functional.gelu(z)
+        close(H[r], g.detach())
+        close(Z[r], torch.autograd.grad(g.sum(), z)[0])
+    # FLAVA: u = dropout(z), C = u * sigmoid(1.702 u), aux = keep * scale * d/du
+    k.gemm(A, Kd, True, B, Kd, True, H, N, M, N, Kd,
+           epi=k.epilogue(k.EPI_BIAS_DROP_QGELU, bias=bias, aux=Z, drop_p=p, seed=seed + 1))
+    for r in rows:
+        keep = torch.from_numpy(_keep_np(seed + 1, idx[r.start], p)).to(dev).float()
+        u = y[r] * keep / (1 - p)
+        sg = torch.sigmoid(1.702 * u)
+        close(H[r], u * sg)
+        close(Z[r], keep / (1 - p) * (sg + 1.702 * u * sg * (1 - sg)))
+
+
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, False), (False, True)])
 def test_gemm_many_tiles_every_element(dev, ak, bk):
     """More tiles than CUs (40 x 9 = 360 tiles; batch 2 x 20 x 9 = 360 items), a ragged last

@@ -18,7 +18,9 @@ from src import resnet as R  # noqa: E402
 
 
 def torch_bn(x, w, b, skip, bn, relu, sink=None):
-    y = F.batch_norm(x, bn.running_mean, bn.running_var, w, b, True, bn.momentum, bn.eps)
+    # (MIOpen's NHWC batch-norm crashes in host code below batch 8: resnet.BatchNorm2d's guard)
+    with torch.backends.cudnn.flags(enabled=x.shape[0] >= R.BatchNorm2d.MIOPEN_MIN_BATCH):
+        y = F.batch_norm(x, bn.running_mean, bn.running_var, w, b, True, bn.momentum, bn.eps)
     if skip is not None:
         y = y + skip
     return torch.relu(y) if relu else y
