@@ -30,31 +30,10 @@ def timed(fn, iters):
     return best
 
 
-def set_env(var, v):
-    """v = a value of var, or 'A=1:B=2' (several variables; the others are cleared), or None"""
-    keys = {var} | {kv.split("=")[0] for kv in (v or "").split(":") if "=" in kv} | set(_SEEN)
-    for k in keys:
-        os.environ.pop(k, None)
-    if v is None:
-        return
-    if "=" in v:
-        for kv in v.split(":"):
-            k, x = kv.split("=")
-            os.environ[k] = x
-            _SEEN.add(k)
-    else:
-        os.environ[var] = v
-
-
-_SEEN = set()
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=256 * 513)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--var", default="MMU_GEMM_PIPE", help="env switch of the variants compared")
-    ap.add_argument("--vals", default="1,0", help="values of --var, timed interleaved in one process")
     a = ap.parse_args()
     M, dev, bf = a.rows, "cuda", torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
@@ -154,20 +133,13 @@ def main():
                         epi=K.epilogue(K.EPI_STORE, accumulate=True)),
          lambda: torch.matmul(dY.t(), O)),
     ]
-    vals = a.vals.split(",")
-    print(f"{'gemm':26s} {'M':>7s} {'N':>5s} {'K':>7s} " + " ".join(f"{(a.var[-8:] + '=' + v)[-18:]:>18s}" for v in vals)
-          + f" {'hipBLASLt':>18s}")
+    print(f"{'gemm':26s} {'M':>7s} {'N':>5s} {'K':>7s} {'mmu_gemm':>18s} {'hipBLASLt':>18s}")
     for name, m, n, k, f_mmu, f_ref in cases:
         fl = 2.0 * m * n * k
-        ts = {v: float("inf") for v in vals}
-        for _ in range(3):  # interleaved rounds in one process
-            for v in vals:
-                set_env(a.var, v)
-                ts[v] = min(ts[v], timed(f_mmu, a.iters))
-        set_env(a.var, None)
+        t1 = min(timed(f_mmu, a.iters) for _ in range(3))
         t2 = timed(f_ref, a.iters)
-        print(f"{name:26s} {m:7d} {n:5d} {k:7d} " + " ".join(f"{ts[v]:8.3f}ms {fl / ts[v] / 1e9:6.0f}T" for v in vals)
-              + f" {t2:8.3f}ms {fl / t2 / 1e9:6.0f}T", flush=True)
+        print(f"{name:26s} {m:7d} {n:5d} {k:7d} {t1:8.3f}ms {fl / t1 / 1e9:6.0f}T {t2:8.3f}ms {fl / t2 / 1e9:6.0f}T",
+              flush=True)
 
 
 if __name__ == "__main__":

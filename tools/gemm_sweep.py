@@ -41,13 +41,9 @@ def main():
         else:
             e = None
         fn = lambda: K.gemm(A, k, True, B, k if a.bk else N, bool(a.bk), out, N, M, N, k, epi=e)  # noqa: E731
-        ts = []
-        for pipe in ("1", "0"):
-            os.environ["MMU_GEMM_PIPE"] = pipe
-            ts.append(timed(fn, 10))
+        t = timed(fn, 10)
         fl = 2.0 * M * N * k
-        print(f"K={k:5d}  pipe {ts[0]:.4f} ms ({fl / ts[0] / 1e9:7.1f} TF/s)   2stg {ts[1]:.4f} ms "
-              f"({fl / ts[1] / 1e9:7.1f} TF/s)", flush=True)
+        print(f"K={k:5d}  {t:.4f} ms ({fl / t / 1e9:7.1f} TF/s)", flush=True)
 
 
 if __name__ == "__main__":
