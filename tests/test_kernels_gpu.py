@@ -228,16 +228,19 @@ def _keep_np(seed, idx, p):
     return draw >= np.uint64(int(p * 65536.0 + 0.5))
 
 
-def test_gemm_epilogues_exact_first_and_last_tile_rows(dev):
+@pytest.mark.parametrize("M,N", [(256 * 257, 768), (256 * 64 + 32, 3072)])
+def test_gemm_epilogues_exact_first_and_last_tile_rows(dev, M, N):
     """M = 256 * 257 rows x 3 column tiles = 771 tiles (3 whole rounds of 256 CUs + a partial
     one), the epilogues' row addressing (per-lane row bases + wave-uniform row offsets) checked
     on the first and the last tile row against torch: the f32 hidden-stream epilogue with the
     residual LayerNorm recomputed and dropout -- keep decisions equal to a numpy restatement
     of mmu_keep4 at the element's global index --, GELU + gelu' aux, and FLAVA's dropout +
-    QuickGELU with its derivative aux."""
+    QuickGELU with its derivative aux.  M = 16416, N = 3072 is batch 32's FFN1 shape (its
+    last tile row holds 32 live rows); the bias-gradient column sums of the dGELU product and
+    a bf16 residual add are checked over all rows."""
     import numpy as np
     k = K()
-    M, N, Kd = 256 * 257, 768, 768
+    Kd = 768
     A, B = rnd(M, Kd, dev=dev, seed=131), rnd(N, Kd, dev=dev, seed=132, scale=0.1)
     bias = torch.randn(N, device=dev) * 0.1
     y = A.float() @ B.float().t() + bias
@@ -275,6 +278,16 @@ def test_gemm_epilogues_exact_first_and_last_tile_rows(dev):
         sg = torch.sigmoid(1.702 * u)
         close(H[r], u * sg)
         close(Z[r], keep / (1 - p) * (sg + 1.702 * u * sg * (1 - sg)))
+    # dGELU (aux = the forward's gelu') + bias-gradient column sums over every row; bf16 residual add
+    Zin = rnd(M, N, dev=dev, seed=133)
+    cs = torch.zeros(N, device=dev)
+    k.gemm(A, Kd, True, B, Kd, True, H, N, M, N, Kd, epi=k.epilogue(k.EPI_DGELU, aux=Zin, colsum=cs))
+    dg = (y - bias) * Zin.float()
+    close(H, dg)
+    torch.testing.assert_close(cs, dg.sum(0), rtol=2e-3, atol=2e-3 * dg.abs().sum(0).max().item())
+    R16 = rnd(M, N, dev=dev, seed=134)
+    k.gemm(A, Kd, True, B, Kd, True, H, N, M, N, Kd, epi=k.epilogue(k.EPI_ADD_RES, residual=R16))
+    close(H, y - bias + R16.float())
 
 
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, False), (False, True)])
