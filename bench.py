@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sync-bn", action="store_true",
                     help="mmbt, N > 1: the trunk's BatchNorms normalise over the whole global batch (cross-rank sums)")
+    ap.add_argument("--no-stream-residue", action="store_true",
+                    help="mmbt: the trunk's residual stream in plain bf16 (the round-4 trunk; for same-box A/Bs)")
     ap.add_argument("--workload", default="mmbt", choices=["mmbt", "flava", "uncertainty", "encoders", "vilt"])
     ap.add_argument("--enc-batch", type=int, default=128, help="encoders / vilt: samples per rank per step")
     ap.add_argument("--members", type=int, default=5, help="uncertainty: deep-ensemble members K")
@@ -533,7 +535,9 @@ def main():
     from src import kernels as K
     from src.dp import GradBucketer, broadcast_parameters, convert_sync_batchnorm
     from src import encoder
+    from src import resnet
 
+    resnet.STREAM_RESIDUE = not args.no_stream_residue
     # MIOpen solver choice for the ResNet convs: "find" mode over the find-db shipped in
     # multi-modal-uncertainty_amd/miopen_db (per-rank batches 256/128/64/32 pre-searched on
     # MI355X, so no search runs here); MMU_MIOPEN_FIND=0 = MIOpen's immediate-mode heuristics
@@ -551,7 +555,7 @@ def main():
         broadcast_parameters(model)
         if args.sync_bn:
             convert_sync_batchnorm(model)
-        bucketer = GradBucketer(model)
+        bucketer = GradBucketer(model, optimizer=opt)  # 1/world folded into the fused BertAdam
     x, y = synthetic_batch(B, T, seed=100 + rank, device=dev)
     model.train()
 
@@ -607,6 +611,7 @@ def main():
                    "global_batch": args.global_batch, "per_rank_batch": B, "seq_len": 512, "tokens": L,
                    "parallelism": f"dp{world}", "grad_accum": 1, "optimizer": "BertAdam (fused HIP)",
                    "batchnorm": "whole-batch (cross-rank sums)" if (args.sync_bn and world > 1) else "per-rank batch",
+                   "trunk_stream": "bf16 + 8-bit residue" if resnet.STREAM_RESIDUE else "bf16",
                    "trainable_params": sum(p.numel() for p in model.parameters())},
         "roofline": {"bound": "mfma", "kernel": "mmu_gemm (all BERT-layer GEMMs, fwd + bwd)",
                      "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",

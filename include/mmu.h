@@ -320,6 +320,11 @@ int mmu_stem_conv_wgrad(const void* dY, const void* X, float* dW, int64_t n_img,
  * eval: running statistics.  weight / bias may be NULL (affine = False).
  * relu_mask (may be NULL; needs relu): [rows, C/8] u8 written with bit e of byte (r, c/8)
  *   = Y[r, c+e] > 0, for the backward to read instead of Y (1/16 of its bytes).
+ * y_res / skip_res (may be NULL): the residual stream past bf16 -- y_res [rows, C] i8 is written
+ *   with the 8-bit residue of each output, r = rint((v - Y) * 2^15 / 2^e) (v the f32 value, e
+ *   the binary exponent of Y); a skip is then read as skip + skip_res * 2^(e(skip) - 15).  Two
+ *   uses: a Bottleneck's bn3 (skip, relu, skip_res and y_res all given) and the downsample's
+ *   BatchNorm (no skip, no relu, y_res only).
  * ws: device scratch of >= mmu_batchnorm_ws_bytes(C) bytes (per-block partial sums +
  * per-channel coefficients, ~8 MiB), 16-B aligned.
  */
@@ -327,8 +332,8 @@ int64_t mmu_batchnorm_ws_bytes(int64_t C);
 int mmu_batchnorm_fwd(const void* X, const void* skip, void* Y, int64_t rows, int64_t C,
                       const float* weight, const float* bias, float* running_mean, float* running_var,
                       int64_t* num_batches_tracked, int training, float momentum, float eps, int relu,
-                      float* save_mean, float* save_invstd, void* relu_mask, void* ws, int64_t ws_bytes,
-                      mmu_stream_t stream);
+                      float* save_mean, float* save_invstd, void* relu_mask, const void* skip_res, void* y_res,
+                      void* ws, int64_t ws_bytes, mmu_stream_t stream);
 /* Training-mode backward.  g = dY * [Y > 0] when relu, from relu_mask when given (the
  * forward's mask), else from Y (the forward's output); g = dY without relu;
  * dX [rows, C] bf16; dSkip (may be NULL) = g, the gradient of the residual input;
@@ -357,7 +362,8 @@ int mmu_batchnorm_stats(const void* X, int64_t rows, int64_t C, double* sums, vo
 int mmu_batchnorm_fwd_sums(const void* X, const void* skip, void* Y, int64_t rows, int64_t C, const double* sums,
                            const float* weight, const float* bias, float* running_mean, float* running_var,
                            int64_t* num_batches_tracked, float momentum, float eps, int relu, float* save_mean,
-                           float* save_invstd, void* relu_mask, void* ws, int64_t ws_bytes, mmu_stream_t stream);
+                           float* save_invstd, void* relu_mask, const void* skip_res, void* y_res, void* ws,
+                           int64_t ws_bytes, mmu_stream_t stream);
 int mmu_batchnorm_bwd_reduce(const void* dY, const void* Y, const void* relu_mask, const void* X, int64_t rows,
                              int64_t C, const float* save_mean, const float* save_invstd, int relu, double* sums,
                              float* dweight, float* dbias, void* ws, int64_t ws_bytes, mmu_stream_t stream);
@@ -376,11 +382,13 @@ int mmu_batchnorm_bwd_sums(const void* dY, const void* Y, const void* relu_mask,
  *   bf16_offset (-1 = none), active (0 = skipped like a None grad), first_chunk,
  *   n_chunks}, followed by 3 per chunk {tensor, start, len}.
  * steps int32 [n_tensors] (device, incremented); ws f32 >= n_chunks + 2*n_tensors.
+ * grad_scale: the gradient the optimizer sees is grads * grad_scale (clip norm included) --
+ * data parallelism's 1/world applied here instead of a separate pass over the summed grads.
  */
 int mmu_bertadam_step(float* params, const float* grads, float* m, float* v, void* bf16_copy,
                       const int64_t* table, int32_t* steps, int64_t n_tensors, int64_t n_chunks,
                       float lr_decay, float lr_nodecay, float wd, float warmup, float t_total,
-                      float b1, float b2, float eps, float max_grad_norm,
+                      float b1, float b2, float eps, float max_grad_norm, float grad_scale,
                       float* ws, int64_t ws_floats, mmu_stream_t stream);
 
 /* ------------------------------------------------------------------ uncertainty

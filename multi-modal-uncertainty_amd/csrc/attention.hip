@@ -24,6 +24,7 @@
 #include "mmu_internal.h"
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
 
 namespace mmu {
 
@@ -43,17 +44,37 @@ static __device__ __forceinline__ uint32_t drop_pair(uint32_t sbh, uint32_t q, u
   return lowbias32(((q * Lp + key) >> 1) ^ sbh);
 }
 
-// v_max3_f32 without hipcc's NaN canonicalisation of each MFMA output (a v_max_f32 x,x per
-// operand under plain fmaxf)
+// max of three as v_max3_f32, compiler-visible: its operands come straight out of MFMA
+// accumulators, and only the compiler's hazard recognizer knows how long to wait before reading
+// them (an asm v_max3_f32 here, rounds 1-4, read the S tile right behind its MFMA -- a stale
+// value, harmless only because the deferred-max softmax is invariant to the subtracted max)
 static __device__ __forceinline__ float max3f(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return __builtin_fmaxf(__builtin_fmaxf(a, b), c);
+}
+// (m & a) | (~m & b), written so that hipcc emits ONE v_bitop3_b32 (gfx950).  Not inline asm: the
+// operands here come straight out of MFMA accumulators, and the hazard recognizer does not see
+// inside an asm statement -- an asm v_bfi_b32 reading an MFMA result two instructions after the
+// MFMA read it before the MFMA had written it (the 13 % dK error of a round-5 dropout test)
+static __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+  return (m & a) | (~m & b);
+}
+// the keep bit `pos` of word w as an all-ones / zero mask (v_bfe_i32).  In asm so that the
+// optimizer cannot see that the mask is 0 / -1: it would turn the bfi above into a compare
+// and a v_cndmask (one VALU more per element)
+static __device__ __forceinline__ uint32_t keepmask(uint32_t w, uint32_t pos) {
+  uint32_t r;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(r) : "v"(w), "v"(pos));
   return r;
 }
-// (m & a) | (~m & b) as ONE v_bfi_b32 (hipcc otherwise rebuilds ~m & b from a sign test)
-static __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+// f(integral_constant<int, R>) for R = 0, 1, ... in order (compile-time indices, C++17)
+template <typename F, int... R>
+static __device__ __forceinline__ void static_for(F&& f, std::integer_sequence<int, R...>) {
+  (f(std::integral_constant<int, R>{}), ...);
+}
+template <int POS>  // (a compile-time bit position as an inline constant, not a VGPR)
+static __device__ __forceinline__ uint32_t keepmask(uint32_t w) {
   uint32_t r;
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(r) : "v"(w), "n"(POS));
   return r;
 }
 static __host__ __device__ __forceinline__ uint32_t drop_thr(float p) { return (uint32_t)(p * 65536.0f + 0.5f); }
@@ -108,6 +129,16 @@ static __device__ __forceinline__ __amdgpu_buffer_rsrc_t urs(const void* base, i
 // ---- LDS-DMA helpers (buffer_load ... lds: lane-linear LDS destination, per-lane source)
 static __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t off) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (MMU_LDS(void)*)lds, 16, off, 0, 0, 0);
+}
+// A tile's descriptor: the buffer [base, base + bytes) advanced by the tile's byte offset `off`
+// (wave-uniform: SALU work), so the lanes' offsets within a tile stay loop-invariant VGPRs and
+// the range check still sees rows past the buffer (the scalar-offset operand of a buffer load is
+// outside the range check, so a per-tile row offset cannot go there: past-the-end rows would be
+// read instead of returning zero)
+// (bytes - off clamped at 0: an empty buffer -- e.g. no keep words without dropout -- reads zeros
+// and keeps the wave's per-tile DMA count, which its vmcnt waits assume)
+static __device__ __forceinline__ __amdgpu_buffer_rsrc_t urs_at(const void* base, int bytes, int off) {
+  return urs((const char*)base + off, bytes > off ? bytes - off : 0);
 }
 static __device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t off) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (MMU_LDS(void)*)lds, 4, off, 0, 0, 0);
@@ -227,8 +258,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   // dropout counter base of row q: seed_bh + 4 (q nkv) + 2h  (+ 4j + s2 per tile half)
   const uint32_t ctr = seed_for(p.seed, bh) + 4u * (uint32_t)q * (uint32_t)nkv + 2u * (uint32_t)h;
 
-  const __amdgpu_buffer_rsrc_t rkv = urs((void*)(p.qkv + (int64_t)b * L * p.ld_qkv), (int)(L * p.ld_qkv * 2));
-  const __amdgpu_buffer_rsrc_t rm = urs((void*)(p.keymask + (int64_t)b * L), (int)(L * 4));
+  const void* kv_base = p.qkv + (int64_t)b * L * p.ld_qkv;
+  const int kv_bytes = (int)(L * p.ld_qkv * 2);
+  const void* m_base = p.keymask + (int64_t)b * L;
   bf16x8 qf[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
@@ -244,20 +276,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   float lsum[4] = {0.f, 0.f, 0.f, 0.f};
 
   // per tile: waves 0,1 -> K pieces, waves 2,3 -> V pieces (4 each, rows in kperm order);
-  // wave 0 also the (unpermuted) mask row
+  // wave 0 also the (unpermuted) mask row.  The lane's source offsets within a tile are
+  // loop-invariant; the tile's row offset goes in the DMA's scalar offset
+  uint32_t kv_off[4];
+#pragma unroll
+  for (int pc = 0; pc < 4; ++pc) {
+    const int piece = 4 * (w & 1) + pc;
+    const int row = 8 * piece + (l >> 3), c = (l & 7) ^ fsw(row);
+    const int key = (row & 32) | kperm(row & 31);
+    kv_off[pc] = (uint32_t)((key * p.ld_qkv + (w < 2 ? HD : 2 * HD) + hd * 64 + 8 * c) * 2);
+  }
+  const uint32_t m_off = (uint32_t)(16 * l);
   auto issue = [&](int j) {
     char* st = smem + (j % FWD_NS) * FWD_STAGE;
     const int k0 = j * 64;
-    const int off_col = (w < 2 ? HD : 2 * HD) + hd * 64;
     char* dst = st + (w < 2 ? 0 : FWD_TILE);
+    const __amdgpu_buffer_rsrc_t rt = urs_at(kv_base, kv_bytes, k0 * p.ld_qkv * 2);
 #pragma unroll
-    for (int pc = 0; pc < 4; ++pc) {
-      const int piece = 4 * (w & 1) + pc;
-      const int row = 8 * piece + (l >> 3), c = (l & 7) ^ fsw(row);
-      const int key = (row & 32) | kperm(row & 31);
-      dma16(rkv, dst + piece * 1024, (uint32_t)(((k0 + key) * p.ld_qkv + off_col + 8 * c) * 2));
-    }
-    if (w == 0 && l < 16) dma16(rm, st + 2 * FWD_TILE, (uint32_t)((k0 + 4 * l) * 4));
+    for (int pc = 0; pc < 4; ++pc) dma16(rt, dst + (4 * (w & 1) + pc) * 1024, kv_off[pc]);
+    if (w == 0 && l < 16) dma16(urs_at(m_base, L * 4, k0 * 4), st + 2 * FWD_TILE, m_off);
   };
   auto wait_for = [&](int ahead) {
     if (w == 0) {
@@ -271,9 +308,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 
   // one 64-key tile; PARTIAL: keys >= L exist in it (the last tile only).  Register r of
   // sc[s2] holds key 64j + 32 s2 + 16h + r.
-  auto tile = [&](int j, auto partial_tag) {
+  auto tile = [&](int j, auto partial_tag, const char* st) {
     constexpr bool PARTIAL = decltype(partial_tag)::value;
-    const char* st = smem + (j % FWD_NS) * FWD_STAGE;
     const char* Ks = st;
     const char* Vs = st + FWD_TILE;
     const float* mk = (const float*)(st + 2 * FWD_TILE);
@@ -381,13 +417,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     raw_barrier();
     if (j + FWD_NS - 1 < nkv) issue(j + FWD_NS - 1);
   };
-  for (int j = 0; j < nfull; ++j) {
+  // full tiles unrolled by the ring depth: the stage base is a constant folded into the
+  // ds_read immediate offsets (a runtime (j % 2) * stage base cost ~25 address VALU per tile)
+  static_assert(FWD_NS == 2, "the forward loop is unrolled by its ring depth");
+  for (int j = 0; j < nfull; j += 2) {
     step(j);
-    if (wave_live) tile(j, std::integral_constant<bool, false>{});
+    if (wave_live) tile(j, std::integral_constant<bool, false>{}, smem);
+    if (j + 1 < nfull) {
+      step(j + 1);
+      if (wave_live) tile(j + 1, std::integral_constant<bool, false>{}, smem + FWD_STAGE);
+    }
   }
   if (nfull < nkv) {
     step(nfull);
-    if (wave_live) tile(nfull, std::integral_constant<bool, true>{});
+    if (wave_live) tile(nfull, std::integral_constant<bool, true>{}, smem + (nfull % FWD_NS) * FWD_STAGE);
   }
   raw_barrier();  // every wave is done with the ring: it becomes the O staging area
   if (!wave_live) return;
@@ -465,26 +508,26 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
   const bool wave_live = k0w < L, kv = key < L;
   const bool drop = DROP;
   const float zs = drop ? 1.0f / (1.0f - p.drop_p) : 1.0f;
-  const float izs = drop ? 1.0f - p.drop_p : 1.0f;
   const int lane31 = l & 31;
   const int nkv = (L + 63) / 64;
   const float mkey = kv ? p.keymask[(int64_t)b * L + key] * LOG2E : NEG_INF;
   const bf16* base = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64;
 
   // operand buffers of this (batch item, head): rows beyond L are out of range -> zero
-  const __amdgpu_buffer_rsrc_t rq = urs((void*)(p.qkv + (int64_t)b * L * p.ld_qkv), (int)(L * p.ld_qkv * 2));
-  const __amdgpu_buffer_rsrc_t rdo = urs((void*)(p.dout + (int64_t)b * L * p.ld_do), (int)(L * p.ld_do * 2));
-  const __amdgpu_buffer_rsrc_t rl = urs((void*)(p.lse + (int64_t)bh * L), (int)(L * 4));
-  const __amdgpu_buffer_rsrc_t rd = urs((void*)(p.delta + (int64_t)bh * L), (int)(L * 4));
-  const __amdgpu_buffer_rsrc_t rk =
-      urs((void*)(drop ? p.dropmask + (int64_t)bh * L * nkv : p.dropmask), drop ? (int)(L * nkv * 8) : 0);
+  const void* q_base = p.qkv + (int64_t)b * L * p.ld_qkv;
+  const int q_bytes = (int)(L * p.ld_qkv * 2);
+  const void* do_base = p.dout + (int64_t)b * L * p.ld_do;
+  const int do_bytes = (int)(L * p.ld_do * 2);
+  const void* l_base = p.lse + (int64_t)bh * L;
+  const void* d_base = p.delta + (int64_t)bh * L;
+  const void* k_base = drop ? (const void*)(p.dropmask + (int64_t)bh * L * nkv) : nullptr;
 
   bf16x8 kf[4], vf[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     uint4 u = kv ? *(const uint4*)(base + (int64_t)key * p.ld_qkv + HD + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
     uint4 v = kv ? *(const uint4*)(base + (int64_t)key * p.ld_qkv + 2 * HD + 16 * ks + 8 * h) : make_uint4(0, 0, 0, 0);
-    kf[ks] = scale_frag(u, 0.125f);
+    kf[ks] = scale_frag(u, -0.125f);  // exact; S enters negated: the accumulator starts at +lse
     vf[ks] = *(bf16x8*)&v;
   }
   f32x16 dk[2], dv[2];
@@ -492,28 +535,33 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
   for (int i = 0; i < 16; ++i) { dk[0][i] = 0.f; dk[1][i] = 0.f; dv[0][i] = 0.f; dv[1][i] = 0.f; }
 
   const int nq = (L + 31) / 32;
-  // per tile: wave 0 -> Q pieces 0..3, lse, delta (6 DMAs); wave 1 -> dO pieces 0..3, keep (5)
+  // per tile: wave 0 -> Q pieces 0..3, lse, delta (6 DMAs); wave 1 -> dO pieces 0..3, keep (5).
+  // Lane offsets within a tile are loop-invariant; the tile's row offset goes in the scalar offset
+  uint32_t pc_off[4];
+  const int ldr = w == 0 ? p.ld_qkv : p.ld_do;
+#pragma unroll
+  for (int pc = 0; pc < 4; ++pc) {
+    const int row = 8 * pc + (l >> 3), c = (l & 7) ^ fsw(row);
+    pc_off[pc] = (uint32_t)((row * ldr + hd * 64 + 8 * c) * 2);
+  }
+  const uint32_t row_off = (uint32_t)(16 * l), kw_off = (uint32_t)((((l >> 1) * nkv + bx) * 8) + 4 * (l & 1));
   auto issue = [&](int i) {
     char* st = smem + (i % DK_NS) * DK_STAGE;
     const int q0 = i * 32;
     if (w == 0) {
+      const __amdgpu_buffer_rsrc_t rt = urs_at(q_base, q_bytes, q0 * p.ld_qkv * 2);
 #pragma unroll
-      for (int pc = 0; pc < 4; ++pc) {
-        const int row = 8 * pc + (l >> 3), c = (l & 7) ^ fsw(row);
-        dma16(rq, st + pc * 1024, (uint32_t)(((q0 + row) * p.ld_qkv + hd * 64 + 8 * c) * 2));
-      }
+      for (int pc = 0; pc < 4; ++pc) dma16(rt, st + pc * 1024, pc_off[pc]);
       if (l < 8) {
-        dma16(rl, st + 2 * DK_TILE, (uint32_t)((q0 + 4 * l) * 4));
-        dma16(rd, st + 2 * DK_TILE + 128, (uint32_t)((q0 + 4 * l) * 4));
+        dma16(urs_at(l_base, L * 4, q0 * 4), st + 2 * DK_TILE, row_off);
+        dma16(urs_at(d_base, L * 4, q0 * 4), st + 2 * DK_TILE + 128, row_off);
       }
     } else {
+      const __amdgpu_buffer_rsrc_t rt = urs_at(do_base, do_bytes, q0 * p.ld_do * 2);
 #pragma unroll
-      for (int pc = 0; pc < 4; ++pc) {
-        const int row = 8 * pc + (l >> 3), c = (l & 7) ^ fsw(row);
-        dma16(rdo, st + DK_TILE + pc * 1024, (uint32_t)(((q0 + row) * p.ld_do + hd * 64 + 8 * c) * 2));
-      }
+      for (int pc = 0; pc < 4; ++pc) dma16(rt, st + DK_TILE + pc * 1024, pc_off[pc]);
       // keep word of query row q0 + l/2 for this key block: 4 B per lane (low / high half)
-      dma4(rk, st + 2 * DK_TILE + 256, (uint32_t)((((q0 + (l >> 1)) * nkv + bx) * 8) + 4 * (l & 1)));
+      dma4(urs_at(k_base, drop ? L * nkv * 8 : 0, q0 * nkv * 8), st + 2 * DK_TILE + 256, kw_off);
     }
   };
   // vmcnt: this wave's DMAs per tile (6 or 5) times the tiles allowed to stay in flight
@@ -530,13 +578,17 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
   };
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K / V fragment loads
   for (int i = 0; i < DK_NS - 1 && i < nq; ++i) issue(i);
-  for (int i = 0; i < nq; ++i) {
+  // one query tile; the loop below is unrolled by the ring depth so the stage is a compile-time
+  // constant folded into the ds_read immediate offsets (a runtime (i % 4) * stage base cost 32
+  // address VALU per tile)
+  auto qtile = [&](int i, auto sg_tag) {
+    constexpr int SG = decltype(sg_tag)::value;
     // tiles i+1, i+2 may stay in flight; tile i must have landed for every wave
     const int ahead = nq - 1 - i < DK_NS - 2 ? nq - 1 - i : DK_NS - 2;
     wait_for(ahead);
     raw_barrier();
     if (i + DK_NS - 1 < nq) issue(i + DK_NS - 1);  // into the stage tile i-1 used (all waves are past it)
-    const char* st = smem + (i % DK_NS) * DK_STAGE;
+    const char* st = smem + SG * DK_STAGE;
     const char* Qs = st;
     const char* Ds = st + DK_TILE;
     const float* lse = (const float*)(st + 2 * DK_TILE);
@@ -545,39 +597,39 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
     if (wave_live) {
       // row constants of the 16 query rows a lane's registers hold: r -> row (r&3) + 8(r>>2) + 4h,
       // i.e. four runs of 4 consecutive rows -> 16-B LDS reads (keep words: stride-2 pairs)
-      f32x4 nl4[4], nd4[4];  // -lse, -delta of the 16 rows
+      f32x4 l4[4], nd4[4];  // +lse, -delta/zs of the 16 rows (dQ stores delta so)
       uint32_t kwr[16];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        nl4[j] = -*(const f32x4*)(lse + 8 * j + 4 * h);
+        l4[j] = *(const f32x4*)(lse + 8 * j + 4 * h);
         nd4[j] = *(const f32x4*)(dlt + 8 * j + 4 * h);
         if (DROP)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) kwr[4 * j + i] = kbit[2 * (8 * j + 4 * h + i)];
+          for (int i2 = 0; i2 < 4; ++i2) kwr[4 * j + i2] = kbit[2 * (8 * j + 4 * h + i2)];
       }
-      // S starts at -lse of its query row, dP at -delta / zs (row constants as initial
-      // accumulators): then dS = p (keep ? dp zs : -delta) and dropped-P = keep ? p zs : 0,
-      // the keep bit as an all-ones / zero mask (v_bfe_i32 of the row's keep word at this
-      // lane's key) bit-selecting between the two; products as packed pairs
+      // the accumulators start at the row constants: sc = lse - S (K negated), dp = dP - delta/zs.
+      // p = exp2(-log2e sc + mask);  dS / zs = p (keep ? dp : -delta/zs),  dropped P / zs =
+      // keep ? p : 0 -- the keep bit as an all-ones / zero mask (v_bfe_i32 of the row's keep
+      // word at this lane's key) bit-selecting; the 1/(1-p) of both goes into dK / dV at the end
       f32x16 sc, dp;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        sc[r] = nl4[r >> 2][r & 3];
-        dp[r] = nd4[r >> 2][r & 3] * izs;
+        sc[r] = l4[r >> 2][r & 3];
+        dp[r] = nd4[r >> 2][r & 3];
       }
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Qs, 0, ks, l), kf[ks], sc, 0, 0, 0);
         dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ds, 0, ks, l), vf[ks], dp, 0, 0, 0);
       }
-      f32x16 pz;  // dropped P (for dV)
+      f32x16 pz;  // dropped P / zs (for dV)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float pr = __builtin_amdgcn_exp2f(fmaf(sc[r], LOG2E, mkey));
+        const float pr = __builtin_amdgcn_exp2f(fmaf(sc[r], -LOG2E, mkey));
         if (DROP) {
-          const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)kwr[r], lane31, 1);
-          pz[r] = __uint_as_float(m & __float_as_uint(pr * zs));
-          sc[r] = pr * __uint_as_float(bfi(m, __float_as_uint(dp[r] * zs), __float_as_uint(nd4[r >> 2][r & 3])));
+          const uint32_t m = keepmask(kwr[r], lane31);
+          pz[r] = __uint_as_float(m & __float_as_uint(pr));
+          sc[r] = pr * __uint_as_float(bfi(m, __float_as_uint(dp[r]), __float_as_uint(nd4[r >> 2][r & 3])));
         } else {
           pz[r] = pr;
           sc[r] = pr * dp[r];
@@ -593,7 +645,16 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
         }
       }
     }
-    }
+  };
+  for (int i0 = 0; i0 < nq; i0 += DK_NS) {
+    qtile(i0, std::integral_constant<int, 0>{});
+    if (i0 + 1 < nq) qtile(i0 + 1, std::integral_constant<int, 1>{});
+    if (i0 + 2 < nq) qtile(i0 + 2, std::integral_constant<int, 2>{});
+    if (i0 + 3 < nq) qtile(i0 + 3, std::integral_constant<int, 3>{});
+  }
+  static_assert(DK_NS == 4, "the dK/dV loop is unrolled by its ring depth");
+  // dK = (1/8) zs sum dS' Q, dV = zs sum P' dO (the primes: the loop's values, 1/zs of the true ones)
+  const float dks = 0.125f * zs;
   if (p.colsum) {  // bias-gradient partials of K and V: this block's 64 keys, per column
     // each lane holds ONE column (32 dt + l&31) for 16 keys: in-lane sum + the other half-wave
     float* red = (float*)smem;  // [2 waves][K 64 | V 64]
@@ -610,8 +671,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
       sk += __shfl_xor(sk, 32, 64);
       sv += __shfl_xor(sv, 32, 64);
       if (h == 0) {
-        red[w * 128 + 32 * dt + l] = sk * 0.125f;
-        red[w * 128 + 64 + 32 * dt + l] = sv;
+        red[w * 128 + 32 * dt + l] = sk * dks;
+        red[w * 128 + 64 + 32 * dt + l] = sv * zs;
       }
     }
     raw_barrier();
@@ -631,8 +692,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
       const int kk = k0w + (r & 3) + 8 * (r >> 2) + 4 * h;
       if (kk < L) {
         const int64_t off = (int64_t)kk * p.ld_out + 32 * dt + (l & 31);
-        outb[off + HD] = f2bf(dk[dt][r] * 0.125f);
-        outb[off + 2 * HD] = f2bf(dv[dt][r]);
+        outb[off + HD] = f2bf(dk[dt][r] * dks);
+        outb[off + 2 * HD] = f2bf(dv[dt][r] * zs);
       }
     }
 }
@@ -663,10 +724,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
   const int nkv = (L + 63) / 64;
   const bf16* base = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64;
 
-  const __amdgpu_buffer_rsrc_t rkv = urs((void*)(p.qkv + (int64_t)b * L * p.ld_qkv), (int)(L * p.ld_qkv * 2));
-  const __amdgpu_buffer_rsrc_t rm = urs((void*)(p.keymask + (int64_t)b * L), (int)(L * 4));
-  const __amdgpu_buffer_rsrc_t rk =
-      urs((void*)(drop ? p.dropmask + (int64_t)bh * L * nkv : p.dropmask), drop ? (int)(L * nkv * 8) : 0);
+  const void* kv_base = p.qkv + (int64_t)b * L * p.ld_qkv;
+  const int kv_bytes = (int)(L * p.ld_qkv * 2);
+  const void* m_base = p.keymask + (int64_t)b * L;
+  const void* k_base = drop ? (const void*)(p.dropmask + (int64_t)bh * L * nkv) : nullptr;
+  const int k_bytes = drop ? (int)(L * nkv * 8) : 0;
 
   bf16x8 qf[4], df[4];
   const bf16* dob = p.dout + ((int64_t)b * L + q) * p.ld_do + hd * 64;
@@ -691,31 +753,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
       for (int e = 0; e < 8; ++e) dsum = fmaf(bf2f(ov[e]), bf2f(df[ks][e]), dsum);
     }
     dsum += __shfl_xor(dsum, 32, 64);
-    if (qv && h == 0) p.delta[(int64_t)bh * L + q] = -dsum;  // stored negated: dK/dV uses -delta
+    // stored as -delta/zs: the dK/dV kernel starts its dP accumulators there and selects it for
+    // the dropped entries (dS / zs = p (keep ? dP - delta/zs : -delta/zs))
+    if (qv && h == 0) p.delta[(int64_t)bh * L + q] = -dsum / zs;
   }
-  const float nlse = qv ? -p.lse[(int64_t)bh * L + q] : -__builtin_huge_valf();
-  const float dlt = dsum;
-  const float ndz = -dlt / zs;
-  const uint32_t ndl_bits = __float_as_uint(-dlt);
+  // -lse log2e: the exponent's per-row constant (p = exp2(log2e S' - lse log2e), S' = S/8 + mask)
+  const float nlse2 = qv ? -p.lse[(int64_t)bh * L + q] * LOG2E : -__builtin_huge_valf();
+  const float ndz = -dsum / zs;
+  const uint32_t ndz_bits = __float_as_uint(ndz);
   f32x16 dq[2];
 #pragma unroll
   for (int i = 0; i < 16; ++i) { dq[0][i] = 0.f; dq[1][i] = 0.f; }
 
   // per tile: waves 0,1 -> K pieces (4 each), waves 2,3 -> V pieces; wave 0 also the mask row;
   // every wave the keep words of its 32 query rows (4 B per lane)
+  // (lane offsets within a tile loop-invariant; the tile's row / word offset in the scalar offset)
+  uint32_t kv_off[4];
+#pragma unroll
+  for (int pc = 0; pc < 4; ++pc) {
+    const int piece = 4 * (w & 1) + pc;
+    const int row = 8 * piece + (l >> 3), c = (l & 7) ^ fsw(row);
+    kv_off[pc] = (uint32_t)((row * p.ld_qkv + (w < 2 ? HD : 2 * HD) + hd * 64 + 8 * c) * 2);
+  }
+  const uint32_t m_off = (uint32_t)(16 * l), kw_off = (uint32_t)(((q0w + (l >> 1)) * nkv * 8) + 4 * (l & 1));
   auto issue = [&](int j) {
     char* st = smem + (j % DQ_NS) * DQ_STAGE;
     const int k0 = j * 64;
-    const int off_col = (w < 2 ? HD : 2 * HD) + hd * 64;
     char* dst = st + (w < 2 ? 0 : DQ_TILE);
+    const __amdgpu_buffer_rsrc_t rt = urs_at(kv_base, kv_bytes, k0 * p.ld_qkv * 2);
 #pragma unroll
-    for (int pc = 0; pc < 4; ++pc) {
-      const int piece = 4 * (w & 1) + pc;
-      const int row = 8 * piece + (l >> 3), c = (l & 7) ^ fsw(row);
-      dma16(rkv, dst + piece * 1024, (uint32_t)(((k0 + row) * p.ld_qkv + off_col + 8 * c) * 2));
-    }
-    if (w == 0 && l < 16) dma16(rm, st + 2 * DQ_TILE, (uint32_t)((k0 + 4 * l) * 4));
-    dma4(rk, st + 2 * DQ_TILE + 256 + w * 256, (uint32_t)((((q0w + (l >> 1)) * nkv + j) * 8) + 4 * (l & 1)));
+    for (int pc = 0; pc < 4; ++pc) dma16(rt, dst + (4 * (w & 1) + pc) * 1024, kv_off[pc]);
+    if (w == 0 && l < 16) dma16(urs_at(m_base, L * 4, k0 * 4), st + 2 * DQ_TILE, m_off);
+    dma4(urs_at(k_base, k_bytes, j * 8), st + 2 * DQ_TILE + 256 + w * 256, kw_off);
   };
   auto wait_for = [&](int ahead) {
     if (w == 0) {
@@ -749,7 +818,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
 #pragma unroll
       for (int st2 = 0; st2 < 2; ++st2) {
         const uint32_t kw32 = (uint32_t)(kwh >> (32 * st2));
-        // S starts at -lse + mask: register r holds key kl = 32 st2 + 8 (r >> 2) + 4 h + (r & 3),
+        // S starts at the mask: register r holds key kl = 32 st2 + 8 (r >> 2) + 4 h + (r & 3),
         // so each group of 4 registers takes 4 contiguous mask entries (one f32x4 read)
         f32x16 sc, dp;
 #pragma unroll
@@ -757,7 +826,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
           const f32x4 mv = *(const f32x4*)(mk + 32 * st2 + 8 * g + 4 * h);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            sc[4 * g + e] = nlse + mv[e];
+            sc[4 * g + e] = mv[e];
             dp[4 * g + e] = ndz;
           }
         }
@@ -766,17 +835,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
           sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ks, 32 * st2, ks, l), qf[ks], sc, 0, 0, 0);
           dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Vs, 32 * st2, ks, l), df[ks], dp, 0, 0, 0);
         }
-        // p = exp2(log2e S');  dS^T = p * (keep ? dP zs - delta : -delta).  dp started at
-        // -delta / zs, so dp zs = dP zs - delta; the keep bit becomes an all-ones / zero mask
-        // (v_bfe_i32) that bit-selects it against -delta (without dropout kw is all ones).
-        // Products as packed pairs.
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float pr = __builtin_amdgcn_exp2f(sc[r] * LOG2E);
-          const int kc = (r & 3) + 8 * (r >> 2);
-          const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)kw32, kc, 1);
-          sc[r] = pr * __uint_as_float(bfi(m, __float_as_uint(dp[r] * zs), ndl_bits));
-        }
+        // p = exp2(log2e S' - lse log2e);  dS^T / zs = p * (keep ? dP - delta/zs : -delta/zs):
+        // dp started at -delta/zs; the keep bit becomes an all-ones / zero mask (v_bfe_i32) that
+        // bit-selects it against -delta/zs (without dropout kw is all ones).  The zs of dS goes
+        // into dQ's final scale.
+        auto one = [&](auto r_tag) {
+          constexpr int r = decltype(r_tag)::value;
+          const float pr = __builtin_amdgcn_exp2f(fmaf(sc[r], LOG2E, nlse2));
+          const uint32_t m = keepmask<(r & 3) + 8 * (r >> 2)>(kw32);
+          sc[r] = pr * __uint_as_float(bfi(m, __float_as_uint(dp[r]), ndz_bits));
+        };
+        static_for(one, std::make_integer_sequence<int, 16>{});
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           bf16x8 sf = acc_frag(sc, s2);
@@ -802,7 +871,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
     float* rows = (float*)smem;  // [4 waves][32 queries][RS]
     raw_barrier();               // every wave is done with the ring
     float* mine = rows + w * 32 * RS + (l & 31) * RS;
-    const float sc = qv ? 0.125f : 0.f;
+    const float sc = qv ? 0.125f * zs : 0.f;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -822,8 +891,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
   for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      bf16x4 v = {f2bf(dq[dt][4 * g] * 0.125f), f2bf(dq[dt][4 * g + 1] * 0.125f), f2bf(dq[dt][4 * g + 2] * 0.125f),
-                  f2bf(dq[dt][4 * g + 3] * 0.125f)};
+      const float s = 0.125f * zs;
+      bf16x4 v = {f2bf(dq[dt][4 * g] * s), f2bf(dq[dt][4 * g + 1] * s), f2bf(dq[dt][4 * g + 2] * s),
+                  f2bf(dq[dt][4 * g + 3] * s)};
       *(bf16x4*)(ob + 32 * dt + 8 * g + 4 * h) = v;
     }
 }

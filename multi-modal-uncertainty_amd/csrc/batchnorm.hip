@@ -201,11 +201,31 @@ __global__ __launch_bounds__(BN_THREADS) void bn_fwd_finalize_kernel(
   }
 }
 
-template <bool SKIP, bool RELU, bool MASK>
+// The trunk's residual stream carried past bf16 (round 5): the block output v (f32 in the
+// apply pass) is stored as its bf16 rounding y plus an 8-bit residue r = rint((v - y) * 2^15 /
+// 2^e), e = the binary exponent of y (|v - y| <= half an ulp of y = 2^(e-8), so |r| <= 128,
+// clamped to 127); the
+// next block's skip reads y + r * 2^(e-15), i.e. the stream to ~2^-15 of its value instead of
+// bf16's 2^-8, for 1 extra byte written and read per element.  The convs still read y (their
+// operands are bf16 anyway).  What it buys: tools/trunk_precision.py (a CPU emulation of the
+// trunk's storage points) and tests/test_mmbt_gpu.py.
+static __device__ __forceinline__ float bn_res_scale(float y) {  // 2^(e - 15), 0 for y == 0 / denormal
+  return __uint_as_float(__float_as_uint(y) & 0x7f800000u) * (1.0f / 32768.0f);
+}
+static __device__ __forceinline__ int8_t bn_res_encode(float v, float y) {
+  const uint32_t eb = __float_as_uint(y) & 0x7f800000u;
+  if (eb == 0u || eb >= (254u << 23)) return 0;
+  const float inv = __uint_as_float((254u << 23) - eb);  // 2^-e
+  const float q = (v - y) * inv * 32768.0f;
+  return (int8_t)(int)rintf(fminf(fmaxf(q, -127.0f), 127.0f));
+}
+
+template <bool SKIP, bool RELU, bool MASK, bool RIN, bool ROUT>
 __global__ __launch_bounds__(BN_THREADS) void bn_apply_kernel(const bf16* __restrict__ X, const bf16* __restrict__ S,
                                                                bf16* __restrict__ Y, int64_t rows, int C, int CH,
                                                                int64_t rows_per_blk, const float* __restrict__ coef,
-                                                               uint8_t* __restrict__ M) {
+                                                               uint8_t* __restrict__ M, const int8_t* __restrict__ SR,
+                                                               int8_t* __restrict__ YR) {
   const BnGeom g = bn_geom(CH, rows, rows_per_blk);
   if (g.rs >= g.rpi) return;
   float sc[8], sh[8];
@@ -221,18 +241,30 @@ __global__ __launch_bounds__(BN_THREADS) void bn_apply_kernel(const bf16* __rest
     const bf16x8 x = *(const bf16x8*)(X + o);
     bf16x8 sk;
     if (SKIP) sk = *(const bf16x8*)(S + o);
+    uint2 sr = make_uint2(0u, 0u);
+    if (SKIP && RIN) sr = *(const uint2*)(SR + o);
     bf16x8 y;
     uint32_t bits = 0;
+    uint32_t yr[2] = {0u, 0u};
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float v = fmaf(bf2f(x[e]), sc[e], sh[e]);
-      if (SKIP) v += bf2f(sk[e]);
+      if (SKIP) {
+        const float s = bf2f(sk[e]);
+        v += s;
+        if (RIN) {
+          const int8_t q = (int8_t)(((e < 4 ? sr.x : sr.y) >> (8 * (e & 3))) & 0xffu);
+          v = fmaf((float)q, bn_res_scale(s), v);
+        }
+      }
       if (RELU) v = fmaxf(v, 0.f);
       y[e] = f2bf(v);
       if (MASK) bits |= (bf2f(y[e]) > 0.f ? 1u : 0u) << e;
+      if (ROUT) yr[e >> 2] |= (uint32_t)(uint8_t)bn_res_encode(v, bf2f(y[e])) << (8 * (e & 3));
     }
     *(bf16x8*)(Y + o) = y;
     if (MASK) M[o >> 3] = (uint8_t)bits;
+    if (ROUT) *(uint2*)(YR + o) = make_uint2(yr[0], yr[1]);
   }
 }
 
@@ -392,15 +424,20 @@ void batchnorm_fwd_launch(const BnFwdParams& q, hipStream_t s) {
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, fin, dim3(BN_THREADS), 0, s, part, nparts, q.gsum, q.rows, q.C,
                      q.w, q.b, q.rmean, q.rvar, q.training, q.momentum, q.eps, q.smean, q.sinvstd, q.nbt, coef);
   const bool sk = q.skip != nullptr, mk = q.relu && q.mask != nullptr;
-#define BN_APPLY(SK, RL, MK)                                                                                    \
-  hipLaunchKernelGGL((bn_apply_kernel<SK, RL, MK>), G.grid, dim3(BN_THREADS), 0, s, q.X, q.skip, q.Y, q.rows, q.C, \
-                     G.CH, G.rpb, coef, q.mask)
-  if (sk && mk) BN_APPLY(true, true, true);
-  else if (sk && q.relu) BN_APPLY(true, true, false);
-  else if (sk) BN_APPLY(true, false, false);
-  else if (mk) BN_APPLY(false, true, true);
-  else if (q.relu) BN_APPLY(false, true, false);
-  else BN_APPLY(false, false, false);
+#define BN_APPLY(SK, RL, MK, RI, RO)                                                                           \
+  hipLaunchKernelGGL((bn_apply_kernel<SK, RL, MK, RI, RO>), G.grid, dim3(BN_THREADS), 0, s, q.X, q.skip, q.Y,    \
+                     q.rows, q.C, G.CH, G.rpb, coef, q.mask, q.skip_res, q.y_res)
+  if (q.y_res) {  // the residual stream's producers (capi checks the combinations)
+    if (sk && mk) BN_APPLY(true, true, true, true, true);       // bn3 (train): skip + stream residue
+    else if (sk && q.relu) BN_APPLY(true, true, false, true, true);  // bn3 (eval)
+    else BN_APPLY(false, false, false, false, true);            // the downsample's BatchNorm
+  }
+  else if (sk && mk) BN_APPLY(true, true, true, false, false);
+  else if (sk && q.relu) BN_APPLY(true, true, false, false, false);
+  else if (sk) BN_APPLY(true, false, false, false, false);
+  else if (mk) BN_APPLY(false, true, true, false, false);
+  else if (q.relu) BN_APPLY(false, true, false, false, false);
+  else BN_APPLY(false, false, false, false, false);
 #undef BN_APPLY
 }
 

@@ -594,12 +594,25 @@ static int bn_common(int64_t rows, int64_t C, void* ws, int64_t ws_bytes, const 
   return 0;
 }
 
+// the residual stream's residue (y_res / skip_res): the block output (skip + ReLU, the skip's
+// residue read) or the downsample's BatchNorm (no skip, no ReLU)
+static int bn_res_check(const void* skip, int relu, const void* relu_mask, const void* skip_res, const void* y_res,
+                        const char* who) {
+  if (skip_res && !y_res) return fail("%s: skip_res needs y_res", who);
+  if (!y_res) return 0;
+  if (skip && (!relu || !skip_res)) return fail("%s: y_res with a skip needs relu and skip_res", who);
+  if (!skip && (relu || relu_mask)) return fail("%s: y_res without a skip takes no relu", who);
+  return 0;
+}
+
 int mmu_batchnorm_fwd(const void* X, const void* skip, void* Y, int64_t rows, int64_t C, const float* weight,
                       const float* bias, float* running_mean, float* running_var, int64_t* num_batches_tracked,
                       int training, float momentum, float eps, int relu, float* save_mean, float* save_invstd,
-                      void* relu_mask, void* ws, int64_t ws_bytes, mmu_stream_t stream) {
+                      void* relu_mask, const void* skip_res, void* y_res, void* ws, int64_t ws_bytes,
+                      mmu_stream_t stream) {
   if (!X || !Y) return fail("mmu_batchnorm_fwd: null pointer");
   if (relu_mask && !relu) return fail("mmu_batchnorm_fwd: relu_mask needs relu");
+  if (bn_res_check(skip, relu, relu_mask, skip_res, y_res, "mmu_batchnorm_fwd")) return 1;
   if (bn_common(rows, C, ws, ws_bytes, "mmu_batchnorm_fwd")) return 1;
   if ((running_mean == nullptr) != (running_var == nullptr))
     return fail("mmu_batchnorm_fwd: running_mean / running_var must both be given or NULL");
@@ -612,6 +625,7 @@ int mmu_batchnorm_fwd(const void* X, const void* skip, void* Y, int64_t rows, in
   q.w = weight; q.b = bias; q.rmean = running_mean; q.rvar = running_var; q.nbt = num_batches_tracked;
   q.training = training; q.relu = relu; q.momentum = momentum; q.eps = eps;
   q.smean = save_mean; q.sinvstd = save_invstd; q.ws = ws; q.mask = (uint8_t*)relu_mask;
+  q.skip_res = (const int8_t*)skip_res; q.y_res = (int8_t*)y_res;
   batchnorm_fwd_launch(q, (hipStream_t)stream);
   return check_launch("mmu_batchnorm_fwd");
 }
@@ -643,9 +657,11 @@ int mmu_batchnorm_stats(const void* X, int64_t rows, int64_t C, double* sums, vo
 int mmu_batchnorm_fwd_sums(const void* X, const void* skip, void* Y, int64_t rows, int64_t C, const double* sums,
                            const float* weight, const float* bias, float* running_mean, float* running_var,
                            int64_t* num_batches_tracked, float momentum, float eps, int relu, float* save_mean,
-                           float* save_invstd, void* relu_mask, void* ws, int64_t ws_bytes, mmu_stream_t stream) {
+                           float* save_invstd, void* relu_mask, const void* skip_res, void* y_res, void* ws,
+                           int64_t ws_bytes, mmu_stream_t stream) {
   if (!X || !Y || !sums) return fail("mmu_batchnorm_fwd_sums: null pointer");
   if (relu_mask && !relu) return fail("mmu_batchnorm_fwd_sums: relu_mask needs relu");
+  if (bn_res_check(skip, relu, relu_mask, skip_res, y_res, "mmu_batchnorm_fwd_sums")) return 1;
   if (bn_common(rows, C, ws, ws_bytes, "mmu_batchnorm_fwd_sums")) return 1;
   if ((running_mean == nullptr) != (running_var == nullptr))
     return fail("mmu_batchnorm_fwd_sums: running_mean / running_var must both be given or NULL");
@@ -656,6 +672,7 @@ int mmu_batchnorm_fwd_sums(const void* X, const void* skip, void* Y, int64_t row
   q.w = weight; q.b = bias; q.rmean = running_mean; q.rvar = running_var; q.nbt = num_batches_tracked;
   q.training = 1; q.relu = relu; q.momentum = momentum; q.eps = eps;
   q.smean = save_mean; q.sinvstd = save_invstd; q.ws = ws; q.mask = (uint8_t*)relu_mask; q.gsum = sums;
+  q.skip_res = (const int8_t*)skip_res; q.y_res = (int8_t*)y_res;
   batchnorm_fwd_launch(q, (hipStream_t)stream);
   return check_launch("mmu_batchnorm_fwd_sums");
 }
@@ -691,16 +708,17 @@ int mmu_batchnorm_bwd_sums(const void* dY, const void* Y, const void* relu_mask,
 
 int mmu_bertadam_step(float* params, const float* grads, float* m, float* v, void* bf16_copy, const int64_t* table,
                       int32_t* steps, int64_t n_tensors, int64_t n_chunks, float lr_decay, float lr_nodecay, float wd,
-                      float warmup, float t_total, float b1, float b2, float eps, float max_grad_norm, float* ws,
-                      int64_t ws_floats, mmu_stream_t stream) {
+                      float warmup, float t_total, float b1, float b2, float eps, float max_grad_norm,
+                      float grad_scale, float* ws, int64_t ws_floats, mmu_stream_t stream) {
   if (!params || !grads || !m || !v || !table || !steps || !ws) return fail("mmu_bertadam_step: null pointer");
   if (n_tensors <= 0 || n_chunks <= 0) return fail("mmu_bertadam_step: empty table");
   if (ws_floats < n_chunks + 2 * n_tensors) return fail("mmu_bertadam_step: workspace too small");
+  if (!(grad_scale > 0.f)) return fail("mmu_bertadam_step: grad_scale must be > 0");
   AdamParams p{};
   p.params = params; p.grads = grads; p.m = m; p.v = v; p.bf16_copy = (bf16*)bf16_copy; p.table = table;
   p.steps = steps; p.n_tensors = n_tensors; p.total = n_chunks; p.lr_decay = lr_decay; p.lr_nodecay = lr_nodecay;
   p.wd = wd; p.warmup = warmup; p.t_total = t_total; p.b1 = b1; p.b2 = b2; p.eps = eps;
-  p.max_grad_norm = max_grad_norm; p.ws = ws; p.ws_floats = ws_floats;
+  p.max_grad_norm = max_grad_norm; p.grad_scale = grad_scale; p.ws = ws; p.ws_floats = ws_floats;
   const char* e = nullptr;
   if (bertadam_launch(p, (hipStream_t)stream, &e)) return fail("mmu_bertadam_step: %s", e ? e : "failed");
   return check_launch("mmu_bertadam_step");

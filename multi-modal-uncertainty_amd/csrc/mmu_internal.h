@@ -152,7 +152,7 @@ struct AdamParams {
   const int64_t* table;
   int32_t* steps;
   int64_t n_tensors, total;
-  float lr_decay, lr_nodecay, wd, warmup, t_total, b1, b2, eps, max_grad_norm;
+  float lr_decay, lr_nodecay, wd, warmup, t_total, b1, b2, eps, max_grad_norm, grad_scale;
   float* ws;
   int64_t ws_floats;
 };
@@ -171,6 +171,8 @@ struct BnFwdParams {
   int64_t* nbt;
   void* ws;
   uint8_t* mask;  // optional ReLU mask out ([rows][C/8] bytes, bit = Y > 0)
+  const int8_t* skip_res;  // the residual stream's 8-bit residue of skip (with y_res only)
+  int8_t* y_res;           // write Y's 8-bit residue (the block output / the downsample's output)
   double* lsum;        // cross-rank statistics: write the local sums {s1[C], s2[C], rows} and stop
   const double* gsum;  // cross-rank statistics: finalize + apply from the exchanged sums
 };

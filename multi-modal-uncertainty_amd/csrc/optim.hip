@@ -6,7 +6,7 @@
 // step / t_total) with the step read BEFORE its increment.  Three launches over the
 // flat f32 parameter / gradient / moment buffers (HBM-bound, ~28 B per element):
 //   1. per-chunk sum of squares of the gradient
-//   2. per tensor: norm -> clip coefficient, scheduled lr, step += 1
+//   2. per tensor: norm -> clip coefficient (x grad_scale), scheduled lr, step += 1
 //   3. per chunk: moment + parameter update, optional bf16 weight copy for the GEMMs
 // Tensor table (7 int64 each): offset, numel, group, bf16_offset, active,
 // first_chunk, n_chunks.  Chunk table (3 int64 each): tensor, start, len.
@@ -23,7 +23,7 @@ struct AdamDev {
   const int64_t* chunks;
   int32_t* steps;
   int64_t n_tensors, n_chunks;
-  float lr_decay, lr_nodecay, wd, warmup, t_total, b1, b2, eps, max_grad_norm;
+  float lr_decay, lr_nodecay, wd, warmup, t_total, b1, b2, eps, max_grad_norm, grad_scale;
   float* ws;  // [n_chunks] partial sq-norms, then [n_tensors][2] (coef, lr_eff)
 };
 
@@ -61,12 +61,15 @@ __global__ void adam_coef_kernel(AdamDev a) {
   if (!T[4]) { out[0] = 1.f; out[1] = 0.f; return; }
   double sq = 0.0;
   for (int64_t c = T[5]; c < T[5] + T[6]; ++c) sq += a.ws[c];
-  const double nrm = sqrt(sq);
+  // the optimizer's gradient is grads * grad_scale (data parallelism's 1/world): its norm
+  // scales with it, and the update multiplies by grad_scale * clip coefficient
+  const double nrm = sqrt(sq) * (double)a.grad_scale;
   double coef = 1.0;
   if (a.max_grad_norm > 0.f) {
     const double cc = a.max_grad_norm / (nrm + 1e-6);
     if (cc < 1.0) coef = cc;
   }
+  coef *= (double)a.grad_scale;
   const int32_t st = a.steps[t];
   double sched = 1.0;
   if (a.t_total > 0.f) {
@@ -138,6 +141,7 @@ int bertadam_launch(const AdamParams& P, hipStream_t s, const char** err) {
   a.n_chunks = P.total;
   a.lr_decay = P.lr_decay; a.lr_nodecay = P.lr_nodecay; a.wd = P.wd; a.warmup = P.warmup;
   a.t_total = P.t_total; a.b1 = P.b1; a.b2 = P.b2; a.eps = P.eps; a.max_grad_norm = P.max_grad_norm;
+  a.grad_scale = P.grad_scale;
   a.ws = P.ws;
   hipLaunchKernelGGL(adam_sqnorm_kernel, dim3((unsigned)a.n_chunks), dim3(256), 0, s, a);
   hipLaunchKernelGGL(adam_coef_kernel, dim3((unsigned)((a.n_tensors + 255) / 256)), dim3(256), 0, s, a);

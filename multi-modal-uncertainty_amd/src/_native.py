@@ -74,18 +74,18 @@ SIGNATURES = {
     "mmu_stem_conv_wgrad": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp]),
     "mmu_batchnorm_ws_bytes": (c_i64, [c_i64]),
     "mmu_batchnorm_fwd": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_f32,
-                                  c_f32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+                                  c_f32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "mmu_batchnorm_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp,
                                   c_vp, c_vp, c_vp, c_i64, c_vp]),
     "mmu_batchnorm_stats": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "mmu_batchnorm_fwd_sums": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32,
-                                       c_f32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+                                       c_f32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "mmu_batchnorm_bwd_reduce": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp,
                                          c_vp, c_i64, c_vp]),
     "mmu_batchnorm_bwd_sums": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp,
                                        c_vp, c_vp, c_i64, c_vp]),
     "mmu_bertadam_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32,
-                                  c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_i64, c_vp]),
+                                  c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_i64, c_vp]),
     "mmu_uncertainty": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mmu_ece_bins": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "mmu_timing_enable": (c_i32, [c_i32]),

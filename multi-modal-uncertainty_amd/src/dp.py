@@ -15,6 +15,11 @@ overlaps the backward of the layers below.  ``finish()`` issues what is left and
 makes the compute stream wait before the optimizer step.  Mean = sum / world size
 (the per-rank loss is a per-rank mean over equal per-rank batches).
 
+``optimizer`` (a src.optim.BertAdam): ``finish()`` leaves the rank SUM in the gradient store and
+sets the optimizer's ``grad_scale`` to 1/world for its next step, whose fused kernel folds the
+mean into the clip coefficient -- no separate pass over the 677 MB f32 gradient buffer.
+Without it ``finish()`` divides the store in place (the gradients read as the mean).
+
 ``reduce_dtype=torch.bfloat16`` all-reduces a bf16 copy of each bucket (half the xGMI
 bytes; every averaged gradient rounded to 8 significant bits before BertAdam) and casts the
 sum back into the f32 store at ``finish()``; the default keeps the f32 buckets
@@ -27,8 +32,9 @@ from . import kernels as K
 
 
 class GradBucketer:
-    def __init__(self, model, bucket_bytes=64 << 20, group=None, reduce_dtype=torch.float32):
+    def __init__(self, model, bucket_bytes=64 << 20, group=None, reduce_dtype=torch.float32, optimizer=None):
         self.model = model
+        self.optimizer = optimizer
         self.reduce_dtype = reduce_dtype
         self._lowp = {}  # bucket -> low-precision copy being all-reduced
         self.enc = model.enc
@@ -197,10 +203,16 @@ class GradBucketer:
             self._issue(b)
         for w in self.pending:
             w.wait()
+        cur = torch.cuda.current_stream(self.store.grad.device) if self.store.grad.is_cuda else None
         for b, buf in self._lowp.items():
             bk = self.buckets[b]
             self.store.grad[bk["start"]:bk["end"]].copy_(buf)
-        self.store.grad.mul_(1.0 / self.world)
+            if cur is not None:  # (allocated on the side stream, read here: keep it until this copy ran)
+                buf.record_stream(cur)
+        if self.optimizer is not None and hasattr(self.optimizer, "grad_scale"):
+            self.optimizer.grad_scale = 1.0 / self.world
+        else:
+            self.store.grad.mul_(1.0 / self.world)
         self.pending, self.launched, self.done_layers, self.done_segs = [], set(), set(), set()
         self._lowp = {}
 

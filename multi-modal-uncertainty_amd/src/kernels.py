@@ -501,24 +501,34 @@ def _bn_map_check(name, X, *ts):
             raise N.NativeError(f"{name}: maps must be bf16 (got {t.dtype} {tuple(t.shape)})")
 
 
+def _bn_res_check(name, X, *ts):
+    for t in ts:
+        if t is not None and (t.dtype != torch.int8 or t.numel() != X.numel() or not t.is_contiguous()):
+            raise N.NativeError(f"{name}: a stream residue must be a contiguous int8 tensor of X's size")
+
+
 def batchnorm_fwd(X, Y, weight, bias, running_mean, running_var, training, momentum, eps, relu=False, skip=None,
-                  num_batches_tracked=None, save_mean=None, save_invstd=None, relu_mask=None):
+                  num_batches_tracked=None, save_mean=None, save_invstd=None, relu_mask=None, skip_res=None,
+                  y_res=None):
     """X, Y, skip: channels-last bf16 [N, C, H, W] (contiguous as [N*H*W, C]).  relu_mask
-    (optional, relu only): uint8 [N*H*W*C/8] written with the bits Y > 0 for batchnorm_bwd."""
+    (optional, relu only): uint8 [N*H*W*C/8] written with the bits Y > 0 for batchnorm_bwd.
+    y_res / skip_res (optional, int8 of X's size): the residual stream's 8-bit residue of Y /
+    of skip (include/mmu.h)."""
     _dev_check(X, Y)
     _want(X, torch.bfloat16, "batchnorm X")
     _bn_mask_check(relu_mask, X, "batchnorm_fwd")
     C = X.shape[1]
     _bn_vec_check("batchnorm_fwd", C, weight, bias, running_mean, running_var, save_mean, save_invstd)
     _bn_map_check("batchnorm_fwd", X, Y, skip)
+    _bn_res_check("batchnorm_fwd", X, skip_res, y_res)
     if num_batches_tracked is not None and num_batches_tracked.dtype != torch.int64:
         raise N.NativeError("batchnorm_fwd: num_batches_tracked must be int64")
     rows = X.numel() // C
     ws = _bn_workspace(X.device)
     N.call("mmu_batchnorm_fwd", _ptr(X), _ptr(skip), _ptr(Y), rows, C, _ptr(weight), _ptr(bias), _ptr(running_mean),
            _ptr(running_var), _ptr(num_batches_tracked), int(bool(training)), float(momentum), float(eps),
-           int(bool(relu)), _ptr(save_mean), _ptr(save_invstd), _ptr(relu_mask), _ptr(ws), ws.numel() * 4,
-           _stream(X))
+           int(bool(relu)), _ptr(save_mean), _ptr(save_invstd), _ptr(relu_mask), _ptr(skip_res), _ptr(y_res),
+           _ptr(ws), ws.numel() * 4, _stream(X))
 
 
 def batchnorm_bwd(dY, Y, X, weight, save_mean, save_invstd, relu, dX, dSkip=None, dweight=None, dbias=None,
@@ -554,7 +564,8 @@ def batchnorm_stats(X, sums):
 
 
 def batchnorm_fwd_sums(X, Y, sums, weight, bias, running_mean, running_var, momentum, eps, relu=False, skip=None,
-                       num_batches_tracked=None, save_mean=None, save_invstd=None, relu_mask=None):
+                       num_batches_tracked=None, save_mean=None, save_invstd=None, relu_mask=None, skip_res=None,
+                       y_res=None):
     """cross-rank BatchNorm, forward second half: batchnorm_fwd (training) with the statistics
     of the exchanged sums"""
     _dev_check(X, Y, sums)
@@ -564,13 +575,14 @@ def batchnorm_fwd_sums(X, Y, sums, weight, bias, running_mean, running_var, mome
     _bn_sums_check("batchnorm_fwd_sums", sums, C)
     _bn_vec_check("batchnorm_fwd_sums", C, weight, bias, running_mean, running_var, save_mean, save_invstd)
     _bn_map_check("batchnorm_fwd_sums", X, Y, skip)
+    _bn_res_check("batchnorm_fwd_sums", X, skip_res, y_res)
     if num_batches_tracked is not None and num_batches_tracked.dtype != torch.int64:
         raise N.NativeError("batchnorm_fwd_sums: num_batches_tracked must be int64")
     ws = _bn_workspace(X.device)
     N.call("mmu_batchnorm_fwd_sums", _ptr(X), _ptr(skip), _ptr(Y), X.numel() // C, C, _ptr(sums), _ptr(weight),
            _ptr(bias), _ptr(running_mean), _ptr(running_var), _ptr(num_batches_tracked), float(momentum), float(eps),
-           int(bool(relu)), _ptr(save_mean), _ptr(save_invstd), _ptr(relu_mask), _ptr(ws), ws.numel() * 4,
-           _stream(X))
+           int(bool(relu)), _ptr(save_mean), _ptr(save_invstd), _ptr(relu_mask), _ptr(skip_res), _ptr(y_res),
+           _ptr(ws), ws.numel() * 4, _stream(X))
 
 
 def batchnorm_bwd_reduce(dY, Y, X, save_mean, save_invstd, relu, sums, dweight=None, dbias=None, relu_mask=None):
@@ -610,12 +622,12 @@ def _bn_sums_check(who, sums, C):
 
 
 def bertadam_step(params, grads, m, v, bf16_copy, table, steps, n_tensors, n_chunks, lr_decay, lr_nodecay, wd,
-                  warmup, t_total, b1, b2, eps, max_grad_norm, ws):
+                  warmup, t_total, b1, b2, eps, max_grad_norm, ws, grad_scale=1.0):
     _dev_check(params, grads, m, v, table, steps, ws)
     N.call("mmu_bertadam_step", _ptr(params), _ptr(grads), _ptr(m), _ptr(v), _ptr(bf16_copy), _ptr(table),
            _ptr(steps), n_tensors, n_chunks, float(lr_decay), float(lr_nodecay), float(wd), float(warmup),
-           float(t_total), float(b1), float(b2), float(eps), float(max_grad_norm), _ptr(ws), ws.numel(),
-           _stream(params))
+           float(t_total), float(b1), float(b2), float(eps), float(max_grad_norm), float(grad_scale), _ptr(ws),
+           ws.numel(), _stream(params))
 
 
 def uncertainty(logits, y, p_bar, nll, conf, correct):

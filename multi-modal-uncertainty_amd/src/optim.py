@@ -49,6 +49,10 @@ class BertAdam(torch.optim.Optimizer):
         self._fused = None
         self._fused_key = None
         self._host_steps_valid = True
+        # factor on the gradients of the NEXT step only (then back to 1): data parallelism's
+        # 1/world, set by dp.GradBucketer.finish() instead of scaling the summed gradients in a
+        # separate pass (the fused kernel folds it into the clip coefficient)
+        self.grad_scale = 1.0
 
     # ------------------------------------------------------------------ fused path setup
     def _find_store(self):
@@ -168,7 +172,8 @@ class BertAdam(torch.optim.Optimizer):
         t_total = g0["t_total"] if g0["t_total"] is not None else -1
         K.bertadam_step(st.flat, st.grad, f["m"], f["v"], st.compute, f["table"], f["steps"], len(f["names"]),
                         f["n_chunks"], lr_decay, lr_nodecay, wd, g0["warmup"], t_total, g0["b1"], g0["b2"], g0["e"],
-                        g0["max_grad_norm"], f["ws"])
+                        g0["max_grad_norm"], f["ws"], grad_scale=self.grad_scale)
+        self.grad_scale = 1.0
         st.sync_transposed()  # the K-major bf16 weight copies the data-gradient GEMMs read
         self._host_steps_valid = False
 
@@ -177,7 +182,7 @@ class BertAdam(torch.optim.Optimizer):
             for p in group["params"]:
                 if p.grad is None:
                     continue
-                grad = p.grad
+                grad = p.grad if self.grad_scale == 1.0 else p.grad * self.grad_scale
                 state = self.state[p]
                 if len(state) == 0:
                     state["step"] = 0
@@ -196,6 +201,7 @@ class BertAdam(torch.optim.Optimizer):
                     update = update + group["weight_decay"] * p
                 p.add_(update, alpha=-group["lr"] * _sched(state["step"], group))
                 state["step"] += 1
+        self.grad_scale = 1.0
 
     def zero_grad(self, set_to_none=False):
         self._ensure_fused()

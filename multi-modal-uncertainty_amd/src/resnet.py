@@ -21,6 +21,12 @@ from . import kernels as K
 
 _TORCH_ONLY = [False]
 
+# The residual stream past bf16 (round 5): each Bottleneck's output and its downsample's
+# BatchNorm output carry an 8-bit residue (int8 of the map's size, csrc/batchnorm.hip), kept as
+# the ``_mmu_res`` attribute of the bf16 map; the next bn3 adds it to its skip, so the stream
+# is held to ~2^-15 of its value instead of bf16's 2^-8.  The convs read the bf16 map.
+STREAM_RESIDUE = True
+
 
 class torch_ops_only:
     """Context (ImageEncoder img_precision "torch_bf16", a TEST comparator): every trunk module
@@ -41,7 +47,7 @@ class _BatchNormAct(torch.autograd.Function):
     mmu_batchnorm_fwd / mmu_batchnorm_bwd (batch statistics, running stats updated)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, skip, bn, relu, sink=None):
+    def forward(ctx, x, weight, bias, skip, bn, relu, sink=None, skip_res=None, y_res=None):
         ctx.bias_ref, ctx.sink = bias, sink
         Y = torch.empty_like(x)
         C = x.shape[1]
@@ -49,9 +55,9 @@ class _BatchNormAct(torch.autograd.Function):
         sinv = torch.empty_like(smean)
         # the backward reads the ReLU mask (1 bit per element) instead of Y (16 bits)
         mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device) if relu else None
-        K.batchnorm_fwd(x, Y, weight, bias, bn.running_mean, bn.running_var, True, bn.momentum, bn.eps, relu=relu,
-                        skip=skip, num_batches_tracked=bn.num_batches_tracked, save_mean=smean, save_invstd=sinv,
-                        relu_mask=mask)
+        K.batchnorm_fwd(x, Y, weight, bias, bn.running_mean, bn.running_var, True, _momentum(bn), bn.eps,
+                        relu=relu, skip=skip, num_batches_tracked=bn.num_batches_tracked, save_mean=smean,
+                        save_invstd=sinv, relu_mask=mask, skip_res=skip_res, y_res=y_res)
         ctx.save_for_backward(x, mask, weight, smean, sinv)
         ctx.relu, ctx.has_skip = relu, skip is not None
         return Y
@@ -74,7 +80,15 @@ class _BatchNormAct(torch.autograd.Function):
         rb = db if (want_b and ctx.bias_ref.grad is None) else None
         if ctx.sink is not None and dS is not None:  # conv1's dX GEMM adds it (EPI_ADD_RES)
             ctx.sink.g, dS = dS, None
-        return dX, rw, rb, dS, None, None, None
+        return dX, rw, rb, dS, None, None, None, None, None
+
+
+def _momentum(bn):
+    """the running-statistics factor of this training pass: bn.momentum, or for momentum=None
+    (torch's cumulative moving average) 1 / num_batches_tracked after this pass's increment"""
+    if bn.momentum is not None:
+        return float(bn.momentum)
+    return 1.0 / float(int(bn.num_batches_tracked) + 1)
 
 
 class _SyncBatchNormAct(torch.autograd.Function):
@@ -88,7 +102,7 @@ class _SyncBatchNormAct(torch.autograd.Function):
     arithmetic in torch ops."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, skip, bn, relu, sink, group, hip):
+    def forward(ctx, x, weight, bias, skip, bn, relu, sink, group, hip, skip_res=None, y_res=None):
         import torch.distributed as dist
         ctx.bias_ref, ctx.sink, ctx.group, ctx.hip = bias, sink, group, hip
         ctx.relu, ctx.has_skip = relu, skip is not None
@@ -101,9 +115,9 @@ class _SyncBatchNormAct(torch.autograd.Function):
             smean = torch.empty(C, dtype=torch.float32, device=x.device)
             sinv = torch.empty_like(smean)
             mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device) if relu else None
-            K.batchnorm_fwd_sums(x, Y, sums, weight, bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps,
+            K.batchnorm_fwd_sums(x, Y, sums, weight, bias, bn.running_mean, bn.running_var, _momentum(bn), bn.eps,
                                  relu=relu, skip=skip, num_batches_tracked=bn.num_batches_tracked, save_mean=smean,
-                                 save_invstd=sinv, relu_mask=mask)
+                                 save_invstd=sinv, relu_mask=mask, skip_res=skip_res, y_res=y_res)
             ctx.save_for_backward(x, mask, weight, smean, sinv)
             return Y
         xd = x.double()
@@ -116,7 +130,7 @@ class _SyncBatchNormAct(torch.autograd.Function):
         invstd = (var + bn.eps).rsqrt()
         if bn.running_mean is not None:
             with torch.no_grad():
-                m = bn.momentum
+                m = _momentum(bn)
                 bn.running_mean.mul_(1 - m).add_(m * mean.to(bn.running_mean.dtype))
                 bn.running_var.mul_(1 - m).add_(m * (var * n / (n - 1)).to(bn.running_var.dtype))
                 bn.num_batches_tracked.add_(1)
@@ -167,7 +181,7 @@ class _SyncBatchNormAct(torch.autograd.Function):
             dS = g if ctx.has_skip and ctx.needs_input_grad[3] else None
         if ctx.sink is not None and dS is not None:  # conv1's dX GEMM adds it (EPI_ADD_RES)
             ctx.sink.g, dS = dS, None
-        return dX, rw, rb, dS, None, None, None, None, None
+        return dX, rw, rb, dS, None, None, None, None, None, None, None
 
 
 class BatchNorm2d(nn.BatchNorm2d):
@@ -182,33 +196,41 @@ class BatchNorm2d(nn.BatchNorm2d):
     MIOPEN_MIN_BATCH = 8
     sync_group = None  # a process group: training statistics over all its ranks' batches (src/dp.py)
 
-    def forward(self, x, skip=None, relu=None, skip_sink=None):
+    def forward(self, x, skip=None, relu=None, skip_sink=None, out_res=False):
+        """``out_res``: this BN produces the residual stream (a Bottleneck's bn3, a downsample's
+        BN): on the HIP path its output carries the 8-bit stream residue (``_mmu_res``,
+        STREAM_RESIDUE), and a skip's own residue is read."""
         relu = self.fused_relu if relu is None else relu
         # (the kernels take f32 per-channel parameters / statistics: a module cast to bf16 --
         # module.to(torch.bfloat16) -- takes the torch path)
         hip = (not _TORCH_ONLY[0] and x.is_cuda and x.dtype == torch.bfloat16 and (skip is None or skip.dtype == torch.bfloat16)
                and x.shape[1] % 8 == 0 and self.weight is not None and self.weight.dtype == torch.float32
                and (self.running_mean is None or self.running_mean.dtype == torch.float32))
-        if self.sync_group is not None and self.training and self.track_running_stats:
-            if hip:
-                x = x.contiguous(memory_format=torch.channels_last)
-                if skip is not None:
-                    skip = skip.contiguous(memory_format=torch.channels_last)
-            return _SyncBatchNormAct.apply(x, self.weight, self.bias, skip, self, relu, skip_sink, self.sync_group, hip)
+        skip_res = getattr(skip, "_mmu_res", None) if skip is not None else None
+        res = hip and out_res and STREAM_RESIDUE and (skip is None or skip_res is not None)
         if hip:
             x = x.contiguous(memory_format=torch.channels_last)
             if skip is not None:
                 skip = skip.contiguous(memory_format=torch.channels_last)
+        y_res = torch.empty(x.numel(), dtype=torch.int8, device=x.device) if res else None
+        if not res:
+            skip_res = None
+        if self.sync_group is not None and self.training and self.track_running_stats:
+            y = _SyncBatchNormAct.apply(x, self.weight, self.bias, skip, self, relu, skip_sink, self.sync_group, hip,
+                                        skip_res, y_res)
+            return _with_res(y, y_res)
+        if hip:
             if self.training and self.track_running_stats:
-                return _BatchNormAct.apply(x, self.weight, self.bias, skip, self, relu, skip_sink)
+                return _with_res(_BatchNormAct.apply(x, self.weight, self.bias, skip, self, relu, skip_sink, skip_res,
+                                                     y_res), y_res)
             if not self.training and not (torch.is_grad_enabled() and (
                     x.requires_grad or self.weight.requires_grad or (skip is not None and skip.requires_grad))):
                 # the one-pass running-statistics kernel has no backward: a graph through an
                 # eval-mode BN (frozen statistics during training) takes the torch path below
                 Y = torch.empty_like(x)
                 K.batchnorm_fwd(x, Y, self.weight, self.bias, self.running_mean, self.running_var, False,
-                                self.momentum, self.eps, relu=relu, skip=skip)
-                return Y
+                                0.0, self.eps, relu=relu, skip=skip, skip_res=skip_res, y_res=y_res)
+                return _with_res(Y, y_res)
         if self.training or not self.track_running_stats:
             # MIOpen's NHWC batch-norm crashes in host code for tiny batches on this stack
             with torch.backends.cudnn.flags(enabled=x.shape[0] >= self.MIOPEN_MIN_BATCH):
@@ -220,6 +242,12 @@ class BatchNorm2d(nn.BatchNorm2d):
         if skip is not None:
             y = y + skip
         return torch.relu(y) if relu else y
+
+
+def _with_res(y, res):
+    if res is not None:
+        y._mmu_res = res
+    return y
 
 
 def _is_stem(w16, stride, padding):
@@ -608,10 +636,19 @@ class Bottleneck(nn.Module):
                 and x.dtype == torch.bfloat16 and self.conv1.takes_skip_grad(x)):
             x = x.contiguous(memory_format=torch.channels_last)
             sink = _SkipGrad()
-        skip = x if self.downsample is None else self.downsample(x)
+        if self.downsample is None:
+            skip = x
+        elif isinstance(self.downsample, nn.Sequential) and len(self.downsample) == 2 and isinstance(
+                self.downsample[1], BatchNorm2d):
+            skip = self.downsample[1](self.downsample[0](x), out_res=True)
+        else:
+            skip = self.downsample(x)
         y = self.bn1(self.conv1(x, sink=sink), relu=True)
         y = self.bn2(self.conv2(y), relu=True)
-        return self.bn3(self.conv3(y), skip=skip, relu=True, skip_sink=sink)
+        out = self.bn3(self.conv3(y), skip=skip, relu=True, skip_sink=sink, out_res=True)
+        if getattr(skip, "_mmu_res", None) is not None:
+            del skip._mmu_res  # read by this bn3 only: free the residue with the block
+        return out
 
 
 def resnet152_trunk(blocks=(3, 8, 36, 3)):

@@ -205,7 +205,7 @@ def _dp_wrap(model, optimizer, accum, sync_bn=False):
     if sync_bn:
         convert_sync_batchnorm(model)
     sync_buffers_on_eval(model)  # BatchNorm running stats averaged over ranks before eval / checkpoints
-    bucketer = GradBucketer(model)
+    bucketer = GradBucketer(model, optimizer=optimizer)  # 1/world folded into BertAdam's step
     state = {"micro": 0}
 
     def count(mod, inp):
@@ -285,6 +285,8 @@ def main(argv=None):
         if mmbt:
             _dp_wrap(model, optimizer, args.gradient_accumulation_steps, bool(getattr(args, "sync_bn", 0)))
         else:
+            if getattr(args, "sync_bn", 0):
+                raise SystemExit("--sync_bn (whole-batch BatchNorm under DP) is implemented for the MMBT trunk only")
             _dp_wrap_flat(model, optimizer)
         # evaluation sharded over the ranks, sample-weighted sums combined in eval_loop
         valid, test = (shard_eval_loader(dl, world, rank) for dl in (valid, test))

@@ -93,7 +93,7 @@ def gen_mmbt(tag, cfg, B, T, lens, seed=0, wseed=0):
              model.enc.pooler.register_forward_hook(lambda m, i, o: rec.__setitem__("pooled", o.detach()))]
     out = {"text": x[0].numpy(), "segment": x[1].numpy(), "mask": x[2].numpy(), "y": y.numpy(),
            "img_sum": np.float64(x[3].double().sum()), "weight_checksum": np.float64(checksum(sd)),
-           "seed": np.int64(seed), "wseed": np.int64(wseed)}
+           "seed": np.int64(seed), "wseed": np.int64(wseed), "bn_last_gamma": np.float64(cfg.bn_last_gamma)}
     model.eval()
     with torch.no_grad():
         logits = model(*x)
@@ -450,20 +450,24 @@ def gen_framework():
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("--what", default="all", choices=["all", "small", "full", "framework", "flava",
+    ap.add_argument("--what", default="all", choices=["all", "small", "small_b8", "full", "full_c", "framework", "flava",
                                                        "robustness", "fmnist", "a0"])
     a = ap.parse_args()
     sys.path.insert(0, REPO)
-    from oracle.weights import SMALL, FULL
+    from oracle.weights import SMALL, FULL, FULL_C
     # each generator imports the reference fresh with its own stub config -> run each in a subprocess
     if a.what == "all":
         import subprocess
-        for w in ("small", "full", "framework", "flava", "robustness", "fmnist", "a0"):
+        for w in ("small", "small_b8", "full", "full_c", "framework", "flava", "robustness", "fmnist", "a0"):
             subprocess.check_call([sys.executable, "-m", "oracle.gen_golden", "--what", w], cwd=REPO)
     elif a.what == "small":
         gen_mmbt("small_t16", SMALL, B=2, T=16, lens=[16, 9], seed=0)
+    elif a.what == "small_b8":  # batch 8: BatchNorm statistics over 4x the values of the B = 2 fixtures
+        gen_mmbt("small_b8", SMALL, B=8, T=16, lens=[16, 9, 16, 12, 5, 16, 14, 16], seed=2)
     elif a.what == "full":
         gen_mmbt("full_t508", FULL, B=2, T=508, lens=[508, 300], seed=1)
+    elif a.what == "full_c":  # the conditioned trunk recipe (oracle/weights.py FULL_C)
+        gen_mmbt("full_t508c", FULL_C, B=2, T=508, lens=[508, 300], seed=1)
     elif a.what == "flava":
         from oracle.flava_ref import FlavaConfig
         for tag, (kw, B, Li, Lt, seed) in FLAVA_CASES.items():

@@ -46,11 +46,19 @@ class MMBTConfig:
     sep_id: int = 102   # bert-base-uncased "[SEP]"
     ln_eps: float = 1e-12
     bert_std: float = 0.02
+    bn_last_gamma: float = 0.3  # mean of each Bottleneck's bn3 weight (the residual branch's scale)
 
 
 FULL = MMBTConfig()
 # reduced configs keep the per-layer shapes (768/12/3072) so kernels see real widths
 SMALL = MMBTConfig(n_layers=2, vocab=4096, resnet_blocks=(1, 1, 1, 1))
+# The conditioned trunk recipe: residual branches at 0.1 of the stream instead of 0.3.  With
+# 0.3, the 50-block random-init ResNet-152 is a chaotic map: a 1e-4 relative perturbation of
+# the input image moves the fp32 trunk's output by ~1e-2 (tools/trunk_precision.py,
+# tests/test_oracle.py::test_trunk_conditioning), so no bf16 computation can be held to 1e-2
+# of the fp32 reference on it.  At 0.1 the same perturbation moves it by ~7e-4 -- the damped
+# residual branches of a trained network -- and the bf16 product trunk is measurable at 1e-2.
+FULL_C = MMBTConfig(bn_last_gamma=0.1)
 
 
 def _gen(seed, name):
@@ -155,7 +163,7 @@ def _draw(name, shape, kind, seed, cfg):
     elif kind == "bn_w":
         t.normal_(1.0, 0.05, generator=g)
     elif kind == "bn_w_last":
-        t.normal_(0.3, 0.02, generator=g)
+        t.normal_(cfg.bn_last_gamma, 0.02, generator=g)
     elif kind == "bn_b":
         t.normal_(0.0, 0.05, generator=g)
     elif kind == "bn_rm":

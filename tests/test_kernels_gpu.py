@@ -930,6 +930,66 @@ def test_batchnorm_cross_rank_sums_equal_whole_batch(dev, C, skip, relu):
         assert torch.equal(torch.cat(dSs), dS)
 
 
+def _res_decode(hi, res):
+    """value of a bf16 map + its 8-bit stream residue (include/mmu.h mmu_batchnorm_fwd y_res):
+    hi + res * 2^(e - 15), e the binary exponent of hi (0 for hi == 0)"""
+    h = hi.float()
+    m, ex = torch.frexp(h)
+    scale = torch.where(h == 0, torch.zeros_like(h), torch.ldexp(torch.ones_like(h), ex - 1 - 15))
+    return h + res.view(hi.permute(0, 2, 3, 1).shape).permute(0, 3, 1, 2).float() * scale
+
+
+def _res_encode(v):
+    """the kernel's encoding restated: (bf16(v), rint((v - hi) * 2^15 / 2^e)) as an NHWC int8 map"""
+    hi = v.to(torch.bfloat16)
+    h = hi.float()
+    m, ex = torch.frexp(h)
+    q = torch.round((v - h) * torch.ldexp(torch.ones_like(h), 15 - (ex - 1))).clamp(-127, 127)
+    q = torch.where(h == 0, torch.zeros_like(q), q)
+    return hi.contiguous(memory_format=torch.channels_last), q.to(torch.int8).permute(0, 2, 3, 1).contiguous().view(-1)
+
+
+@pytest.mark.parametrize("training", [True, False])
+def test_batchnorm_stream_residue(dev, training):
+    """The residual stream's 8-bit residue (round 5): bn3 reads its skip as bf16 + residue and
+    writes the block output's residue; the downsample's BN writes its output's.  The decoded
+    stream is held to 2^-14 of the f32 value (bf16 alone: 2^-8), against an f32 torch BN on the
+    same bf16 conv output and the f32 skip; the C-ABI rejects a y_res without skip_res."""
+    k = K()
+    g = torch.Generator(device=dev).manual_seed(11)
+    cl = torch.channels_last
+    N, C, H, W = 3, 256, 7, 5
+    x = (torch.randn(N, C, H, W, generator=g, device=dev) * 2 + 0.3).to(torch.bfloat16).contiguous(memory_format=cl)
+    s32 = torch.randn(N, C, H, W, generator=g, device=dev) * 3
+    s32[:, :, 0, 0] = 0.0  # exact zeros in the stream
+    shi, sres = _res_encode(s32)
+    assert sres.abs().max().item() <= 127
+    assert (_res_decode(shi, sres) - s32).abs().max().item() <= 2.0 ** -15 * s32.abs().max().item()
+    w = torch.rand(C, generator=g, device=dev) + 0.5
+    b = torch.randn(C, generator=g, device=dev) * 0.1
+    rm, rv = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
+    Y, yres = torch.empty_like(x), torch.empty(x.numel(), dtype=torch.int8, device=dev)
+    kw = dict(save_mean=torch.empty(C, device=dev), save_invstd=torch.empty(C, device=dev),
+              relu_mask=torch.empty(x.numel() // 8, dtype=torch.uint8, device=dev)) if training else {}
+    k.batchnorm_fwd(x, Y, w, b, rm.clone(), rv.clone(), training, 0.1, 1e-5, relu=True, skip=shi, skip_res=sres,
+                    y_res=yres, **kw)
+    ref = torch.relu(torch.nn.functional.batch_norm(x.float(), rm, rv, w, b, training=training, eps=1e-5) + s32)
+    got = _res_decode(Y, yres)
+    scale = ref.abs().max().item()
+    err = (got - ref).abs().max().item()
+    err_bf16 = (Y.float() - ref).abs().max().item()
+    assert err <= 2.0 ** -13 * scale, (err, err_bf16, scale)
+    assert err_bf16 > 8 * err  # the residue carries the bits bf16 drops
+    # the downsample's BN: no skip, no ReLU, the output's residue
+    Y2, yres2 = torch.empty_like(x), torch.empty(x.numel(), dtype=torch.int8, device=dev)
+    kw2 = dict(save_mean=torch.empty(C, device=dev), save_invstd=torch.empty(C, device=dev)) if training else {}
+    k.batchnorm_fwd(x, Y2, w, b, rm.clone(), rv.clone(), training, 0.1, 1e-5, y_res=yres2, **kw2)
+    ref2 = torch.nn.functional.batch_norm(x.float(), rm, rv, w, b, training=training, eps=1e-5)
+    assert (_res_decode(Y2, yres2) - ref2).abs().max().item() <= 2.0 ** -13 * ref2.abs().max().item()
+    with pytest.raises(Exception, match="skip_res"):
+        k.batchnorm_fwd(x, Y, w, b, rm.clone(), rv.clone(), training, 0.1, 1e-5, relu=True, skip=shi, y_res=yres, **kw)
+
+
 def test_batchnorm_eval_and_module(dev):
     """the module path (train, then eval from the updated running statistics) against
     torch.nn.BatchNorm2d in f32 on the same bf16 inputs, with the fused residual + ReLU"""

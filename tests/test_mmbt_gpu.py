@@ -24,11 +24,13 @@ def tol_check(got, ref, rel=1e-2, abs_=0.0, what=""):
     return err
 
 
-def build(cfgname, dev, **over):
+def build(cfgname, dev, cfg=None, **over):
+    """the model + the seeded state dict (oracle/weights.py recipe ``cfg``, default SMALL / FULL)"""
     from oracle.weights import SMALL, FULL, make_state_dict
     from src.mmbt import MultimodalBertClf
     from src.testing import small_args, make_args
-    cfg = SMALL if cfgname == "small" else FULL
+    if cfg is None:
+        cfg = SMALL if cfgname == "small" else FULL
     over.setdefault("img_precision", "fp32")
     args = (small_args if cfgname == "small" else make_args)(**over)
     torch.manual_seed(0)
@@ -82,22 +84,37 @@ def test_forward_control_draws_reference_indices(dev, small):
 
 
 GRAD_REL = 1e-2  # north star: 1e-2 for bf16
-NOISE_X = 2.0    # a bf16-trunk-borne error (projection bias, eval logits) up to NOISE_X x PyTorch's bf16 trunk's
-MEDIAN_X = 3.5   # trunk gradients: median over the trunk tensors <= MEDIAN_X x torch's (small model: 2.3-2.9x)
-TAIL_X = 2.5     # ... their 90th percentile and maximum <= TAIL_X x torch's (measured 0.9-1.9x)
+# Bars of the bf16 product trunk's gradients (fixed before the round-5 runs): over
+# the trunk tensors above the floor, the median grad-norm error <= TRUNK_MEDIAN and every
+# tensor <= TRUNK_MAX (a BatchNorm bias gradient is a sum over the batch whose terms largely
+# cancel, so single tensors sit at a few 1e-2 in any bf16 trunk: tools/trunk_precision.py)
+TRUNK_MEDIAN = 1e-2
+TRUNK_MAX = 0.1
+# fixtures whose fp32 trunk is chaotic (tests/test_oracle.py::test_trunk_conditioning_of_the_
+# fixture_recipes): the bf16 trunk is compared there as a printed diagnostic only
+CHAOTIC = ("full_t508",)
+
+
+def fixture(tag):
+    from test_oracle import fixture_cfg
+    g = np.load(os.path.join(GOLD, f"mmbt_{tag}.npz"))
+    return g, fixture_cfg(tag, g)
 
 
 def _golden_batch(g, cfg, dev):
     from src.testing import synthetic_batch
     x = tuple(torch.from_numpy(g[k]).to(dev) for k in ("text", "segment", "mask"))
-    (_, _, _, img), _ = synthetic_batch(2, g["text"].shape[1], vocab=cfg.vocab, lens=None, seed=int(g["seed"]))
+    B, T = g["text"].shape
+    (_, _, _, img), _ = synthetic_batch(B, T, vocab=cfg.vocab, lens=None, seed=int(g["seed"]))
     assert abs(float(img.double().sum()) - float(g["img_sum"])) < 1e-3
     return x + (img.to(dev),), torch.from_numpy(g["y"]).to(dev)
 
 
-def _train_step(cfgname, g, dev, prec):
+def _train_step(cfgname, g, dev, prec, cfg=None):
     """one train-mode forward + backward (BERT dropout 0) -> loss, {name: grad norm}, clf grad, proj bias grad"""
-    model, sd, cfg = build(cfgname, dev, bert_hidden_dropout=0.0, bert_attn_dropout=0.0, img_precision=prec)
+    model, sd, cfg = build(cfgname, dev, cfg, bert_hidden_dropout=0.0, bert_attn_dropout=0.0, img_precision=prec)
+    from oracle.weights import checksum
+    assert abs(checksum(sd) - float(g["weight_checksum"])) < 1e-6 * float(g["weight_checksum"])
     x, y = _golden_batch(g, cfg, dev)
     model.train()
     model.store.zero_grad()
@@ -116,75 +133,70 @@ def _rel(a, b):
     return abs(a - b) / max(abs(b), 1e-30)
 
 
+def _trunk_summary(rows):
+    e = np.array([r[1] for r in rows if "img_encoder" in r[0]])
+    return {"median": float(np.median(e)), "p90": float(np.quantile(e, 0.9)), "max": float(e.max()),
+            "n_above_1e-2": int((e > GRAD_REL).sum()), "n": len(e)}
+
+
 @pytest.mark.parametrize("tag,cfgname,prec", [("small_t16", "small", "fp32"), ("small_t16", "small", "bf16"),
-                                              ("full_t508", "full", "fp32"), ("full_t508", "full", "bf16")])
+                                              ("small_b8", "small", "bf16"), ("full_t508", "full", "fp32"),
+                                              ("full_t508c", "full", "fp32"), ("full_t508c", "full", "bf16"),
+                                              ("full_t508", "full", "bf16")])
 def test_train_step_grads_match_reference_golden(dev, tag, cfgname, prec):
     """Train mode (BN batch statistics), BERT dropout 0, against the reference's own train-mode
     loss and per-tensor gradient norms (oracle/gen_golden.py gen_mmbt).  prec "bf16" is the
-    product / bench trunk: HIP stem conv, BatchNorm(+res)(+ReLU), implicit / strided convs,
-    1x1 GEMMs, max-pool, row-pool; "fp32" routes the trunk to torch fp32 convs.  Both run the
-    full ResNet-152 + 12-layer BERT for full_t508.
-    Bar: loss within 1e-2 (relative); every per-tensor gradient norm within 1e-2 (relative)
-    above the noise floor 1e-4 * max norm (key biases have an exactly-zero true gradient:
-    softmax shift invariance; the reference reads ~1e-9, bf16 arithmetic ~1e-5).  With the
-    bf16 trunk, the trunk tensors' gradients pass back through ~150 bf16 layers (batch-2
-    BatchNorm statistics amplify every rounding) and no bf16 implementation holds them to
-    1e-2, so they are held to the noise of PyTorch's own bf16 trunk on the same step
-    (img_precision "torch_bf16": MIOpen bf16 convs + torch BatchNorm) as a DISTRIBUTION --
-    one noisy realisation per tensor on each side makes a per-tensor ratio a coin flip
-    (measured: a tensor at 8.7 % for HIP where torch happened to land at 0.06 %, others the
-    other way round): over the trunk tensors above the floor, the HIP median <= MEDIAN_X x
-    torch's median, the 90th percentile and the maximum <= TAIL_X x torch's, each + 1e-3, and
-    no trunk tensor beyond 1.0 (a wrong sign or a dropped term).  Measured and printed here."""
-    g = np.load(os.path.join(GOLD, f"mmbt_{tag}.npz"))
+    product / bench trunk: HIP stem conv, BatchNorm(+res)(+ReLU) with the residual stream's
+    8-bit residue, implicit / strided convs, 1x1 GEMMs, max-pool, row-pool; "fp32" routes the
+    trunk to torch fp32 convs.  Both run the full ResNet-152 + 12-layer BERT for full_*.
+    Bars: loss within 1e-2 (relative); every non-trunk gradient norm within 1e-2 above the
+    noise floor 1e-4 * max norm (key biases have an exactly-zero true gradient: softmax shift
+    invariance; the reference reads ~1e-9, bf16 arithmetic ~1e-5); the fp32 trunk's tensors
+    within 1e-2 each; the bf16 trunk's tensors median <= TRUNK_MEDIAN and each <= TRUNK_MAX.
+    On a CHAOTIC fixture (full_t508: its fp32 trunk moves 1e-2 for a 1e-4 input perturbation)
+    the bf16 trunk's tensors are printed, with PyTorch's own bf16 trunk beside them, not held."""
+    g, cfg = fixture(tag)
     names = json.load(open(os.path.join(GOLD, f"mmbt_{tag}_keys.json")))["named_parameters"]
     ref = dict(zip(names, (float(v) for v in g["grad_norms"])))
-    loss, norms, clf_g, proj_g = _train_step(cfgname, g, dev, prec)
-    tnorms = tproj_g = None
-    if prec == "bf16":
-        _, tnorms, _, tproj_g = _train_step(cfgname, g, dev, "torch_bf16")
+    loss, norms, clf_g, proj_g = _train_step(cfgname, g, dev, prec, cfg)
+    chaotic = prec == "bf16" and tag in CHAOTIC
     lerr = _rel(loss, float(g["loss_train"]))
     floor = 1e-4 * float(np.max(g["grad_norms"]))
     bad, rows = [], []
     for n in names:
         e = _rel(norms[n], ref[n])
-        bar = GRAD_REL
-        te = None
-        if tnorms is not None and "img_encoder" in n:
-            te = _rel(tnorms[n], ref[n])
-            bar = 1.0  # held as a distribution below
+        trunk = "img_encoder" in n
         if ref[n] > floor:
-            rows.append((n, e, te))
+            rows.append((n, e))
+        bar = (TRUNK_MAX if prec == "bf16" else GRAD_REL) if trunk else GRAD_REL
+        if chaotic and trunk:
+            continue
         if not abs(norms[n] - ref[n]) <= bar * ref[n] + floor:
-            bad.append((n, norms[n], ref[n], e, te))
+            bad.append((n, norms[n], ref[n], e))
     rows.sort(key=lambda r: -r[1])
+    ts = _trunk_summary(rows)
     msg = (f"\n[{tag} {prec}] loss rel err {lerr:.2e}; grad-norm rel err over {len(rows)} tensors above the floor: "
-           f"max {rows[0][1]:.2e} ({rows[0][0]}), median {rows[len(rows) // 2][1]:.2e}")
-    if tnorms is not None:
-        tq = np.array([r[2] for r in rows if r[2] is not None])
-        hq = np.array([r[1] for r in rows if r[2] is not None])
-        q = {k: (float(np.quantile(hq, f)), float(np.quantile(tq, f))) for k, f in (("median", 0.5), ("p90", 0.9),
-                                                                                   ("max", 1.0))}
-        msg += ("; trunk tensors HIP vs torch bf16: " + ", ".join(f"{k} {h:.2e} / {t:.2e}" for k, (h, t) in q.items())
-                + f"; > 1e-2: {int((hq > GRAD_REL).sum())} / {int((tq > GRAD_REL).sum())} of {len(hq)}")
-        assert q["median"][0] <= MEDIAN_X * q["median"][1] + 1e-3, msg
-        assert q["p90"][0] <= TAIL_X * q["p90"][1] + 1e-3, msg
-        assert q["max"][0] <= TAIL_X * q["max"][1] + 1e-3, msg
+           f"max {rows[0][1]:.2e} ({rows[0][0]}), median {rows[len(rows) // 2][1]:.2e}; trunk tensors: median "
+           f"{ts['median']:.2e} p90 {ts['p90']:.2e} max {ts['max']:.2e}, > 1e-2: {ts['n_above_1e-2']} of {ts['n']}")
+    if chaotic:
+        _, tnorms, _, _ = _train_step(cfgname, g, dev, "torch_bf16", cfg)
+        trows = [(n, _rel(tnorms[n], ref[n])) for n, _ in rows]
+        tt = _trunk_summary(trows)
+        msg += (f"; PyTorch's own bf16 trunk (diagnostic): median {tt['median']:.2e} p90 {tt['p90']:.2e} max "
+                f"{tt['max']:.2e}, > 1e-2: {tt['n_above_1e-2']} of {tt['n']}")
     print(msg)
     assert lerr < 1e-2, f"train loss {loss:.6f} vs {float(g['loss_train']):.6f}"
     assert not bad, f"{len(bad)} of {len(names)} grad norms off: worst {sorted(bad, key=lambda r: -r[3])[:5]}"
+    if prec == "bf16" and not chaotic:
+        assert ts["median"] <= TRUNK_MEDIAN, msg
     tol_check(clf_g, g["clf_weight_grad"], rel=1e-2, what="clf grad")
-    # the image projection's bias gradient is the trunk features' gradient summed: it carries
-    # the trunk's noise (bar as for a trunk tensor)
-    ref_p = g["img_proj_bias_grad"]
-    prel = 2e-2
-    if tproj_g is not None:
-        prel = max(prel, NOISE_X * float(np.abs(tproj_g.numpy() - ref_p).max() / np.abs(ref_p).max()))
-    tol_check(proj_g, ref_p, rel=prel, what="img proj bias grad")
+    # the image projection's bias gradient is the trunk features' gradient summed
+    if not chaotic:
+        tol_check(proj_g, g["img_proj_bias_grad"], rel=2e-2, what="img proj bias grad")
 
 
-def _bnfit_logits(cfgname, g, dev, prec):
-    model, sd, cfg = build(cfgname, dev, img_precision=prec, bert_hidden_dropout=0.0, bert_attn_dropout=0.0)
+def _bnfit_logits(cfgname, g, dev, prec, cfg=None):
+    model, sd, cfg = build(cfgname, dev, cfg, img_precision=prec, bert_hidden_dropout=0.0, bert_attn_dropout=0.0)
     x, y = _golden_batch(g, cfg, dev)
     bns = [m for m in model.modules() if isinstance(m, torch.nn.BatchNorm2d)]
     assert bns
@@ -209,27 +221,33 @@ def _bnfit_logits(cfgname, g, dev, prec):
     return {k: v.float().cpu().numpy() for k, v in out.items()}, loss, rm
 
 
-@pytest.mark.parametrize("tag,cfgname", [("small_t16", "small"), ("full_t508", "full")])
-def test_bnfit_eval_variants_bf16_trunk_match_reference_golden(dev, tag, cfgname):
-    """The product-precision (bf16 HIP) trunk in eval mode, on BatchNorm running statistics
-    fitted to the batch (momentum 1, one train-mode pass: the fixture's bnfit_* entries, made
-    the same way by the reference model), so the trunk's activations are normalised: logits of
-    all 5 variants (full, image-only, text-only, both controls).  Bar per variant:
-    max(1e-2, NOISE_X x PyTorch's own bf16 trunk's error) * max|logit| (printed)."""
-    g = np.load(os.path.join(GOLD, f"mmbt_{tag}.npz"))
-    got, loss, rm = _bnfit_logits(cfgname, g, dev, "bf16")
-    tgot, _, _ = _bnfit_logits(cfgname, g, dev, "torch_bf16")
+@pytest.mark.parametrize("tag,cfgname,prec", [("small_t16", "small", "bf16"), ("small_b8", "small", "bf16"),
+                                              ("full_t508c", "full", "bf16"), ("full_t508", "full", "fp32"),
+                                              ("full_t508", "full", "bf16")])
+def test_bnfit_eval_variants_bf16_trunk_match_reference_golden(dev, tag, cfgname, prec):
+    """Eval mode on BatchNorm running statistics fitted to the batch (momentum 1, one
+    train-mode pass: the fixture's bnfit_* entries, made the same way by the reference model),
+    so the trunk's activations are normalised: logits of all 5 variants (full, image-only,
+    text-only, both controls) within 1e-2 * max|logit| (north star, bf16), with the bf16 HIP
+    product trunk -- or, on the chaotic fixture full_t508, with the fp32 trunk (the bf16
+    trunk's errors printed beside PyTorch's own bf16 trunk's, as a diagnostic)."""
+    g, cfg = fixture(tag)
+    got, loss, rm = _bnfit_logits(cfgname, g, dev, prec, cfg)
+    chaotic = prec == "bf16" and tag in CHAOTIC
+    tgot = _bnfit_logits(cfgname, g, dev, "torch_bf16", cfg)[0] if chaotic else None
     assert abs(rm - float(g["bnfit_running_mean_sum"])) <= 2e-2 * abs(float(g["bnfit_running_mean_sum"])) + 1e-2
     errs = {}
     for v in ("full", "img_only", "txt_only", "control_image", "control_text"):
         ref = g[f"bnfit_logits_{v}"]
         scale = np.abs(ref).max()
-        e, te = np.abs(got[v] - ref).max() / scale, np.abs(tgot[v] - ref).max() / scale
-        errs[v] = (e, te)
-    print(f"\n[{tag} bnfit] logits rel err per variant (HIP bf16 trunk, torch bf16 trunk): "
-          + ", ".join(f"{k} {e:.2e} / {te:.2e}" for k, (e, te) in errs.items()))
-    for v, (e, te) in errs.items():
-        assert e <= max(1e-2, NOISE_X * te), f"bnfit {v}: {e:.3e} (torch bf16 trunk {te:.3e})"
+        errs[v] = (np.abs(got[v] - ref).max() / scale,
+                   np.abs(tgot[v] - ref).max() / scale if tgot is not None else float("nan"))
+    print(f"\n[{tag} {prec} bnfit] logits rel err per variant" + (" (HIP bf16 trunk / torch bf16 trunk)" if chaotic else "")
+          + ": " + ", ".join(f"{k} {e:.2e}" + (f" / {te:.2e}" if chaotic else "") for k, (e, te) in errs.items()))
+    if chaotic:
+        return
+    for v, (e, _) in errs.items():
+        assert e <= 1e-2, f"bnfit {v}: {e:.3e}"
     assert abs(loss - float(g["bnfit_loss_eval"])) < 1e-2 * abs(float(g["bnfit_loss_eval"]))
 
 

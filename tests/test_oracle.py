@@ -9,22 +9,32 @@ import torch
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
+def fixture_cfg(tag, g):
+    """the weight recipe a mmbt_<tag> fixture was made with (oracle/weights.py)"""
+    import dataclasses
+    from oracle.weights import SMALL, FULL
+    cfg = SMALL if tag.startswith("small") else FULL
+    if "bn_last_gamma" in g:
+        cfg = dataclasses.replace(cfg, bn_last_gamma=float(g["bn_last_gamma"]))
+    return cfg
+
+
 def _inputs(g, cfg):
     from oracle.gen_golden import make_inputs
-    T = g["text"].shape[1]
+    B, T = g["text"].shape
     lens = g["mask"].sum(1).tolist()
-    x, y = make_inputs(cfg, 2, T, lens, int(g["seed"]))
+    x, y = make_inputs(cfg, B, T, lens, int(g["seed"]))
     assert np.array_equal(x[0].numpy(), g["text"]) and np.array_equal(y.numpy(), g["y"])
     assert abs(float(x[3].double().sum()) - float(g["img_sum"])) < 1e-6 * abs(float(g["img_sum"])) + 1e-6
     return x, y
 
 
-@pytest.mark.parametrize("tag", ["small_t16", "full_t508"])
+@pytest.mark.parametrize("tag", ["small_t16", "small_b8", "full_t508", "full_t508c"])
 def test_oracle_matches_reference_golden(tag):
     from oracle import mmbt_ref as R
-    from oracle.weights import SMALL, FULL, make_state_dict, checksum, key_shapes
-    cfg = SMALL if tag.startswith("small") else FULL
+    from oracle.weights import make_state_dict, checksum, key_shapes
     g = np.load(os.path.join(GOLD, f"mmbt_{tag}.npz"))
+    cfg = fixture_cfg(tag, g)
     keys = json.load(open(os.path.join(GOLD, f"mmbt_{tag}_keys.json")))["state_dict_keys"]
     assert keys == [k for k, *_ in key_shapes(cfg)]
     sd = make_state_dict(int(g["wseed"]), cfg)
@@ -44,6 +54,38 @@ def test_oracle_matches_reference_golden(tag):
         lo, pooled = R.forward(sd, txt, seg, mask, img, cfg, "full", feats=feats, return_pooled=True)
         np.testing.assert_allclose(pooled.numpy(), g["pooled_full"], rtol=1e-4, atol=1e-5)
         assert abs(float(R.cross_entropy(lo, y)) - float(g["loss_eval"])) < 1e-5
+
+
+def _trunk_sensitivity(cfg, eps=1e-4, B=2):
+    """relative RMS change of the fp32 trunk's output map (train mode: batch statistics) when
+    the input image is perturbed by a relative N(0, eps) -- the trunk's condition number x eps"""
+    from oracle import mmbt_ref as R
+    from oracle.weights import make_state_dict
+    sd = make_state_dict(0, cfg)
+    g = torch.Generator().manual_seed(1)
+    img = torch.randn(B, 3, 224, 224, generator=g)
+    noisy = img * (1 + eps * torch.randn(img.shape, generator=g))
+    with torch.no_grad():
+        a = R.resnet_trunk(sd, img, cfg, train=True)
+        b = R.resnet_trunk(sd, noisy, cfg, train=True)
+    return float((a - b).norm() / a.norm())
+
+
+def test_trunk_conditioning_of_the_fixture_recipes():
+    """Why the bf16 product trunk is held to the north star's 1e-2 on mmbt_full_t508c and not on
+    mmbt_full_t508 (tests/test_mmbt_gpu.py): with the round-1 recipe (each Bottleneck's bn3
+    weight ~ N(0.3, 0.02)) the random-init ResNet-152 is chaotic -- a 1e-4 relative perturbation
+    of the input image moves the fp32 trunk's output by ~1e-2 (measured 9.7e-3), so even an fp32
+    trunk fed an image off by 1e-4 misses 1e-2, and bf16's 2^-9 rounding of every stored map
+    cannot meet it.  The conditioned recipe (bn3 ~ N(0.1, 0.02): FULL_C, damped residual branches
+    as in a trained network) moves it by < 1e-3.  The 1-block-per-stage small model is well
+    conditioned under the round-1 recipe."""
+    from oracle.weights import FULL, FULL_C, SMALL
+    chaotic, cond, small = (_trunk_sensitivity(c) for c in (FULL, FULL_C, SMALL))
+    print(f"\nfp32 trunk output change for a 1e-4 input perturbation: full {chaotic:.2e}, full_c {cond:.2e}, "
+          f"small {small:.2e}")
+    assert chaotic > 5e-3
+    assert cond < 1.5e-3 and small < 1e-3
 
 
 def test_oracle_control_indices_follow_reference_rng():

@@ -284,3 +284,45 @@ def test_model_grads_with_side_stream_wgrad(dev, monkeypatch):
     for n in g0:
         err = (g1[n] - g0[n]).abs().max().item()
         assert err <= 1e-5 * g0[n].abs().max().item() + 1e-12, f"{n}: side-stream gradient differs by {err:.3e}"
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_stream_residue_carried_through_the_trunk(dev, monkeypatch, train):
+    """The residual stream's 8-bit residue (resnet.STREAM_RESIDUE, csrc/batchnorm.hip) reaches
+    every Bottleneck: each block output carries ``_mmu_res`` when the block returns (train and
+    eval), the next block frees it, and with it the trunk's output map lies closer to the fp32
+    trunk's than without it (the 4-block small trunk at batch 8: a small but systematic gain;
+    the full model's measured in tests/test_mmbt_gpu.py)."""
+    from oracle.weights import SMALL, make_state_dict
+    from src import resnet as R
+    from src.mmbt import MultimodalBertClf
+    from src.testing import small_args, synthetic_batch
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    (_, _, _, img), _ = synthetic_batch(8, 16, vocab=SMALL.vocab, seed=12)
+    img = img.to(dev)
+    sd = make_state_dict(0, SMALL)
+
+    def trunk(precision, residue):
+        monkeypatch.setattr(R, "STREAM_RESIDUE", residue)
+        torch.manual_seed(0)
+        m = MultimodalBertClf(small_args(img_precision=precision))
+        m.load_state_dict(sd, strict=True)
+        m = m.to(dev).train(train)
+        seen = []
+        blocks = [mod for mod in m.modules() if isinstance(mod, R.Bottleneck)]
+        hooks = [b.register_forward_hook(lambda mod, i, o: seen.append(getattr(o, "_mmu_res", None) is not None))
+                 for b in blocks]
+        with torch.no_grad():
+            out = m.enc.img_encoder.trunk(img).float()
+        for h in hooks:
+            h.remove()
+        return out, seen, len(blocks)
+
+    ref, _, _ = trunk("fp32", True)
+    on, seen_on, nb = trunk("bf16", True)
+    off, seen_off, _ = trunk("bf16", False)
+    assert seen_on == [True] * nb and seen_off == [False] * nb
+    e_on, e_off = _rel(on, ref), _rel(off, ref)
+    print(f"\n[stream residue, train={train}] trunk output rel err vs fp32: with {e_on:.3e}, without {e_off:.3e}")
+    assert not torch.equal(on, off)
+    assert e_on < e_off

@@ -13,7 +13,7 @@ import torch.nn.functional as F
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(HERE, "..", "multi-modal-uncertainty_amd"), os.path.join(HERE, "..")]
 sys.path.insert(0, os.path.join(HERE, "..", "tests"))
-from test_mmbt_gpu import GOLD, _train_step  # noqa: E402
+from test_mmbt_gpu import GOLD, _train_step, fixture  # noqa: E402
 from src import resnet as R  # noqa: E402
 
 
@@ -28,6 +28,7 @@ def torch_bn(x, w, b, skip, bn, relu, sink=None):
 
 VARIANTS = {
     "hip": {},
+    "hip, bf16 stream (no residue)": {"STREAM_RESIDUE": False},
     "hip, convs on MIOpen": {"_mmu_conv": lambda *a: (False, False, False), "_mmu_1x1": lambda *a: (False, False, False)},
     "hip, BN on torch": {"bn": True},
     "hip, stem on MIOpen": {"_is_stem": lambda *a: False},
@@ -35,7 +36,7 @@ VARIANTS = {
 
 
 def run(tag, cfgname, dev="cuda"):
-    g = np.load(os.path.join(GOLD, f"mmbt_{tag}.npz"))
+    g, cfg = fixture(tag)
     names = json.load(open(os.path.join(GOLD, f"mmbt_{tag}_keys.json")))["named_parameters"]
     ref = dict(zip(names, (float(v) for v in g["grad_norms"])))
     floor = 1e-4 * float(np.max(g["grad_norms"]))
@@ -44,7 +45,7 @@ def run(tag, cfgname, dev="cuda"):
     def summ(norms):
         e = np.array([abs(norms[n] - ref[n]) / ref[n] for n in trunk])
         return f"median {np.median(e):.2e}  p90 {np.quantile(e, 0.9):.2e}  max {e.max():.2e}  (>1e-2: {(e > 1e-2).sum()}/{len(e)})"
-    _, tn, _, _ = _train_step(cfgname, g, dev, "torch_bf16")
+    _, tn, _, _ = _train_step(cfgname, g, dev, "torch_bf16", cfg)
     print(f"[{tag}] torch bf16            {summ(tn)}", flush=True)
     for name, patch in VARIANTS.items():
         saved = {}
@@ -56,7 +57,7 @@ def run(tag, cfgname, dev="cuda"):
                 saved[k] = getattr(R, k)
                 setattr(R, k, v)
         try:
-            _, hn, _, _ = _train_step(cfgname, g, dev, "bf16")
+            _, hn, _, _ = _train_step(cfgname, g, dev, "bf16", cfg)
         finally:
             for k, v in saved.items():
                 if k == "bn":
@@ -67,5 +68,5 @@ def run(tag, cfgname, dev="cuda"):
 
 
 if __name__ == "__main__":
-    for tag, cfgname in (("small_t16", "small"), ("full_t508", "full")):
+    for tag, cfgname in (("small_t16", "small"), ("small_b8", "small"), ("full_t508c", "full")):
         run(tag, cfgname)
