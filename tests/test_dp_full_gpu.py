@@ -206,9 +206,14 @@ def _sync_worker(rank, world, port, q):
             torch.cuda.synchronize()
             if keep is None:  # without the key biases: their true gradient is 0 (softmax shift invariance)
                 keep = torch.ones_like(m.store.grad, dtype=torch.bool)
+                trunk = torch.zeros_like(keep)
                 for n in m.store.names:
+                    sl_ = slice(m.store.offsets[n], m.store.offsets[n] + m.store.params[n].numel())
                     if n.endswith("attention.self.key.bias"):
-                        keep[m.store.offsets[n]:m.store.offsets[n] + m.store.params[n].numel()] = False
+                        keep[sl_] = False
+                    if "img_encoder" in n:
+                        trunk[sl_] = True
+                keep = (keep, trunk)
             g = m.store.grad.clone()
             bufs = torch.cat([b.double().flatten() for b in m.buffers() if b.is_floating_point()])
             del m, o
@@ -219,8 +224,9 @@ def _sync_worker(rank, world, port, q):
         g1, b1 = run("bf16", False)
         g2, b2 = run("bf16", True, sync=True)
         g3, _ = run("bf16", True, sync=False)
-        rel = lambda a: ((a - gr)[keep].norm() / gr[keep].norm()).item()  # noqa: E731
-        q.put((rank, rel(g1), rel(g2), rel(g3), ((b2 - b1).norm() / b1.norm()).item()))
+        rel = lambda a, b=gr, k=0: ((a - b)[keep[k]].norm() / b[keep[k]].norm()).item()  # noqa: E731
+        # (the statistics show in the trunk's gradients: compared there, BERT's dominate the whole)
+        q.put((rank, rel(g1), rel(g2), rel(g3, g1, 1), rel(g2, g1, 1), ((b2 - b1).norm() / b1.norm()).item()))
         dist.destroy_process_group()
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
@@ -230,11 +236,13 @@ def _sync_worker(rank, world, port, q):
 def test_dp_full_model_sync_batchnorm_train_mode():
     """Whole-batch BatchNorm under DP on the full trunk (155 BatchNorms exchanging their sums):
     the synchronised 2-rank bf16 step is no further from the exact step than 1.5x the single
-    device's bf16 step; per-rank statistics (no exchange) are >= 2x further; the running
-    statistics equal the single device's (1e-3: statistics of bf16 maps)."""
-    for rank, e1, e2, e3, eb in _spawn(_sync_worker, 2):
+    device's bf16 step; per-rank statistics (no exchange) put the trunk's gradients >= 3x further
+    from the single device's than the synchronised run does; the running statistics equal the
+    single device's (1e-3: statistics of bf16 maps)."""
+    for rank, e1, e2, e3, e2s, eb in _spawn(_sync_worker, 2):
         print(f"\n[dp full sync-bn] rank {rank}: grad rel err vs the exact step: single-device bf16 {e1:.3e}, "
-              f"2-rank whole-batch BN {e2:.3e}, 2-rank per-rank BN {e3:.3e}; running stats {eb:.3e}")
+              f"2-rank whole-batch BN {e2:.3e}; trunk grads vs the single device: whole-batch BN {e2s:.3e}, "
+              f"per-rank BN {e3:.3e}; running stats {eb:.3e}")
         assert e2 <= 1.5 * e1 + 1e-6, (e2, e1)
-        assert e3 >= 2 * e2, (e3, e2)
+        assert e3 >= 3 * e2s, (e3, e2s)
         assert eb <= 1e-3, eb

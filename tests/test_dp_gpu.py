@@ -279,11 +279,11 @@ def _sync_bn_worker(rank, world, port, q, precision):
         _, g3, _, _ = run(True, False)
         if precision == "fp32":
             q.put((rank, rel(g2, g1), rel(d2, d1), ((b2 - b1).norm() / b1.norm()).item(), rel(g3, g1), rel(g0, g1),
-                   rel(d0, d1)))
+                   rel(d0, d1), rel(g2, g1)))
         else:  # the reference step: one device, the fp32 trunk
             _, gr, dr, _ = run(False, False, prec="fp32")
-            q.put((rank, rel(g2, gr), rel(d2, dr), ((b2 - b1).norm() / b1.norm()).item(), rel(g3, gr), rel(g1, gr),
-                   rel(d1, dr)))
+            q.put((rank, rel(g2, gr), rel(d2, dr), ((b2 - b1).norm() / b1.norm()).item(), rel(g3, g1), rel(g1, gr),
+                   rel(d1, dr), rel(g2, g1)))
         dist.destroy_process_group()
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
@@ -308,15 +308,15 @@ def test_dp_sync_batchnorm_two_ranks_equal_single_device_train_mode(precision):
     9.4e-3 of the single device's, round 5), so both are measured against the EXACT step (one
     device, fp32 trunk): the synchronised 2-rank step no further from it than 1.5x the single
     device's bf16 step.  Running statistics within 1e-5 (fp32 trunk) / 1e-3 (statistics of bf16
-    maps); per-rank statistics (no exchange) off by >= 2x more than the synchronised run, so the
-    test sees the statistics.  Measured errors printed."""
+    maps); per-rank statistics (no exchange) off from the single device by >= 3x more than the
+    synchronised run, so the test sees the statistics.  Measured errors printed."""
     x = 2 if precision == "fp32" else 1.5
     what = "reordered batch" if precision == "fp32" else "single-device bf16 trunk"
-    for rank, gerr, perr, berr, gloc, gnoise, pnoise in _spawn(_sync_bn_worker, 2, precision):
+    for rank, gerr, perr, berr, gloc, gnoise, pnoise, gsd in _spawn(_sync_bn_worker, 2, precision):
         print(f"\n[dp sync-bn {precision} trunk] rank {rank}: grad rel err {gerr:.3e} ({what} {gnoise:.3e}), "
               f"post-step param-change rel err {perr:.3e} ({what} {pnoise:.3e}), running-stats rel err "
-              f"{berr:.3e}; per-rank statistics: grad rel err {gloc:.3e}")
+              f"{berr:.3e}; vs the single device: synchronised {gsd:.3e}, per-rank statistics {gloc:.3e}")
         assert gerr <= x * gnoise + 1e-6, (gerr, gnoise)
         assert perr <= x * pnoise + 1e-6, (perr, pnoise)
         assert berr <= (1e-5 if precision == "fp32" else 1e-3), berr  # bf16 maps: their roundings
-        assert gloc >= (3 if precision == "fp32" else 2) * max(gerr, gnoise), (gloc, gerr, gnoise)
+        assert gloc >= 3 * gsd, (gloc, gsd)
