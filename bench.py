@@ -55,6 +55,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sync-bn", action="store_true",
                     help="mmbt, N > 1: the trunk's BatchNorms normalise over the whole global batch (cross-rank sums)")
+    ap.add_argument("--main-priority", default="normal", choices=["normal", "high"],
+                    help="mmbt: run the step on a high-priority stream (the side stream's weight-gradient work "
+                         "then yields to the main stream's critical path)")
+    ap.add_argument("--defer-gb", type=float, default=None,
+                    help="mmbt: encoder.DEFER_MAX_BYTES in GB (deferred weight-gradient inputs retained before "
+                         "an early flush; default a quarter of HBM: everything deferred to the trunk backward)")
     ap.add_argument("--no-stream-residue", action="store_true",
                     help="mmbt: the trunk's residual stream in plain bf16 (the round-4 trunk; for same-box A/Bs)")
     ap.add_argument("--workload", default="mmbt", choices=["mmbt", "flava", "uncertainty", "encoders", "vilt"])
@@ -538,6 +544,10 @@ def main():
     from src import resnet
 
     resnet.STREAM_RESIDUE = not args.no_stream_residue
+    if args.defer_gb is not None:
+        encoder.DEFER_MAX_BYTES = int(args.defer_gb * 1e9)
+    if args.main_priority == "high":
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
     # MIOpen solver choice for the ResNet convs: "find" mode over the find-db shipped in
     # multi-modal-uncertainty_amd/miopen_db (per-rank batches 256/128/64/32 pre-searched on
     # MI355X, so no search runs here); MMU_MIOPEN_FIND=0 = MIOpen's immediate-mode heuristics
