@@ -207,7 +207,7 @@ def test_dp_two_ranks_equal_single_device_global_batch(reduce_dtype):
 
 
 
-def _sync_bn_worker(rank, world, port, q, precision):
+def _sync_bn_worker(rank, world, port, q, precision, backend="gloo"):
     """TRAINING-mode step (batch statistics) three ways: one device on the global batch; two
     ranks on its halves with the trunk's BatchNorms exchanging their sums; two ranks without
     the exchange (per-rank statistics).  Gradients are compared over the flat store without
@@ -219,14 +219,18 @@ def _sync_bn_worker(rank, world, port, q, precision):
         here = os.path.dirname(os.path.abspath(__file__))
         sys.path[:0] = [os.path.join(os.path.dirname(here), "multi-modal-uncertainty_amd"), os.path.dirname(here)]
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        if backend == "nccl":  # RCCL: one device per rank
+            torch.cuda.set_device(rank)
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", rank))
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.backends.cudnn.deterministic = True
         from src.dp import GradBucketer, broadcast_parameters, convert_sync_batchnorm
         from src.mmbt import MultimodalBertClf
         from src.optim import BertAdam
         from src.testing import small_args, synthetic_batch
         from oracle.weights import SMALL
-        dev, B = "cuda:0", 8
+        dev, B = (f"cuda:{rank}" if backend == "nccl" else "cuda:0"), 8
 
         def make(prec=precision):
             torch.manual_seed(0)
@@ -320,3 +324,17 @@ def test_dp_sync_batchnorm_two_ranks_equal_single_device_train_mode(precision):
         assert perr <= x * pnoise + 1e-6, (perr, pnoise)
         assert berr <= (1e-5 if precision == "fp32" else 1e-3), berr  # bf16 maps: their roundings
         assert gloc >= 3 * gsd, (gloc, gsd)
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL needs one GPU per rank (2 here)")
+def test_dp_sync_batchnorm_two_ranks_rccl():
+    """The whole-batch BatchNorm exchange over RCCL (backend "nccl"), one device per rank: its
+    own communicator (dp.convert_sync_batchnorm's second group) running beside the gradient
+    buckets' all-reduces on the default one, through the bf16 HIP trunk -- the configuration
+    train.py --sync_bn / bench.py --sync-bn use.  Bars as the gloo test's bf16 arm."""
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    for rank, gerr, perr, berr, gloc, gnoise, pnoise, gsd in _spawn(_sync_bn_worker, 2, "bf16", "nccl"):
+        print(f"\n[dp sync-bn rccl] rank {rank}: grad rel err {gerr:.3e} (single-device bf16 trunk {gnoise:.3e}), "
+              f"vs the single device: synchronised {gsd:.3e}, per-rank statistics {gloc:.3e}")
+        assert gerr <= 1.5 * gnoise + 1e-6 and perr <= 1.5 * pnoise + 1e-6, (gerr, gnoise, perr, pnoise)
+        assert berr <= 1e-3 and gloc >= 3 * gsd, (berr, gloc, gsd)
