@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--defer-gb", type=float, default=None,
                     help="mmbt: encoder.DEFER_MAX_BYTES in GB (deferred weight-gradient inputs retained before "
                          "an early flush; default a quarter of HBM: everything deferred to the trunk backward)")
+    ap.add_argument("--side-cu-frac", type=float, default=None,
+                    help="mmbt: restrict the side stream (weight-gradient GEMMs) to this fraction of the CUs "
+                         "(hipExtStreamCreateWithCUMask), leaving the rest to the main stream's chain")
     ap.add_argument("--no-stream-residue", action="store_true",
                     help="mmbt: the trunk's residual stream in plain bf16 (the round-4 trunk; for same-box A/Bs)")
     ap.add_argument("--workload", default="mmbt", choices=["mmbt", "flava", "uncertainty", "encoders", "vilt"])
@@ -546,6 +549,9 @@ def main():
     resnet.STREAM_RESIDUE = not args.no_stream_residue
     if args.defer_gb is not None:
         encoder.DEFER_MAX_BYTES = int(args.defer_gb * 1e9)
+    if args.side_cu_frac:
+        from src import kernels
+        kernels.SIDE_CU_FRAC = args.side_cu_frac
     if args.main_priority == "high":
         torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
     # MIOpen solver choice for the ResNet convs: "find" mode over the find-db shipped in

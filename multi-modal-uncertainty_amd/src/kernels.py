@@ -75,13 +75,42 @@ def _splitk_workspace(dev):
     return t
 
 
+SIDE_CU_FRAC = None  # e.g. 0.75: the side stream's kernels run on that fraction of every XCD's CUs
+
+
+def _cu_masked_stream(dev, frac):
+    """A stream whose dispatches are restricted to ``frac`` of the CUs (hipExtStreamCreateWithCUMask),
+    so the side stream's weight-gradient GEMMs leave the rest to the main stream's chain.  The
+    mask keeps whole 8-CU groups, 3 of every 4 for 0.75: balanced across the 8 XCDs whether the
+    runtime numbers CUs XCD-blocked or XCD-interleaved."""
+    import ctypes
+    n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+    groups = n_cu // 8
+    keep = max(1, min(groups, round(frac * groups)))
+    # spread the kept groups evenly over the group index (Bresenham)
+    bits = [0] * ((n_cu + 31) // 32)
+    for g in range(groups):
+        if (g + 1) * keep // groups != g * keep // groups:
+            for c in range(8 * g, 8 * g + 8):
+                bits[c // 32] |= 1 << (c % 32)
+    hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime torch already loaded (same soname)
+    h = ctypes.c_void_p()
+    arr = (ctypes.c_uint32 * len(bits))(*bits)
+    with torch.cuda.device(dev):
+        err = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(len(bits)), arr)
+    if err != 0:
+        raise N.NativeError(f"hipExtStreamCreateWithCUMask failed ({err})")
+    return torch.cuda.ExternalStream(h.value, device=dev)
+
+
 def side_stream(dev):
     """The per-device stream the weight-gradient products run on, beside the data-gradient
     chain of the backward (src/encoder.py)."""
     dev = torch.device(dev)
     s = _side.get(dev)
     if s is None:
-        s = _side[dev] = torch.cuda.Stream(device=dev)
+        s = _side[dev] = (_cu_masked_stream(dev, SIDE_CU_FRAC) if SIDE_CU_FRAC
+                          else torch.cuda.Stream(device=dev))
     return s
 
 
