@@ -33,6 +33,15 @@ enum { MMU_BF16 = 0, MMU_F32 = 1 };
 int mmu_version(void);
 const char* mmu_last_error(void);
 
+/* Dropout under HIP-graph replay (round 5).  A captured launch replays the seed it was
+ * captured with; with a device counter set here (uint64, caller-owned, NULL = off) every
+ * dropout launch made afterwards folds *counter into its seed when it RUNS
+ * (seed ^ counter * 0x9E3779B97F4A7C15), so a graph that advances the counter once per
+ * replay draws fresh masks each step while forward and backward of one step agree.
+ * A counter of 0 reproduces the eager masks bit for bit.  Process-wide setting.
+ * (No reference counterpart: the reference draws torch's RNG per dropout call.) */
+int mmu_set_seed_offset(const uint64_t* dev_counter);
+
 /* ------------------------------------------------------------------ GEMM
  * C[m,n] (op)= sum_k A(m,k) * B(n,k), batched over `batch` with element strides.
  *   A(m,k) = A[m*lda + k] if a_kmajor else A[k*lda + m]      (bf16)

@@ -256,7 +256,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   uint64_t* kbuf = kbuf_all + w * 32 * nkv;
   const bool store_bits = STORE && DROP && p.dropmask != nullptr;
   // dropout counter base of row q: seed_bh + 4 (q nkv) + 2h  (+ 4j + s2 per tile half)
-  const uint32_t ctr = seed_for(p.seed, bh) + 4u * (uint32_t)q * (uint32_t)nkv + 2u * (uint32_t)h;
+  const uint32_t ctr = seed_for(mmu_eff_seed(p.seed, p.seed_off), bh) + 4u * (uint32_t)q * (uint32_t)nkv + 2u * (uint32_t)h;
 
   const void* kv_base = p.qkv + (int64_t)b * L * p.ld_qkv;
   const int kv_bytes = (int)(L * p.ld_qkv * 2);

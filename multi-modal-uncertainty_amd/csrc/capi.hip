@@ -14,6 +14,15 @@ using namespace mmu;
 
 static thread_local std::string g_err;
 
+namespace mmu {
+const uint64_t* g_seed_off = nullptr;
+}
+
+int mmu_set_seed_offset(const uint64_t* dev_counter) {
+  g_seed_off = dev_counter;
+  return 0;
+}
+
 static int fail(const char* fmt, ...) {
   char buf[512];
   va_list ap;
@@ -128,7 +137,7 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
     p.residual = epi->residual; p.ldr = epi->ldr; p.res_bstride = epi->res_bstride;
     p.aux = epi->aux; p.ldx = epi->ldx; p.aux_bstride = epi->aux_bstride;
     p.colsum = epi->colsum; p.colsum_bstride = epi->colsum_bstride;
-    p.drop_p = epi->drop_p; p.seed = epi->seed;
+    p.drop_p = epi->drop_p; p.seed = epi->seed; p.seed_off = g_seed_off;
     p.res_ln_mean = epi->res_ln_mean; p.res_ln_rstd = epi->res_ln_rstd;
     p.res_ln_w = epi->res_ln_w; p.res_ln_b = epi->res_ln_b; p.res_ln_bstride = epi->res_ln_bstride;
   }
@@ -233,6 +242,7 @@ int mmu_attention_fwd(const void* QKV, int64_t ld_qkv, const float* keymask, voi
   AttnParams p{};
   p.qkv = (const bf16*)QKV; p.ld_qkv = ld_qkv; p.keymask = keymask; p.out = (bf16*)O; p.ld_out = ld_o;
   p.lse = LSE; p.batch = (int)batch; p.L = (int)L; p.heads = (int)heads; p.drop_p = drop_p; p.seed = seed;
+  p.seed_off = g_seed_off;
   p.dropmask = dropmask;
   attention_fwd_launch(p, (hipStream_t)stream);
   return check_launch("mmu_attention_fwd");
@@ -252,6 +262,7 @@ int mmu_attention_bwd(const void* QKV, int64_t ld_qkv, const float* keymask, con
   p.qkv = (const bf16*)QKV; p.ld_qkv = ld_qkv; p.keymask = keymask; p.o = (const bf16*)O; p.ld_o = ld_o;
   p.dout = (const bf16*)dO; p.ld_do = ld_do; p.lse = (float*)LSE; p.delta = delta; p.out = (bf16*)dQKV;
   p.ld_out = ld_dqkv; p.batch = (int)batch; p.L = (int)L; p.heads = (int)heads; p.drop_p = drop_p; p.seed = seed;
+  p.seed_off = g_seed_off;
   p.dropmask = (uint64_t*)dropmask;
   p.colsum = dbias_parts;
   attention_bwd_launch(p, (hipStream_t)stream);
@@ -277,7 +288,7 @@ int mmu_layernorm_bwd(const void* dY, const void* X, const float* mean, const fl
   if (rows <= 0 || H <= 0 || H % 256 || H > 1024 || rows_per_part <= 0) return fail("mmu_layernorm_bwd: bad shape");
   if (drop_p < 0.f || drop_p >= 1.f) return fail("mmu_layernorm_bwd: drop_p out of range");
   layernorm_bwd_launch((const bf16*)dY, X, false, mean, rstd, w, (bf16*)dX, (bf16*)dXdrop, nullptr, drop_p, seed,
-                       part_dw, part_db, part_dbias, rows, H, rows_per_part, (hipStream_t)stream);
+                       g_seed_off, part_dw, part_db, part_dbias, rows, H, rows_per_part, (hipStream_t)stream);
   return check_launch("mmu_layernorm_bwd");
 }
 
@@ -301,7 +312,7 @@ int mmu_layernorm_bwd_f32(const void* dY, const float* X, const float* mean, con
   if (rows <= 0 || H <= 0 || H % 256 || H > 1024 || rows_per_part <= 0) return fail("mmu_layernorm_bwd_f32: bad shape");
   if (drop_p < 0.f || drop_p >= 1.f) return fail("mmu_layernorm_bwd_f32: drop_p out of range");
   layernorm_bwd_launch((const bf16*)dY, X, true, mean, rstd, w, (bf16*)dX, (bf16*)dXdrop, nullptr, drop_p, seed,
-                       part_dw, part_db, part_dbias, rows, H, rows_per_part, (hipStream_t)stream);
+                       g_seed_off, part_dw, part_db, part_dbias, rows, H, rows_per_part, (hipStream_t)stream);
   return check_launch("mmu_layernorm_bwd_f32");
 }
 
@@ -311,7 +322,7 @@ int mmu_layernorm_bwd_res(const void* dY, const void* X, const float* mean, cons
   if (!dY || !X || !mean || !rstd || !w || !dX || !dRes) return fail("mmu_layernorm_bwd_res: null pointer");
   if (rows <= 0 || H <= 0 || H % 256 || H > 1024 || rows_per_part <= 0) return fail("mmu_layernorm_bwd_res: bad shape");
   layernorm_bwd_launch((const bf16*)dY, X, false, mean, rstd, w, (bf16*)dX, nullptr, (const bf16*)dRes, 0.f, 0,
-                       part_dw, part_db, part_dbias, rows, H, rows_per_part, (hipStream_t)stream);
+                       nullptr, part_dw, part_db, part_dbias, rows, H, rows_per_part, (hipStream_t)stream);
   return check_launch("mmu_layernorm_bwd_res");
 }
 
@@ -372,7 +383,7 @@ int mmu_embed_fwd(const int64_t* ids, const int64_t* seg, const int64_t* txt_mas
   p.type = type; p.ln_w = ln_w; p.ln_b = ln_b; p.eps = eps; p.cls_id = cls_id; p.sep_id = sep_id; p.V = V; p.B = B;
   p.T = T; p.n_img = n_img; p.Lout = Lout; p.H = H; p.X = (bf16*)X; p.X32 = X32;
   if (drop_txt < 0.f || drop_txt >= 1.f || drop_img < 0.f || drop_img >= 1.f) return fail("mmu_embed_fwd: bad dropout");
-  p.drop_txt = drop_txt; p.drop_img = drop_img; p.seed = seed; p.keymask = keymask; p.mean = mean; p.rstd = rstd;
+  p.drop_txt = drop_txt; p.drop_img = drop_img; p.seed = seed; p.seed_off = g_seed_off; p.keymask = keymask; p.mean = mean; p.rstd = rstd;
   embed_fwd_launch(p, (hipStream_t)stream);
   return check_launch("mmu_embed_fwd");
 }
@@ -390,7 +401,7 @@ int mmu_embed_bwd(const void* dX, const int64_t* ids, const int64_t* seg, const 
   EmbedBwdParams q{};
   q.dX = (const bf16*)dX; q.ids = ids; q.seg = seg; q.proj = proj; q.word = word; q.pos = pos; q.type = type;
   q.ln_w = ln_w; q.mean = mean; q.rstd = rstd; q.cls_id = cls_id; q.sep_id = sep_id; q.B = B; q.T = T;
-  q.n_img = n_img; q.H = H; q.drop_txt = drop_txt; q.drop_img = drop_img; q.seed = seed; q.d_word = d_word; q.d_pos = d_pos; q.d_type = d_type; q.d_ln_w = d_ln_w;
+  q.n_img = n_img; q.H = H; q.drop_txt = drop_txt; q.drop_img = drop_img; q.seed = seed; q.seed_off = g_seed_off; q.d_word = d_word; q.d_pos = d_pos; q.d_type = d_type; q.d_ln_w = d_ln_w;
   q.d_ln_b = d_ln_b; q.d_proj = d_proj; q.ws = ws;
   embed_bwd_launch(q, (hipStream_t)stream);
   return check_launch("mmu_embed_bwd");

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbedParams p) {
     float y[4] = {(e[i][0] - mu) * rs * w.x + bb.x, (e[i][1] - mu) * rs * w.y + bb.y,
                   (e[i][2] - mu) * rs * w.z + bb.z, (e[i][3] - mu) * rs * w.w + bb.w};
     if (thr) {
-      const uint32_t keep = mmu_keep4(p.seed, (uint64_t)(row * 768 + c) >> 2, thr);
+      const uint32_t keep = mmu_keep4(mmu_eff_seed(p.seed, p.seed_off), (uint64_t)(row * 768 + c) >> 2, thr);
 #pragma unroll
       for (int k = 0; k < 4; ++k) y[k] = ((keep >> k) & 1) ? y[k] * dsc : 0.f;
     }
@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256) void embed_bwd_rows_kernel(EmbedBwdParams q, E
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       bf16x4 d = *(const bf16x4*)(q.dX + row * H + 256 * i + 4 * l);
-      const uint32_t keep = thr ? mmu_keep4(q.seed, (uint64_t)(row * H + 256 * i + 4 * l) >> 2, thr) : 0xFu;
+      const uint32_t keep = thr ? mmu_keep4(mmu_eff_seed(q.seed, q.seed_off), (uint64_t)(row * H + 256 * i + 4 * l) >> 2, thr) : 0xFu;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const float dy = ((keep >> k) & 1) ? bf2f(d[k]) * dsc : 0.f;

@@ -111,7 +111,8 @@ static __device__ __forceinline__ bf16x8 s_frag(const char* s, int row0, int ks,
 // dropout quad counter ((z M + m) N + n) / 4
 template <int EPI, bool OUT_F32>
 static __device__ __forceinline__ void epi_oct(const GemmParams& p, void* cdst, bf16* xdst, uint64_t qd,
-                                               float (&v)[8], const float (&in)[8], float scale, uint32_t thr) {
+                                               float (&v)[8], const float (&in)[8], float scale, uint32_t thr,
+                                               uint64_t seed) {
   if (EPI == MMU_EPI_BIAS_GELU) {  // C = gelu(z); aux (optional) = gelu'(z) for the backward
     float d[8];
 #pragma unroll
@@ -124,7 +125,7 @@ static __device__ __forceinline__ void epi_oct(const GemmParams& p, void* cdst, 
     }
   } else if (EPI == MMU_EPI_BIAS_DROP_RES) {
     if (thr) {  // counter over the whole batched output: batch item z, row m, column n (quads)
-      const uint32_t keep = mmu_keep4(p.seed, qd, thr) | (mmu_keep4(p.seed, qd + 1, thr) << 4);
+      const uint32_t keep = mmu_keep4(seed, qd, thr) | (mmu_keep4(seed, qd + 1, thr) << 4);
 #pragma unroll
       for (int r = 0; r < 8; ++r) v[r] = ((keep >> r) & 1) ? v[r] * scale : 0.f;
     }
@@ -132,7 +133,7 @@ static __device__ __forceinline__ void epi_oct(const GemmParams& p, void* cdst, 
     for (int r = 0; r < 8; ++r) v[r] += in[r];  // residual (f32 when C is f32: the hidden stream)
   } else if (EPI == MMU_EPI_BIAS_DROP_QGELU) {  // FLAVA mlp: u = dropout(z); C = u*sigmoid(1.702u)
     uint32_t keep = 0xFFu;                         // aux (optional) = dC/dz = keep*scale*qgelu'(u)
-    if (thr) keep = mmu_keep4(p.seed, qd, thr) | (mmu_keep4(p.seed, qd + 1, thr) << 4);
+    if (thr) keep = mmu_keep4(seed, qd, thr) | (mmu_keep4(seed, qd + 1, thr) << 4);
     float d[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
@@ -217,6 +218,7 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
   const int64_t x_l = XST ? m_l * p.ldx + n : 0;
   const int64_t s_l = EPI == MMU_EPI_STORE ? m_l * p.N + n : 0;
   const int64_t q_l = DRP ? (z * p.M + m_l) * p.N + n : 0;
+  const uint64_t seed = DRP && thr ? mmu_eff_seed(p.seed, p.seed_off) : 0;
   // residual = LN(residual rows): per-column gamma / beta here, per-row mean / rstd per pass
   const bool res_ln = RES32 && p.res_ln_w != nullptr && !slab;
   float lw[8], lb[8];
@@ -300,7 +302,7 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
       }
       void* cdst = OUT_F32 ? (void*)((float*)p.C + c_l + d * p.ldc) : (void*)((bf16*)p.C + c_l + d * p.ldc);
       epi_oct<EPI, OUT_F32>(p, cdst, (XST && aux) ? aux + x_l + d * p.ldx : nullptr,
-                            DRP ? (uint64_t)(q_l + d * p.N) >> 2 : 0, v, inf, scale, thr);
+                            DRP ? (uint64_t)(q_l + d * p.N) >> 2 : 0, v, inf, scale, thr, seed);
       if (want_cs) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) cs[e] += v[e];

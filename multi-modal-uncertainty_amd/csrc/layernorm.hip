@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dY
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ w, bf16* __restrict__ dX,
                                                      bf16* __restrict__ dXd, const bf16* __restrict__ dR,
-                                                     float drop_p, uint64_t seed,
+                                                     float drop_p, uint64_t seed, const uint64_t* seed_off,
                                                      float* __restrict__ pdw, float* __restrict__ pdb,
                                                      float* __restrict__ pdbias, int64_t rows, int rpp) {
   constexpr int H = 256 * NV, nv = NV;
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dY
         }
         *(bf16x4*)(dX + row * H + c) = bf16x4{f2bf(dx[0]), f2bf(dx[1]), f2bf(dx[2]), f2bf(dx[3])};
         if (dXd) {
-          uint32_t keep = thr ? mmu_keep4(seed, (uint64_t)(row * H + c) >> 2, thr) : 0xFu;
+          uint32_t keep = thr ? mmu_keep4(mmu_eff_seed(seed, seed_off), (uint64_t)(row * H + c) >> 2, thr) : 0xFu;
 #pragma unroll
           for (int e = 0; e < 4; ++e) dx[e] = ((keep >> e) & 1) ? dx[e] * scale : 0.f;
           *(bf16x4*)(dXd + row * H + c) = bf16x4{f2bf(dx[0]), f2bf(dx[1]), f2bf(dx[2]), f2bf(dx[3])};
@@ -366,11 +366,12 @@ void layernorm_fwd32_launch(const float* X, const float* w, const float* b, bf16
 
 template <typename XT>
 static void ln_bwd_launch_t(const bf16* dY, const XT* X, const float* mean, const float* rstd, const float* w,
-                            bf16* dX, bf16* dXdrop, const bf16* dR, float drop_p, uint64_t seed, float* pdw,
-                            float* pdb, float* pdbias, int64_t rows, int64_t H, int64_t rpp, hipStream_t s) {
+                            bf16* dX, bf16* dXdrop, const bf16* dR, float drop_p, uint64_t seed,
+                            const uint64_t* seed_off, float* pdw, float* pdb, float* pdbias, int64_t rows, int64_t H,
+                            int64_t rpp, hipStream_t s) {
   const dim3 g((unsigned)((rows + rpp - 1) / rpp));
 #define LNB(NV) hipLaunchKernelGGL((ln_bwd_kernel<NV, XT>), g, dim3(256), 0, s, dY, X, mean, rstd, w, dX, dXdrop, dR, \
-                                   drop_p, seed, pdw, pdb, pdbias, rows, (int)rpp)
+                                   drop_p, seed, seed_off, pdw, pdb, pdbias, rows, (int)rpp)
   switch (H / 256) {
     case 1: LNB(1); break;
     case 2: LNB(2); break;
@@ -382,11 +383,14 @@ static void ln_bwd_launch_t(const bf16* dY, const XT* X, const float* mean, cons
 
 void layernorm_bwd_launch(const bf16* dY, const void* X, bool x_f32, const float* mean, const float* rstd,
                           const float* w, bf16* dX, bf16* dXdrop, const bf16* dR, float drop_p, uint64_t seed,
-                          float* pdw, float* pdb, float* pdbias, int64_t rows, int64_t H, int64_t rpp, hipStream_t s) {
+                          const uint64_t* seed_off, float* pdw, float* pdb, float* pdbias, int64_t rows, int64_t H,
+                          int64_t rpp, hipStream_t s) {
   if (x_f32)
-    ln_bwd_launch_t(dY, (const float*)X, mean, rstd, w, dX, dXdrop, dR, drop_p, seed, pdw, pdb, pdbias, rows, H, rpp, s);
+    ln_bwd_launch_t(dY, (const float*)X, mean, rstd, w, dX, dXdrop, dR, drop_p, seed, seed_off, pdw, pdb, pdbias, rows,
+                    H, rpp, s);
   else
-    ln_bwd_launch_t(dY, (const bf16*)X, mean, rstd, w, dX, dXdrop, dR, drop_p, seed, pdw, pdb, pdbias, rows, H, rpp, s);
+    ln_bwd_launch_t(dY, (const bf16*)X, mean, rstd, w, dX, dXdrop, dR, drop_p, seed, seed_off, pdw, pdb, pdbias, rows,
+                    H, rpp, s);
 }
 
 }  // namespace mmu

@@ -37,6 +37,12 @@ static __device__ __forceinline__ uint32_t mmu_keep4(uint64_t seed, uint64_t qua
   return ((h0 & 0xFFFFu) >= thr16 ? 1u : 0u) | ((h0 >> 16) >= thr16 ? 2u : 0u) |
          ((h1 & 0xFFFFu) >= thr16 ? 4u : 0u) | ((h1 >> 16) >= thr16 ? 8u : 0u);
 }
+// Graph replays (mmu_set_seed_offset): a captured launch keeps the seed it was captured with,
+// so every dropout kernel folds in a device counter the replayed graph advances; off == NULL
+// (eager launches) and *off == 0 both leave the seed as given.
+static __device__ __forceinline__ uint64_t mmu_eff_seed(uint64_t seed, const uint64_t* off) {
+  return off ? seed ^ (*off * 0x9E3779B97F4A7C15ull) : seed;
+}
 static __device__ __forceinline__ bool mmu_keep1(uint64_t seed, uint64_t idx, uint32_t thr16) {
   const uint64_t quad = idx >> 2;
   const uint32_t x = (((uint32_t)quad << 1) ^ ((uint32_t)(quad >> 31) * 0x9E3779B8u)) ^ mmu_seed32(seed);

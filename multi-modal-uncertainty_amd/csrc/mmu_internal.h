@@ -8,6 +8,9 @@ typedef __bf16 bf16;
 
 namespace mmu {
 
+// mmu_set_seed_offset's device counter (capi.hip), copied into every dropout launch
+extern const uint64_t* g_seed_off;
+
 struct GemmParams {
   const bf16* A;
   const bf16* B;
@@ -27,6 +30,7 @@ struct GemmParams {
   int64_t colsum_bstride;
   float drop_p;
   uint64_t seed;
+  const uint64_t* seed_off;  // per-replay seed counter (mmu_set_seed_offset), or NULL
   // f32 residual = LN(residual rows) recomputed per element (mmu_epilogue res_ln_*)
   const float *res_ln_mean, *res_ln_rstd, *res_ln_w, *res_ln_b;
   int64_t res_ln_bstride;
@@ -81,6 +85,7 @@ struct AttnParams {
   int batch, L, heads;
   float drop_p;
   uint64_t seed;
+  const uint64_t* seed_off;
 };
 void attention_fwd_launch(const AttnParams& p, hipStream_t s);
 void attention_bwd_launch(const AttnParams& p, hipStream_t s);
@@ -92,8 +97,8 @@ void layernorm_fwd32_launch(const float* X, const float* w, const float* b, bf16
                             hipStream_t s);
 void layernorm_bwd_launch(const bf16* dY, const void* X, bool x_f32, const float* mean, const float* rstd,
                           const float* w, bf16* dX, bf16* dXdrop, const bf16* dR, float drop_p, uint64_t seed,
-                          float* pdw, float* pdb, float* pdbias, int64_t rows, int64_t H, int64_t rows_per_part,
-                          hipStream_t s);
+                          const uint64_t* seed_off, float* pdw, float* pdb, float* pdbias, int64_t rows, int64_t H,
+                          int64_t rows_per_part, hipStream_t s);
 
 // FLAVA attention over the sequence (= batch) axis, flava.hip
 struct SeqAttnParams {
@@ -118,6 +123,7 @@ struct EmbedParams {
   const float *proj, *word, *pos, *type, *ln_w, *ln_b;
   float eps, drop_txt, drop_img;
   uint64_t seed;
+  const uint64_t* seed_off;
   int64_t cls_id, sep_id, V, B, T, n_img, Lout, H;
   bf16* X;
   float* X32;  // optional f32 copy of X (the encoder's f32 hidden stream)
@@ -131,6 +137,7 @@ struct EmbedBwdParams {
   int64_t cls_id, sep_id, B, T, n_img, H;
   float drop_txt, drop_img;
   uint64_t seed;
+  const uint64_t* seed_off;
   float *d_word, *d_pos, *d_type, *d_ln_w, *d_ln_b, *d_proj, *ws;
 };
 void embed_bwd_launch(const EmbedBwdParams& p, hipStream_t s);

@@ -31,6 +31,7 @@ class Epilogue(ctypes.Structure):
 SIGNATURES = {
     "mmu_version": (c_i32, []),
     "mmu_last_error": (ctypes.c_char_p, []),
+    "mmu_set_seed_offset": (c_i32, [c_vp]),
     "mmu_gemm": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_i64, c_i64, c_i64,
                          c_i64, c_i64, c_i64, c_i64, ctypes.POINTER(Epilogue), c_vp]),
     "mmu_colsum_reduce": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_vp]),

@@ -674,6 +674,22 @@ def ece_bins(conf, correct, n_bins, out):
 _alg = {"on": False, "bytes": 0.0, "n": 0}
 
 
+_seed_counter = None
+
+
+def set_seed_offset(counter):
+    """Dropout seeds under HIP-graph replay (include/mmu.h mmu_set_seed_offset): ``counter`` = a
+    1-element int64 device tensor every later dropout launch folds into its seed when it runs
+    (None = off).  The tensor is kept referenced here while it is set."""
+    global _seed_counter
+    if counter is not None:
+        _want(counter, torch.int64, "seed counter")
+        if counter.numel() != 1 or not counter.is_cuda:
+            raise N.NativeError("seed counter: a 1-element int64 CUDA tensor")
+    _seed_counter = counter
+    N.call("mmu_set_seed_offset", _ptr(counter) if counter is not None else None)
+
+
 def timing_enable(on=True):
     """HIP-event timing of every mmu_gemm launch (and a count of its algorithmic bytes)."""
     N.call("mmu_timing_enable", int(on))

@@ -1,0 +1,138 @@
+"""HIP-graph replay of the whole MMBT training step (src/graphs.py; bench.py --graph).
+
+* The dropout seed counter (include/mmu.h mmu_set_seed_offset): a counter of 0 leaves every
+  dropout launch as eager execution draws it (same loss and gradients as no counter), a
+  counter of 1 draws other masks.
+* Replay == eager: a graph-replayed training step (forward with attention / hidden / embedding
+  dropout, backward with the deferred side-stream weight gradients, fused BertAdam) equals the
+  eager step run with the same host-drawn seeds and the same counter value, step after step
+  (loss to 1e-5; the parameters after 4 optimizer steps to 1e-4 of their update, without the
+  attention key biases, whose zero gradient BertAdam turns into sign-of-noise steps);
+  consecutive replays draw new masks.
+Model: the small MMBT (2 BERT layers, one Bottleneck per stage), batch 8, in training mode
+(batch-statistic BatchNorm), the reference's step (src/framework.py:276-304)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+B, T, P = 8, 16, 0.1
+
+
+def _model(sd=None):
+    from oracle.weights import SMALL, make_state_dict
+    from src.mmbt import MultimodalBertClf
+    from src.optim import BertAdam
+    from src.testing import small_args
+    torch.manual_seed(0)
+    m = MultimodalBertClf(small_args(bert_hidden_dropout=P, bert_attn_dropout=P, dropout=P))
+    m.load_state_dict(sd if sd is not None else make_state_dict(0, SMALL), strict=True)
+    m = m.to("cuda:0").train()
+    named = list(m.named_parameters())
+    nd = ["bias", "LayerNorm.bias", "LayerNorm.weight"]
+    groups = [{"params": [p for n, p in named if not any(k in n for k in nd)], "weight_decay": 0.01},
+              {"params": [p for n, p in named if any(k in n for k in nd)], "weight_decay": 0.0}]
+    return m, BertAdam(groups, lr=1e-5, warmup=0.1, t_total=20.0)
+
+
+def _batch():
+    from oracle.weights import SMALL
+    from src.testing import synthetic_batch
+    x, y = synthetic_batch(B, T, vocab=SMALL.vocab, lens=[16, 9, 16, 12, 5, 16, 14, 16], seed=4)
+    return tuple(t.to("cuda:0") for t in x), y.to("cuda:0")
+
+
+def _stepper(m, o, x, y, optimize=True):
+    def step():
+        o.zero_grad()
+        loss = m.compute_loss(m(*x), y)
+        loss.backward()
+        if optimize:
+            o.step()
+        return loss
+    return step
+
+
+def test_seed_counter_zero_is_the_eager_draw(dev):
+    from src import kernels as K
+    torch.backends.cudnn.deterministic = True
+    m, o = _model()
+    x, y = _batch()
+    step = _stepper(m, o, x, y, optimize=False)
+    out = []
+    ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+    try:
+        for value in (None, None, 0, 1):  # (the first step builds the lazily made buffers)
+            if value is not None:
+                ctr.fill_(value)
+            K.set_seed_offset(None if value is None else ctr)
+            torch.manual_seed(11)  # the host-drawn seeds (src/mmbt.py _seed)
+            loss = step()
+            torch.cuda.synchronize()
+            out.append((loss.item(), m.store.grad.clone()))
+    finally:
+        K.set_seed_offset(None)
+    (lw, gw), (l0, g0), (l1, g1), (l2, g2) = out
+    rel = lambda a, b: ((a - b).norm() / b.norm()).item()  # noqa: E731
+    print(f"\n[seed counter] loss first {lw:.6f} (grad rel diff {rel(gw, g0):.2e}) none {l0:.6f} / zero {l1:.6f} / "
+          f"one {l2:.6f}; grad rel diff zero {rel(g1, g0):.2e}, one {rel(g2, g0):.2e}")
+    noise = rel(gw, g0)  # the eager step against itself (float-atomic summation order)
+    assert abs(l1 - l0) <= max(3 * abs(lw - l0), 1e-7 * abs(l0)) and rel(g1, g0) <= max(3 * noise, 1e-6)
+    assert rel(g2, g0) > max(30 * noise, 1e-2)
+
+
+def test_graph_replay_equals_eager_steps(dev):
+    from src import kernels as K
+    torch.backends.cudnn.deterministic = True
+    from src.graphs import StepGraph
+    x, y = _batch()
+    ma, oa = _model()
+    sd0 = {k: v.detach().cpu().clone() for k, v in ma.state_dict().items()}
+    torch.manual_seed(21)
+    g = StepGraph(_stepper(ma, oa, x, y), dev, warmup=1)
+    # host RNG state after the capture's draws (the graph's seeds): the eager arm restores the
+    # state from before the capture for each of its steps instead
+    losses_a = []
+    for _ in range(3):
+        losses_a.append(g.replay().item())
+    torch.cuda.synchronize()
+    flat_a = ma.store.flat.clone()
+    ctr_a = int(g.counter.item())
+    g.release()
+    del g
+
+    mb, ob = _model(sd0)
+    flat0 = mb.store.flat.clone()
+    step_b = _stepper(mb, ob, x, y)
+    ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+    K.set_seed_offset(ctr)
+    try:
+        torch.manual_seed(21)
+        ctr.fill_(1)
+        step_b()  # = StepGraph's eager warmup step (counter 1)
+        rng = torch.get_rng_state()  # the capture drew its seeds from here
+        losses_b = []
+        for k in range(3):
+            torch.set_rng_state(rng)
+            ctr.fill_(2 + k)  # the replay's first node advanced the counter to 2, 3, 4
+            losses_b.append(step_b().item())
+        torch.cuda.synchronize()
+    finally:
+        K.set_seed_offset(None)
+    flat_b = mb.store.flat
+    # without the key biases: their true gradient is 0 (softmax shift invariance), so BertAdam
+    # moves them by the sign of float-atomic noise, which differs with the kernels' overlap
+    keep = torch.ones_like(flat_b, dtype=torch.bool)
+    for n in mb.store.names:
+        if n.endswith("attention.self.key.bias"):
+            keep[mb.store.offsets[n]:mb.store.offsets[n] + mb.store.params[n].numel()] = False
+    d = ((flat_a - flat_b)[keep].norm() / (flat_b - flat0)[keep].norm()).item()  # relative to the 4 steps' update
+    moved = (flat_b - flat0).norm().item()
+    print(f"\n[graph] replay losses {losses_a}, eager {losses_b}; counter {ctr_a}; params after 4 steps: diff / update {d:.2e} "
+          f"(moved {moved:.3e})")
+    assert ctr_a == 4
+    for a, b in zip(losses_a, losses_b):
+        assert abs(a - b) <= 1e-5 * abs(b), (losses_a, losses_b)
+    assert len(set(losses_a)) == 3, "consecutive replays drew the same dropout masks"
+    assert moved > 0
+    assert d <= 1e-4, d
