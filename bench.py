@@ -77,7 +77,8 @@ def parse():
     ap.add_argument("--eval-batch", type=int, default=32, help="uncertainty: samples per rank per step")
     ap.add_argument("--flava-batch", type=int, default=128, help="FLAVA per-rank batch (train.py --batch_size)")
     ap.add_argument("--flava-tokens", type=str, default="197,77", help="FLAVA image,text embedding lengths")
-    ap.add_argument("--cpu-batch", type=int, default=2)
+    ap.add_argument("--cpu-batch", type=int, default=8,
+                    help="samples per oracle step of the CPU baseline (SURVEY §8(d): B = 8, 3 steps)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: affinity, capped by OMP_NUM_THREADS")
     return ap.parse_args()
 
@@ -146,7 +147,7 @@ def cpu_baseline(args, L_text):
             fn()
         return (time.perf_counter() - t0) / n
 
-    n = 2
+    n = 3
     t_train = timed(one, n)
     with torch.no_grad():
         t_eval = timed(lambda: R.forward(sd, txt, mask, mask, img, FULL), n)

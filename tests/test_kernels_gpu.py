@@ -316,6 +316,48 @@ def test_gemm_many_tiles_every_element(dev, ak, bk):
         close(C2, A2.float() @ B2.float().transpose(1, 2))
 
 
+@pytest.mark.parametrize("M,N,Kd", [(256 * 257, 768, 3072), (16416, 768, 3072), (16416, 3072, 768),
+                                     (256 * 65 + 32, 768, 2304)])
+def test_gemm_stream_k_tail(dev, M, N, Kd):
+    """The stream-K tail (csrc/gemm.hip gemm_sk_kernel; on by default): the last round of
+    256 x 256 tiles split over one workgroup per CU, split tiles summed from partial slabs by
+    their last-arriving contributor.  Shapes: batch 256's N = 768 class (771 tiles = 3 rounds
+    + 3), batch 32's (195 / 780 tiles for 256 CUs) and a 32-row M tail.  Every element of every
+    epilogue against torch, and bitwise-equal results from two runs (the contributor-order sum
+    does not depend on which workgroup arrives last)."""
+    k = K()
+    A, B = rnd(M, Kd, dev=dev, seed=141), rnd(N, Kd, dev=dev, seed=142, scale=0.1)
+    ref = A.float() @ B.float().t()
+    bias = torch.randn(N, device=dev) * 0.1
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    k.gemm(A, Kd, True, B, Kd, True, out, N, M, N, Kd, epi=k.epilogue(k.EPI_STORE, bias=bias))
+    close(out, ref + bias)
+    again = torch.empty_like(out)
+    k.gemm(A, Kd, True, B, Kd, True, again, N, M, N, Kd, epi=k.epilogue(k.EPI_STORE, bias=bias))
+    assert torch.equal(out, again)
+    # f32 hidden stream: bias + dropout(p = 0) + f32 residual
+    R32 = torch.randn(M, N, device=dev)
+    f = torch.empty(M, N, dtype=torch.float32, device=dev)
+    k.gemm(A, Kd, True, B, Kd, True, f, N, M, N, Kd,
+           epi=k.epilogue(k.EPI_BIAS_DROP_RES, bias=bias, residual=R32, drop_p=0.0, seed=3))
+    torch.testing.assert_close(f, ref + bias + R32, rtol=1e-3, atol=2e-3 * ref.abs().max().item())
+    # GELU + its derivative, then dGELU with the bias-gradient column sums, then a residual add
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    k.gemm(A, Kd, True, B, Kd, True, out, N, M, N, Kd, epi=k.epilogue(k.EPI_BIAS_GELU, bias=bias, aux=aux))
+    z = ref + bias
+    phi = 0.5 * (1 + torch.erf(z / math.sqrt(2)))
+    close(out, z * phi)
+    close(aux, phi + z * torch.exp(-0.5 * z * z) / math.sqrt(2 * math.pi))
+    cs = torch.zeros(N, device=dev)
+    k.gemm(A, Kd, True, B, Kd, True, out, N, M, N, Kd, epi=k.epilogue(k.EPI_DGELU, aux=aux, colsum=cs))
+    dg = ref * aux.float()
+    close(out, dg)
+    torch.testing.assert_close(cs, dg.sum(0), rtol=2e-3, atol=2e-3 * dg.abs().sum(0).max().item())
+    R16 = rnd(M, N, dev=dev, seed=143)
+    k.gemm(A, Kd, True, B, Kd, True, out, N, M, N, Kd, epi=k.epilogue(k.EPI_ADD_RES, residual=R16))
+    close(out, ref + R16.float())
+
+
 def test_gemm_partial_last_wave_batched(dev):
     """batch 2 x 129 tile rows x 3 column tiles = 774 tiles, per-item bias"""
     k = K()
