@@ -79,11 +79,7 @@ typedef struct mmu_epilogue {
   uint64_t seed;            /* dropout stream: element (z, m, n) uses counter (z*M+m)*N+n */
   float* workspace;         /* optional f32 scratch: lets a STORE/f32/no-bias product split K
                                over workgroups (weight gradients); slabs summed in slice
-                               order, so results stay deterministic.  With both operands
-                               K-major and batch 1 it also holds the stream-K tail's partial
-                               tiles (round 5: 2 x 256 KiB per CU + a counter per tile; used
-                               when it fits, else whole tiles only; MMU_GEMM_SK=0 disables),
-                               summed in contributor order, equally deterministic.
+                               order, so results stay deterministic.
                                Stream-ordered: one workspace per stream.                */
   int64_t workspace_floats;
   /* BIAS_DROP_RES into an f32 C only (optional, all four or none): the f32 residual is the

@@ -490,9 +490,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 __global__ __launch_bounds__(256) void attn_keep_kernel(AttnParams p) {
   const int L = p.L, nkv = (L + 63) / 64;
   const int bh = blockIdx.y;
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (int64_t)L * nkv) return;
-  const int q = (int)(idx / nkv), j = (int)(idx - (int64_t)q * nkv);
+  const int idx = (int)blockIdx.x * 256 + (int)threadIdx.x;  // (L * nkv <= 576 * 9: 32-bit math)
+  if (idx >= L * nkv) return;
+  const int q = (int)((uint32_t)idx / (uint32_t)nkv), j = idx - q * nkv;
   const uint32_t thr = drop_thr(p.drop_p), thr_hi = thr << 16;
   const uint32_t base = seed_for(mmu_eff_seed(p.seed, p.seed_off), bh) + 4u * (uint32_t)q * (uint32_t)nkv +
                         4u * (uint32_t)j;

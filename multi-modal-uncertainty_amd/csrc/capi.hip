@@ -99,26 +99,6 @@ int mmu_timing_read(double* total_ms, int64_t* launches, double* flops) {
   return 0;
 }
 
-// stream-K tail of mmu_gemm: the CUs of the current device (one stream-K workgroup each), the
-// MMU_GEMM_SK switch (0: off), and the least idle K-steps of a last round that pays for it
-static int64_t device_cus() {
-  static int cached[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (!cached[dev]) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    cached[dev] = n;
-  }
-  return cached[dev];
-}
-static bool sk_enabled() {
-  static const int on = getenv("MMU_GEMM_SK") ? atoi(getenv("MMU_GEMM_SK")) : 0;
-  return on != 0;
-}
-constexpr double SK_MIN_KSTEPS = 6.0;
-constexpr int64_t SK_SLAB_FLOATS_HOST = 8 * 32 * 64 * 4;  // = gemm.hip SK_SLAB_FLOATS
-
 int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb, int b_kmajor, void* C,
              int64_t ldc, int c_dtype, int64_t M, int64_t N, int64_t K, int64_t batch, int64_t strideA,
              int64_t strideB, int64_t strideC, const mmu_epilogue* epi, mmu_stream_t stream) {
@@ -200,26 +180,6 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
     }
   }
   hipStream_t s = (hipStream_t)stream;
-  // stream-K tail (gemm.hip gemm_sk_kernel) when the last round of 256 x 256 tiles would leave
-  // at least SK_MIN_KSTEPS K-steps' worth of the chip idle: the last full round and the partial
-  // one are split evenly over one workgroup per CU (the partial-tile slabs and the tiles'
-  // ticket counters in the workspace; counters zeroed by a memset ahead of the launch)
-  if (big && a_kmajor && b_kmajor && batch == 1 && p.splitk == 1 && epi && epi->workspace && sk_enabled()) {
-    const int64_t cus = device_cus();
-    const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n, nk = K / 64, rem = tiles % cus;
-    const double idle = (double)(cus - rem) / (double)cus;  // of the last round (tiles < cus: rem = tiles)
-    int64_t dp = tiles - rem - cus;
-    if (dp < 0) dp = 0;
-    const int64_t U = (tiles - dp) * nk;
-    const int64_t need = 2 * cus * SK_SLAB_FLOATS_HOST + (tiles - dp);
-    if (cus > 0 && rem > 0 && (double)nk * idle >= SK_MIN_KSTEPS && U >= 2 * cus && need <= epi->workspace_floats) {
-      p.sk_dp = (int)dp;
-      p.sk_wgs = (int)cus;
-      p.ws = epi->workspace;
-      p.sk_cnt = (int*)(epi->workspace + 2 * cus * SK_SLAB_FLOATS_HOST);
-      (void)hipMemsetAsync(p.sk_cnt, 0, sizeof(int) * (size_t)(tiles - dp), s);
-    }
-  }
   bool timed;
   std::pair<hipEvent_t, hipEvent_t> ev;
   {

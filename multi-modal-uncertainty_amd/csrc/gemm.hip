@@ -699,143 +699,6 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p) {
   gemm_big_body<AK, BKM, EPI, OUT_F32, 0>(p);
 }
 
-// ---------------------------------------------------------------- big, stream-K tail
-// The big tiles of a product whose last round of workgroups would leave most CUs idle (1539
-// tiles of the N = 768 BERT products at batch 256 = 6 rounds of 256 + 3 tiles; 195 tiles at
-// batch 32): workgroups 0 .. sk_dp-1 take whole tiles as gemm_big_kernel does (dynamic
-// dispatch), and the last sk_wgs workgroups (one per CU) split the remaining tiles' K-steps
-// evenly -- workgroup s runs units [s U / S, (s+1) U / S) of the U = tiles x K-steps, crossing
-// tile boundaries.  A tile split between workgroups: every contributor stores its raw f32
-// partial (lane-linear, 256 KiB) in its own slab, releases it (agent scope) and takes a ticket
-// on the tile's counter; the last arriver acquires, sums the partials in contributor order
-// (deterministic whatever the arrival order) and runs the tile's epilogue.  No workgroup waits
-// for another (no deadlock under any dispatch order).  Both operands K-major, batch 1, no
-// split-K; the host sizes the split so that U >= 2 S (no empty ranges).
-static __device__ __forceinline__ void kmaj_tile(const GemmParams& p, int64_t m0, int64_t n0, int64_t kb, int64_t ke,
-                                                 f32x4 (&acc)[4][8], char* smem, int w, int wm, int wn, int l) {
-  const __amdgpu_buffer_rsrc_t ra =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, (int)(uint32_t)(p.M * p.lda * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.B, 0, (int)(uint32_t)(p.N * p.ldb * 2), 0x00020000);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nk = (int)((ke - kb) / BKT);
-  dma_tile<true>(smem, ra, p.lda, m0, kb, w, l);
-  dma_tile<true>(smem + B_TILE, rb, p.ldb, n0, kb, w, l);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* sa = smem + (kt & 1) * B_STAGE;
-    const char* sb = sa + B_TILE;
-    if (kt + 1 < nk) {
-      char* d = smem + ((kt + 1) & 1) * B_STAGE;
-      const int64_t k1 = kb + (int64_t)(kt + 1) * BKT;
-      dma_tile<true>(d, ra, p.lda, m0, k1, w, l);
-      dma_tile<true>(d + B_TILE, rb, p.ldb, n0, k1, w, l);
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 fb[4], fa[8];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fb[i] = s_frag<true, 512>(sb, 64 * wn + 16 * i, ks, l);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) fa[j] = s_frag<true, 512>(sa, 128 * wm + 16 * j, ks, l);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-}
-
-constexpr int SK_SLAB_FLOATS = 8 * 32 * 64 * 4;  // one workgroup's 256 x 256 f32 partial, lane-linear
-
-// the workgroup of the stream-K range that contains unit x: the largest s with floor(s U / S) <= x
-static __device__ __forceinline__ int sk_owner(int64_t x, int64_t U, int S) { return (int)(((x + 1) * S + U - 1) / U) - 1; }
-
-template <int EPI, bool OUT_F32>
-__global__ __launch_bounds__(512) void gemm_sk_kernel(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * B_STAGE];
-  const int t = threadIdx.x, l = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wm = w >> 2, wn = w & 3;
-  const int lin = (int)blockIdx.x;
-  f32x4 acc[4][8];
-  int tm, tn;
-  if (lin < p.sk_dp) {  // a whole tile
-    tile_of(xcd_remap(lin, p.sk_dp), p.tiles_m, p.tiles_n, p.group_m, tm, tn);
-    const int64_t m0 = (int64_t)tm * BBM, n0 = (int64_t)tn * BBN;
-    kmaj_tile(p, m0, n0, 0, p.K, acc, smem, w, wm, wn, l);
-    epilogue_block<EPI, OUT_F32, 8>(p, 0, 0, m0 + 128 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
-    return;
-  }
-  const int S = p.sk_wgs, s = lin - p.sk_dp;
-  const int64_t nk = p.K / BKT;
-  const int64_t U = (int64_t)(p.tiles_m * p.tiles_n - p.sk_dp) * nk;
-  const int64_t u0 = (int64_t)s * U / S, u1 = (int64_t)(s + 1) * U / S;
-  int* flag = (int*)(smem + 2 * B_STAGE - 16);
-  for (int64_t u = u0; u < u1;) {
-    const int tau = (int)(u / nk);
-    const int64_t tb = (int64_t)tau * nk, te = tb + nk, e = u1 < te ? u1 : te;
-    tile_of(p.sk_dp + tau, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
-    const int64_t m0 = (int64_t)tm * BBM, n0 = (int64_t)tn * BBN;
-    kmaj_tile(p, m0, n0, (u - tb) * BKT, (e - tb) * BKT, acc, smem, w, wm, wn, l);
-    if (u == tb && e == te) {
-      epilogue_block<EPI, OUT_F32, 8>(p, 0, 0, m0 + 128 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
-    } else {
-      const int s_first = sk_owner(tb, U, S), s_last = sk_owner(te - 1, U, S);
-      const int nc = s_last - s_first + 1;
-      // slab (s', 0) holds s''s partial of its first tile, (s', 1) of its last one
-      auto slab = [&](int sc) {
-        const int which = (int)(((int64_t)sc * U / S) / nk) == tau ? 0 : 1;
-        return p.ws + ((int64_t)sc * 2 + which) * SK_SLAB_FLOATS;
-      };
-      float* mine = slab(s);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) *(f32x4*)(mine + ((w * 32 + i * 8 + j) * 64 + l) * 4) = acc[i][j];
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (t == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int old = __hip_atomic_fetch_add(p.sk_cnt + tau, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *(volatile int*)flag = old == nc - 1;
-      }
-      __syncthreads();
-      const int last = *(volatile int*)flag;
-      if (last) {
-        if (t == 0) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();  // (also: every wave has read the flag before the epilogue reuses the LDS)
-        // the contributors' partials summed in contributor order, this one's included (read
-        // back from its slab), so the result does not depend on which contributor came last
-        for (int c = 0; c < nc; ++c) {
-          const float* src = slab(s_first + c);
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const f32x4 v = *(const f32x4*)(src + ((w * 32 + i * 8 + j) * 64 + l) * 4);
-              acc[i][j] = c == 0 ? v : acc[i][j] + v;
-            }
-        }
-        epilogue_block<EPI, OUT_F32, 8>(p, 0, 0, m0 + 128 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
-      }
-    }
-    __syncthreads();  // the epilogue's LDS is the next tile's staging
-    u = e;
-  }
-}
-
 // dW[co][tap][ci] (+)= sum over pixels dY[pixel][co] * X[pixel shifted by tap][ci]
 __global__ __launch_bounds__(512) void gemm_convw_kernel(GemmParams p) {
   gemm_big_body<false, false, MMU_EPI_STORE, true, 1>(p);
@@ -882,9 +745,7 @@ void conv3x3_wgrad_launch(const GemmParams& p, hipStream_t s) {
 template <bool AK, bool BKM, int EPI, bool F32>
 static void launch_t(const GemmParams& p, bool big, int batch, hipStream_t s) {
   dim3 grid(p.tiles_m * p.tiles_n, p.splitk, batch);
-  if (big && AK && BKM && p.sk_wgs > 0) {
-    hipLaunchKernelGGL((gemm_sk_kernel<EPI, F32>), dim3(p.sk_dp + p.sk_wgs), dim3(512), 0, s, p);
-  } else if (big) {
+  if (big) {
     hipLaunchKernelGGL((gemm_big_kernel<AK, BKM, EPI, F32>), grid, dim3(512), 0, s, p);
   } else {
     hipLaunchKernelGGL((gemm_small_kernel<AK, BKM, EPI, F32>), grid, dim3(256), 0, s, p);

@@ -18,10 +18,6 @@ struct GemmParams {
   int64_t lda, ldb, ldc, M, N, K, sA, sB, sC;
   int tiles_m, tiles_n;
   int group_m;  // tile-order group height (gemm.hip tile_of)
-  // stream-K tail (gemm_sk_kernel; sk_wgs = 0: off): whole-tile workgroups, stream-K workgroups,
-  // the stream-K tiles' ticket counters (zeroed before the launch); partial slabs in ws
-  int sk_dp, sk_wgs;
-  int* sk_cnt;
   // epilogue (flattened mmu_epilogue)
   int kind, accumulate;
   const float* bias;

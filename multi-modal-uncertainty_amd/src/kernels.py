@@ -62,8 +62,7 @@ def epilogue(kind=EPI_STORE, bias=None, residual=None, aux=None, colsum=None, dr
     return e
 
 
-SPLITK_WS_FLOATS = 36 << 20  # 144 MiB per (device, stream), reused stream-ordered by every split-K product
-# and by the stream-K tails of the big K-major products (2 x 256 KiB partial slabs per CU + counters)
+SPLITK_WS_FLOATS = 16 << 20  # 64 MiB per (device, stream), reused stream-ordered by every split-K product
 _ws = {}
 _side = {}
 

@@ -318,13 +318,11 @@ def test_gemm_many_tiles_every_element(dev, ak, bk):
 
 @pytest.mark.parametrize("M,N,Kd", [(256 * 257, 768, 3072), (16416, 768, 3072), (16416, 3072, 768),
                                      (256 * 65 + 32, 768, 2304)])
-def test_gemm_stream_k_tail(dev, M, N, Kd):
-    """The stream-K tail (csrc/gemm.hip gemm_sk_kernel; on by default): the last round of
-    256 x 256 tiles split over one workgroup per CU, split tiles summed from partial slabs by
-    their last-arriving contributor.  Shapes: batch 256's N = 768 class (771 tiles = 3 rounds
-    + 3), batch 32's (195 / 780 tiles for 256 CUs) and a 32-row M tail.  Every element of every
-    epilogue against torch, and bitwise-equal results from two runs (the contributor-order sum
-    does not depend on which workgroup arrives last)."""
+def test_gemm_tail_round_shapes(dev, M, N, Kd):
+    """The tile counts of the BERT products whose last round of 256 x 256 tiles is nearly empty:
+    batch 256's N = 768 class (771 tiles = 3 rounds + 3), batch 32's (195 / 780 tiles for 256
+    CUs) and a 32-row M tail (round 5's stream-K tail ran these; profiles/r5_streamk_keepin_ab.txt).
+    Every element of every epilogue against torch, and bitwise-equal results from two runs."""
     k = K()
     A, B = rnd(M, Kd, dev=dev, seed=141), rnd(N, Kd, dev=dev, seed=142, scale=0.1)
     ref = A.float() @ B.float().t()
