@@ -163,7 +163,7 @@ static __device__ __forceinline__ void block_coords(int& bx, int& bh) {
 // ---------------------------------------------------------------- forward ring geometry
 constexpr int FWD_NS = 2;                      // K/V ring depth (tiles)
 constexpr int FWD_TILE = 64 * 128;             // 64 keys x 64 d bf16
-constexpr int FWD_STAGE = 2 * FWD_TILE + 256 + 4 * 256;  // K tile, V tile, key-mask row, 4 waves x 32 keep words
+constexpr int FWD_STAGE = 2 * FWD_TILE + 256;  // K tile, V tile, key-mask row
 constexpr int FWD_MAX_NKV = 9;                 // L <= 576 (BERT: 512 text + image tokens)
 
 // ---------------------------------------------------------------- forward v2 (lean softmax)
@@ -237,11 +237,8 @@ static __device__ __forceinline__ void drop_pair_apply(uint32_t hsh, uint32_t th
 }
 
 // STORE = false: dropout without the keep-bit words (p.dropmask ignored): MC-dropout
-// inference, where no backward reads them; fewer live registers -> 3 waves / SIMD.
-// KEEPIN: training dropout from keep words attn_keep_kernel wrote into p.dropmask ahead of the
-// launch (DMA'd with the K / V tiles, 4 B per lane like dQ's): no hash in the exponent loop,
-// no keep bits to collect and store.
-template <bool DROP, int WPE, bool NOHOIST, bool STORE = true, bool KEEPIN = false>
+// inference, where no backward reads them; fewer live registers -> 3 waves / SIMD
+template <bool DROP, int WPE, bool NOHOIST, bool STORE = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void attn_fwd_v2_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) char smem[FWD_NS * FWD_STAGE + 4 * 32 * FWD_MAX_NKV * 8];
   uint64_t* kbuf_all = (uint64_t*)(smem + FWD_NS * FWD_STAGE);
@@ -257,7 +254,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const uint32_t thr = drop_thr(p.drop_p), thr_hi = thr << 16;
   const int nkv = (L + 63) / 64;
   uint64_t* kbuf = kbuf_all + w * 32 * nkv;
-  const bool store_bits = STORE && DROP && !KEEPIN && p.dropmask != nullptr;
+  const bool store_bits = STORE && DROP && p.dropmask != nullptr;
   // dropout counter base of row q: seed_bh + 4 (q nkv) + 2h  (+ 4j + s2 per tile half)
   const uint32_t ctr = seed_for(mmu_eff_seed(p.seed, p.seed_off), bh) + 4u * (uint32_t)q * (uint32_t)nkv + 2u * (uint32_t)h;
 
@@ -290,11 +287,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     kv_off[pc] = (uint32_t)((key * p.ld_qkv + (w < 2 ? HD : 2 * HD) + hd * 64 + 8 * c) * 2);
   }
   const uint32_t m_off = (uint32_t)(16 * l);
-  // KEEPIN: the keep words of this wave's 32 query rows for the tile (row q0w + l/2, low / high
-  // half by lane parity; rows past L read as zero through the buffer range)
-  const void* k_base = KEEPIN ? (const void*)(p.dropmask + (int64_t)bh * L * nkv) : nullptr;
-  const int k_bytes = KEEPIN ? L * nkv * 8 : 0;
-  const uint32_t kw_off = (uint32_t)(((q0w + (l >> 1)) * nkv * 8) + 4 * (l & 1));
   auto issue = [&](int j) {
     char* st = smem + (j % FWD_NS) * FWD_STAGE;
     const int k0 = j * 64;
@@ -303,7 +295,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
     for (int pc = 0; pc < 4; ++pc) dma16(rt, dst + (4 * (w & 1) + pc) * 1024, kv_off[pc]);
     if (w == 0 && l < 16) dma16(urs_at(m_base, L * 4, k0 * 4), st + 2 * FWD_TILE, m_off);
-    if (KEEPIN) dma4(urs_at(k_base, k_bytes, j * 8), st + 2 * FWD_TILE + 256 + w * 256, kw_off);
   };
   auto wait_for = [&](int ahead) {
     if (w == 0) {
@@ -384,16 +375,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         sc[s2][i] = e;
         lsum[i & 3] += e;
       }
-      if (KEEPIN) {
-        // bit 32 s2 + 16 h + r of the row's word keeps register r of sc[s2]: an all-ones /
-        // zero mask (v_bfe_i32) ANDed into the exponential (the undropped value stays in lsum)
-        const uint32_t* kwords = (const uint32_t*)(st + 2 * FWD_TILE + 256 + w * 256);
-        const uint32_t w32 = kwords[2 * (l & 31) + s2] >> (16 * h);
-        static_for([&](auto rr) {
-          constexpr int r = decltype(rr)::value;
-          sc[s2][r] = __uint_as_float(keepmask<r>(w32) & __float_as_uint(sc[s2][r]));
-        }, std::make_integer_sequence<int, 16>{});
-      } else if (DROP) {
+      if (DROP) {
         // one full hash per (row, tile, half, half-wave); its 8 pairs' 32-bit draws come
         // from pair_draw (3 full-rate VALU per pair instead of a 7-VALU hash)
         const uint32_t hb = lowbias32(c0 + (uint32_t)s2);
@@ -482,56 +464,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
 }
 
-// The training forward's keep words ahead of it: word (bh, q, j) bit 32 s2 + 16 h + r = the keep
-// decision attn_fwd_v2_kernel's hash path draws for register r of sc[s2] of half-wave h (key
-// 64 j + 32 s2 + 16 h + r, before the LDS key permutation): the same counters, pair draws and
-// bit order, so either forward (and the dQ / dK-dV kernels, which read the words) agrees.
-// One thread per word: 4 block hashes + 32 pair draws.
-__global__ __launch_bounds__(256) void attn_keep_kernel(AttnParams p) {
-  const int L = p.L, nkv = (L + 63) / 64;
-  const int bh = blockIdx.y;
-  const int idx = (int)blockIdx.x * 256 + (int)threadIdx.x;  // (L * nkv <= 576 * 9: 32-bit math)
-  if (idx >= L * nkv) return;
-  const int q = (int)((uint32_t)idx / (uint32_t)nkv), j = idx - q * nkv;
-  const uint32_t thr = drop_thr(p.drop_p), thr_hi = thr << 16;
-  const uint32_t base = seed_for(mmu_eff_seed(p.seed, p.seed_off), bh) + 4u * (uint32_t)q * (uint32_t)nkv +
-                        4u * (uint32_t)j;
-  uint64_t word = 0;
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const uint32_t hb = lowbias32(base + 2u * (uint32_t)h + (uint32_t)s2);
-      uint32_t field = 0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint32_t hsh = pair_draw(hb, i);
-        field |= ((hsh & 0xFFFFu) >= thr ? 1u : 0u) << (2 * i);
-        field |= (hsh >= thr_hi ? 1u : 0u) << (2 * i + 1);
-      }
-      word |= (uint64_t)field << (32 * s2 + 16 * h);
-    }
-  p.dropmask[(int64_t)bh * L * nkv + idx] = word;
-}
-
-static int attn_keep_mode() {  // MMU_ATTN_KEEPIN: 0 = hash in the forward, 2 / 3 = words ahead, 2 / 3 waves per SIMD
-  static const int m = getenv("MMU_ATTN_KEEPIN") ? atoi(getenv("MMU_ATTN_KEEPIN")) : 0;
-  return m;
-}
-
 void attention_fwd_launch(const AttnParams& p, hipStream_t s) {
   dim3 grid((p.L + 127) / 128, p.batch * p.heads);
   if (drop_thr(p.drop_p) && !p.dropmask) {
     // inference dropout (MC-dropout passes): no keep bits to store, 3 waves / SIMD
     hipLaunchKernelGGL((attn_fwd_v2_kernel<true, 3, true, false>), grid, dim3(256), 0, s, p);
-  } else if (drop_thr(p.drop_p) && attn_keep_mode()) {
-    const int nkv = (p.L + 63) / 64;
-    hipLaunchKernelGGL(attn_keep_kernel, dim3((unsigned)(((int64_t)p.L * nkv + 255) / 256), p.batch * p.heads),
-                       dim3(256), 0, s, p);
-    if (attn_keep_mode() == 3)
-      hipLaunchKernelGGL((attn_fwd_v2_kernel<true, 3, false, false, true>), grid, dim3(256), 0, s, p);
-    else
-      hipLaunchKernelGGL((attn_fwd_v2_kernel<true, 2, false, false, true>), grid, dim3(256), 0, s, p);
   } else if (drop_thr(p.drop_p)) {
     // training dropout at 2 waves / SIMD (at the 3-wave register cap it spills lane-constant
     // LDS addresses around the loop: 0.89 vs 0.59 ms at B = 256, L = 513, p = 0.1)
