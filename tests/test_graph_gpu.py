@@ -7,7 +7,9 @@
   dropout, backward with the deferred side-stream weight gradients, fused BertAdam) equals the
   eager step run with the same host-drawn seeds and the same counter value, step after step
   (loss to 1e-5; the parameters after 4 optimizer steps to 1e-4 of their update, without the
-  attention key biases, whose zero gradient BertAdam turns into sign-of-noise steps);
+  attention key biases, whose zero gradient BertAdam turns into sign-of-noise steps; on the
+  full model, whose float-atomic gradient sums differ from run to run, within 3x of the eager
+  step's own run-to-run spread, measured in the test);
   consecutive replays draw new masks.
 Model: the small MMBT (2 BERT layers, one Bottleneck per stage), batch 8, in training mode
 (batch-statistic BatchNorm), the reference's step (src/framework.py:276-304)."""
@@ -19,14 +21,15 @@ pytestmark = pytest.mark.gpu
 B, T, P = 8, 16, 0.1
 
 
-def _model(sd=None):
-    from oracle.weights import SMALL, make_state_dict
+def _model(sd=None, full=False):
+    from oracle.weights import FULL_C, SMALL, make_state_dict
     from src.mmbt import MultimodalBertClf
     from src.optim import BertAdam
-    from src.testing import small_args
+    from src.testing import make_args, small_args
     torch.manual_seed(0)
-    m = MultimodalBertClf(small_args(bert_hidden_dropout=P, bert_attn_dropout=P, dropout=P))
-    m.load_state_dict(sd if sd is not None else make_state_dict(0, SMALL), strict=True)
+    mk = make_args if full else small_args
+    m = MultimodalBertClf(mk(bert_hidden_dropout=P, bert_attn_dropout=P, dropout=P))
+    m.load_state_dict(sd if sd is not None else make_state_dict(0, FULL_C if full else SMALL), strict=True)
     m = m.to("cuda:0").train()
     named = list(m.named_parameters())
     nd = ["bias", "LayerNorm.bias", "LayerNorm.weight"]
@@ -35,10 +38,13 @@ def _model(sd=None):
     return m, BertAdam(groups, lr=1e-5, warmup=0.1, t_total=20.0)
 
 
-def _batch():
+def _batch(full=False):
     from oracle.weights import SMALL
     from src.testing import synthetic_batch
-    x, y = synthetic_batch(B, T, vocab=SMALL.vocab, lens=[16, 9, 16, 12, 5, 16, 14, 16], seed=4)
+    if full:  # BASELINE config 4's per-rank shapes at a small batch: L = 513
+        x, y = synthetic_batch(4, 508, lens=[508, 300, 508, 77], seed=4)
+    else:
+        x, y = synthetic_batch(B, T, vocab=SMALL.vocab, lens=[16, 9, 16, 12, 5, 16, 14, 16], seed=4)
     return tuple(t.to("cuda:0") for t in x), y.to("cuda:0")
 
 
@@ -81,12 +87,15 @@ def test_seed_counter_zero_is_the_eager_draw(dev):
     assert rel(g2, g0) > max(30 * noise, 1e-2)
 
 
-def test_graph_replay_equals_eager_steps(dev):
+@pytest.mark.parametrize("full", [False, True])
+def test_graph_replay_equals_eager_steps(dev, full):
+    """full: ResNet-152 + 12 BERT layers at L = 513, batch 4 (MIOpen convs, the side stream's
+    deferred weight gradients and the trunk's residual-stream residue inside the capture)."""
     from src import kernels as K
     torch.backends.cudnn.deterministic = True
     from src.graphs import StepGraph
-    x, y = _batch()
-    ma, oa = _model()
+    x, y = _batch(full)
+    ma, oa = _model(full=full)
     sd0 = {k: v.detach().cpu().clone() for k, v in ma.state_dict().items()}
     torch.manual_seed(21)
     g = StepGraph(_stepper(ma, oa, x, y), dev, warmup=1)
@@ -101,38 +110,53 @@ def test_graph_replay_equals_eager_steps(dev):
     g.release()
     del g
 
-    mb, ob = _model(sd0)
-    flat0 = mb.store.flat.clone()
-    step_b = _stepper(mb, ob, x, y)
-    ctr = torch.zeros(1, dtype=torch.int64, device=dev)
-    K.set_seed_offset(ctr)
-    try:
-        torch.manual_seed(21)
-        ctr.fill_(1)
-        step_b()  # = StepGraph's eager warmup step (counter 1)
-        rng = torch.get_rng_state()  # the capture drew its seeds from here
-        losses_b = []
-        for k in range(3):
-            torch.set_rng_state(rng)
-            ctr.fill_(2 + k)  # the replay's first node advanced the counter to 2, 3, 4
-            losses_b.append(step_b().item())
-        torch.cuda.synchronize()
-    finally:
-        K.set_seed_offset(None)
-    flat_b = mb.store.flat
-    # without the key biases: their true gradient is 0 (softmax shift invariance), so BertAdam
-    # moves them by the sign of float-atomic noise, which differs with the kernels' overlap
-    keep = torch.ones_like(flat_b, dtype=torch.bool)
-    for n in mb.store.names:
-        if n.endswith("attention.self.key.bias"):
-            keep[mb.store.offsets[n]:mb.store.offsets[n] + mb.store.params[n].numel()] = False
-    d = ((flat_a - flat_b)[keep].norm() / (flat_b - flat0)[keep].norm()).item()  # relative to the 4 steps' update
+    def eager():
+        """the eager arm: the StepGraph's warm-up step, then 3 steps with the capture's host
+        seeds and the counter values the replays ran with"""
+        mb, ob = _model(sd0, full=full)
+        flat0 = mb.store.flat.clone()
+        step_b = _stepper(mb, ob, x, y)
+        ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        K.set_seed_offset(ctr)
+        try:
+            torch.manual_seed(21)
+            ctr.fill_(1)
+            step_b()  # = StepGraph's eager warmup step (counter 1)
+            rng = torch.get_rng_state()  # the capture drew its seeds from here
+            losses = []
+            for k in range(3):
+                torch.set_rng_state(rng)
+                ctr.fill_(2 + k)  # the replay's first node advanced the counter to 2, 3, 4
+                losses.append(step_b().item())
+            torch.cuda.synchronize()
+        finally:
+            K.set_seed_offset(None)
+        # without the key biases: their true gradient is 0 (softmax shift invariance), so BertAdam
+        # moves them by the sign of float-atomic noise
+        keep = torch.ones_like(flat0, dtype=torch.bool)
+        for n in mb.store.names:
+            if n.endswith("attention.self.key.bias"):
+                keep[mb.store.offsets[n]:mb.store.offsets[n] + mb.store.params[n].numel()] = False
+        out = (losses, mb.store.flat.clone(), flat0, keep)
+        del mb, ob
+        torch.cuda.empty_cache()
+        return out
+
+    losses_b, flat_b, flat0, keep = eager()
+    rel = lambda u, v: ((u - v)[keep].norm() / (v - flat0)[keep].norm()).item()  # noqa: E731  (of the update)
+    d = rel(flat_a, flat_b)
     moved = (flat_b - flat0).norm().item()
-    print(f"\n[graph] replay losses {losses_a}, eager {losses_b}; counter {ctr_a}; params after 4 steps: diff / update {d:.2e} "
+    # the floor: the eager step against itself (float-atomic summation order: bias-gradient
+    # column sums, embedding-row gradients), which BertAdam amplifies on near-zero gradients
+    losses_c, flat_c, _, _ = eager()
+    d_ee = rel(flat_c, flat_b)
+    l_ee = max(abs(a - b) for a, b in zip(losses_c, losses_b))
+    print(f"\n[graph{' full' if full else ''}] replay losses {losses_a}, eager {losses_b}, eager again {losses_c}; "
+          f"counter {ctr_a}; params after 4 steps: replay vs eager {d:.2e}, eager vs eager {d_ee:.2e} of the update "
           f"(moved {moved:.3e})")
     assert ctr_a == 4
     for a, b in zip(losses_a, losses_b):
-        assert abs(a - b) <= 1e-5 * abs(b), (losses_a, losses_b)
+        assert abs(a - b) <= max(1e-5 * abs(b), 3 * l_ee), (losses_a, losses_b, losses_c)
     assert len(set(losses_a)) == 3, "consecutive replays drew the same dropout masks"
     assert moved > 0
-    assert d <= 1e-4, d
+    assert d <= max(1e-4, 3 * d_ee), (d, d_ee)
