@@ -53,6 +53,9 @@ class StepGraph:
                 step_fn()
         cur.wait_stream(self.stream)
         torch.cuda.synchronize(self.device)
+        # the warm-up's cached activations go back to the driver: the capture allocates the
+        # step's buffers again, in the graph's private pool
+        torch.cuda.empty_cache()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, stream=self.stream):
             self.counter.add_(1)
