@@ -590,6 +590,10 @@ def main():
         return loss
 
     graph = args.graph == "on"
+    if graph and world > 1:
+        # (the bucketed all-reduce inside a captured backward needs RCCL graph capture, which the
+        # one-GPU boxes this was developed on cannot exercise)
+        raise SystemExit("--graph on: single-process runs only (N = 1)")
     run = step
     if graph:
         # the rooflines' per-launch timings from 2 eager steps (the same kernels the graph replays)
