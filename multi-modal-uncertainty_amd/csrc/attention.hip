@@ -391,6 +391,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
+        // (partial tile: keys 8-15 and 24-31 of the half all past L -- L = 513 -- skip their
+        // P V step: their P is exactly 0)
+        if (PARTIAL && u == 1 && 64 * j + 32 * s2 + 8 >= L) break;
         const bf16x8 pf = acc_frag(sc[s2], u);
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt)
@@ -637,6 +640,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void a
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
+        // a last query tile whose live rows all sit in its first 16 (L = 513: one) skips the
+        // second 16: their Q / dO rows are the zeros past L, which add exactly nothing
+        if (s2 == 1 && 32 * i + 16 >= L) break;
         bf16x8 pf = acc_frag(pz, s2), sf = acc_frag(sc, s2);
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
@@ -817,6 +823,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
       const uint64_t kwh = kw >> (4 * h);
 #pragma unroll
       for (int st2 = 0; st2 < 2; ++st2) {
+        // a last tile whose live keys all sit in its first half (L = 513: one) skips the second:
+        // its K / V rows are the zeros past L, which add exactly nothing to dQ
+        if (st2 == 1 && 64 * j + 32 >= L) break;
         const uint32_t kw32 = (uint32_t)(kwh >> (32 * st2));
         // S starts at the mask: register r holds key kl = 32 st2 + 8 (r >> 2) + 4 h + (r & 3),
         // so each group of 4 registers takes 4 contiguous mask entries (one f32x4 read)

@@ -559,10 +559,11 @@ def test_attention_dropout_consistent(dev):
         k.attention_bwd(qkv, km, O, dO, lse, delta, dqkv, B, L, drop_p=p, seed=seed)
 
 
-@pytest.mark.parametrize("B,L", [(2, 200), (1, 321)])
+@pytest.mark.parametrize("B,L", [(2, 200), (1, 321), (2, 280)])
 def test_attention_dropout_multiword(dev, B, L):
     """L > 64: several keep words per query row; fwd and bwd against autograd with the
-    mask decoded from the emitted bits, plus the drop rate."""
+    mask decoded from the emitted bits, plus the drop rate.  L = 280: 24 query rows past the
+    last 128-row block and 24 keys past the last 64-key block (the one-wave TAIL kernels)."""
     k = K()
     p, seed = 0.1, 1234
     qkv, km = make_attn_inputs(dev, B, L, pad=True, seed=11, scale=1.0)
