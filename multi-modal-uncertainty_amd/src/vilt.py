@@ -35,9 +35,11 @@ def _f32(t, dev):
 
 
 def patch_mask(pixel_mask, gh, gw):
-    """[B, H, W] pixel mask -> [B, gh, gw] long patch mask (nearest), on the host
-    (ViltEmbeddings.visual_embed's x_mask)"""
-    return F.interpolate(pixel_mask[:, None].float().cpu(), size=(gh, gw)).long()[:, 0]
+    """[B, H, W] pixel mask -> [B, gh, gw] long patch mask (nearest: pixel (i H / gh, j W / gw)),
+    returned on the host (ViltEmbeddings.visual_embed's x_mask).  The sampling runs where the
+    mask lives and only the patch grid crosses to the host (copying the full-resolution mask
+    was 11 ms of a 22 ms batch-128 step, tools/vilt_profile.py)."""
+    return F.interpolate(pixel_mask[:, None].float(), size=(gh, gw)).long()[:, 0].cpu()
 
 
 def image_length(xm, max_image_length):
@@ -58,6 +60,15 @@ def select_patches(xm, max_len):
     patches ([B * max_len]) and their mask values [B, max_len]."""
     B, P = xm.shape
     n_valid = xm.sum(1)
+    nv0 = int(n_valid[0])
+    if 0 < max_len <= nv0 and bool((n_valid == nv0).all()):
+        # every sample keeps max_len of its nv0 valid patches: the B per-sample draws in one
+        # [B, nv0] multinomial call, which consumes the generator exactly as the B calls in
+        # sample order do (tests/test_vilt.py checks the two against each other)
+        v = xm.nonzero(as_tuple=False)[:, 1].view(B, nv0)
+        pick = torch.gather(v, 1, torch.multinomial(torch.ones(B, nv0).float(), max_len))
+        flat = (pick + torch.arange(B).unsqueeze(1) * P).flatten()
+        return flat, xm.flatten()[flat].view(B, -1)
     v_all = torch.split(xm.nonzero(as_tuple=False)[:, 1], n_valid.tolist())
     nv_all = torch.split((1 - xm).nonzero(as_tuple=False)[:, 1], (P - n_valid).tolist())
     sel = []

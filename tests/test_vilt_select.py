@@ -46,3 +46,35 @@ def test_patch_selection_matches_visual_embed(max_image_length, partial):
     with torch.no_grad():
         emb.visual_embed(pix, pmask, max_image_length=max_image_length)
     assert torch.equal(after, torch.rand(4))  # ... is where the reference leaves it
+
+
+@pytest.mark.parametrize("max_image_length", [-1, 100])
+def test_batched_draws_match_visual_embed_at_bench_shape(max_image_length):
+    """bench.py --workload vilt's shape (64 full 384 x 384 images, 144 patches each): every
+    sample keeps max_len of an equal number of valid patches, which select_patches draws with
+    ONE [B, 144] multinomial call -- the same patches, and the generator left in the same state,
+    as visual_embed's 64 per-sample calls"""
+    from transformers import ViltConfig
+    from transformers.models.vilt.modeling_vilt import ViltEmbeddings
+    from src.vilt import image_length, patch_mask, select_patches
+    torch.manual_seed(0)
+    cfg = ViltConfig(image_size=384, patch_size=32, hidden_size=32, num_attention_heads=2, intermediate_size=32,
+                     num_hidden_layers=1, max_image_length=max_image_length)
+    emb = ViltEmbeddings(cfg).eval()
+    B = 64
+    pix = torch.randn(B, 3, 384, 384, generator=torch.Generator().manual_seed(2))
+    pmask = torch.ones(B, 384, 384, dtype=torch.long)
+    torch.manual_seed(7)
+    with torch.no_grad():
+        _, ref_mask, (ref_idx, _) = emb.visual_embed(pix, pmask, max_image_length=max_image_length)
+    ref_after = torch.rand(4)
+    torch.manual_seed(7)
+    xm = patch_mask(pmask, 12, 12)
+    L = image_length(xm, max_image_length)
+    flat, mask = select_patches(xm.flatten(1), L)
+    after = torch.rand(4)
+    p = flat % 144
+    got_idx = torch.stack([p // 12, p % 12], -1).view(B, -1, 2)
+    assert torch.equal(got_idx, ref_idx[:, 1:] if ref_idx.shape[1] == L + 1 else ref_idx)
+    assert torch.equal(mask, ref_mask[:, 1:])
+    assert torch.equal(after, ref_after)
