@@ -787,7 +787,16 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   const int64_t e = q * 4, m = e / N, n = e - m * N;
   const float* s = ws + z * splitk * M * N + e;
   float4 a = *(const float4*)s;
-  for (int k = 1; k < splitk; ++k) {
+  // 4 slabs' loads in flight per thread, added in slice order
+  int k = 1;
+  for (; k + 4 <= splitk; k += 4) {
+    float4 b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) b[u] = *(const float4*)(s + (k + u) * M * N);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { a.x += b[u].x; a.y += b[u].y; a.z += b[u].z; a.w += b[u].w; }
+  }
+  for (; k < splitk; ++k) {
     const float4 b = *(const float4*)(s + k * M * N);
     a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
   }
