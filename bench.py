@@ -18,6 +18,7 @@ per rank instead ("scaling": "weak"; DESIGN.md §6 has both).
   python bench.py --workload encoders  BASELINE config 5's producer: the FLAVA image + text
                                        encoders (data/encoding_with_flava.py) on HIP kernels
   python bench.py --workload vilt      ViLT classification inference (train.py setup_vilt model)
+  python bench.py --workload vilt_train   ViLT classification training step (forward, backward, AdamW)
 
 Rank 0 prints one JSON line (see README/DESIGN for the field definitions).
 """
@@ -70,7 +71,8 @@ def parse():
                          "before the capture)")
     ap.add_argument("--no-stream-residue", action="store_true",
                     help="mmbt: the trunk's residual stream in plain bf16 (the round-4 trunk; for same-box A/Bs)")
-    ap.add_argument("--workload", default="mmbt", choices=["mmbt", "flava", "uncertainty", "encoders", "vilt"])
+    ap.add_argument("--workload", default="mmbt",
+                    choices=["mmbt", "flava", "uncertainty", "encoders", "vilt", "vilt_train"])
     ap.add_argument("--enc-batch", type=int, default=128, help="encoders / vilt: samples per rank per step")
     ap.add_argument("--members", type=int, default=5, help="uncertainty: deep-ensemble members K")
     ap.add_argument("--mc-samples", type=int, default=30, help="uncertainty: MC-dropout passes T")
@@ -424,6 +426,102 @@ def _encoder_cpu_baseline(args, run, B, what):
                       f"torch CPU {torch.get_num_threads()} threads"}
 
 
+def bench_vilt_train(args, world, rank, dev):
+    """The reference's ViLT training step (train.py:164-182 setup_vilt: ViltForImagesAndTextClassification,
+    AdamW over its parameters; src/framework.py:262-300: outputs = model(**batch), loss.backward(),
+    optimizer.step()) on the HIP kernels (src/vilt.py ViltTrainHIP): 384^2 image -> 145 tokens + 40
+    text tokens, B samples per rank.  Random-init weights, synthetic inputs; the gradient
+    all-reduce over ranks (flat, like --workload flava) when N > 1."""
+    from src import kernels as K
+    from src.vilt import ViltTrainHIP
+    from transformers import ViltConfig, ViltForImagesAndTextClassification
+    B = args.enc_batch
+    torch.manual_seed(1234)
+    cfg = ViltConfig(num_images=1, num_labels=2)
+    model = ViltForImagesAndTextClassification(cfg).to(dev).train()
+    if world > 1:
+        for p in model.parameters():
+            dist.broadcast(p.data, 0)
+    hip = ViltTrainHIP(model)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4)
+    params = list(model.parameters())
+    g = torch.Generator().manual_seed(300 + rank)
+    Lt = cfg.max_position_embeddings
+    batch = dict(input_ids=torch.randint(1000, cfg.vocab_size, (B, Lt), generator=g).to(dev),
+                 attention_mask=torch.ones(B, Lt, dtype=torch.long, device=dev),
+                 pixel_values=torch.randn(B, 1, 3, cfg.image_size, cfg.image_size, generator=g).to(dev),
+                 labels=torch.randint(0, 2, (B,), generator=g).to(dev))
+
+    def step():
+        opt.zero_grad()
+        out = hip(**batch)
+        out.loss.backward()
+        if world > 1:
+            grads = [p.grad for p in params]
+            flat = torch._utils._flatten_dense_tensors(grads)
+            dist.all_reduce(flat)
+            flat.mul_(1.0 / world)
+            for gr, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
+                gr.copy_(f)
+        opt.step()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    K.timing_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    gemm_ms, gemm_n, gemm_flop = K.timing_read()
+    K.timing_enable(False)
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    H, L = 768, Lt + (cfg.image_size // cfg.patch_size) ** 2 + 1
+    flop_sample = 3 * cfg.num_hidden_layers * L * (24 * H * H + 4 * L * H)  # forward + backward
+    ms_step = 1000.0 * dt / args.steps
+    gemm_tf = gemm_flop / (gemm_ms * 1e-3) / 1e12 if gemm_ms else 0.0
+    out = {
+        "metric": "ViLT classification train samples/sec (train.py setup_vilt, AdamW)",
+        "value": round(B * world * args.steps / dt, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded images / token ids; random-init weights)",
+        "config": {"workload": "vilt_train", "model": "ViltForImagesAndTextClassification", "per_rank_batch": B,
+                   "global_batch": B * world, "tokens": str(L), "parallelism": f"dp{world}"},
+        "roofline": {"bound": "mfma", "achieved": round(gemm_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(gemm_tf / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "gemm_launches_timed": gemm_n, "gemm_ms_per_step": round(gemm_ms / args.steps, 3)},
+        "model_tflops_achieved": round(flop_sample * B * world / (ms_step * 1e-3) / 1e12, 1),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        ref = ViltForImagesAndTextClassification(cfg).train()
+        ropt = torch.optim.AdamW(ref.parameters(), lr=1e-4)
+        cb = {k: v[:2].cpu() for k, v in batch.items()}
+        torch.set_num_threads(_cpu_threads(args))
+
+        def cpu_step():
+            ropt.zero_grad()
+            ref(**cb).loss.backward()
+            ropt.step()
+        cpu_step()
+        t0 = time.perf_counter()
+        for _ in range(2):
+            cpu_step()
+        cdt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(2 * 2 / cdt, 3), "unit": "samples/s", "cores": _cpu_threads(args),
+                               "kind": "reference", "sample": "transformers ViltForImagesAndTextClassification fp32 "
+                               "train step (forward, backward, AdamW; random init), B=2, 2 timed steps after 1 warm-up, "
+                               f"torch CPU {torch.get_num_threads()} threads"}
+    return out
+
+
 def bench_encoders(args, world, rank, dev):
     """BASELINE config 5's producer (reference data/encoding_with_flava.py:11-41): FLAVA image
     (224^2 -> 197 tokens) + text (77 tokens) encoders of a transformers FlavaModel on the HIP
@@ -521,9 +619,9 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
-    if args.workload in ("flava", "uncertainty", "encoders", "vilt"):
+    if args.workload in ("flava", "uncertainty", "encoders", "vilt", "vilt_train"):
         fn = {"flava": bench_flava, "uncertainty": bench_uncertainty, "encoders": bench_encoders,
-              "vilt": bench_encoders}[args.workload]
+              "vilt": bench_encoders, "vilt_train": bench_vilt_train}[args.workload]
         out = fn(args, world, rank, dev)
         if rank == 0:
             print(json.dumps(out), flush=True)

@@ -21,6 +21,7 @@ The residual stream is f32, GEMM operands bf16 with f32 accumulation.  No CPU pa
 kernels raise on CPU tensors.
 """
 import torch
+import torch.nn as nn
 import torch.nn.functional as F
 
 from . import kernels as K
@@ -217,3 +218,245 @@ class ViltHIP:
         h = F.linear(torch.cat(pooled, -1), w0, b0)
         h = F.gelu(F.layer_norm(h, (h.shape[-1],), lw, lb, eps))
         return F.linear(h, w1, b1)
+
+
+# ---------------------------------------------------------------------------------- training
+# The reference trains ViltForImagesAndTextClassification (train.py:164-182 setup_vilt: AdamW over
+# model.parameters(); src/framework.py:262-300: outputs = model(**batch), outputs.loss.backward()).
+# ViltTrainHIP runs that forward and backward on the HIP kernels with the transformers module as
+# the parameter container (same nn.Parameters, state_dict keys and optimizer target):
+#   text embed    torch (gathers + LayerNorm in f32: 0.1 ms of a step)
+#   patch embed   mmu_gemm (32x32 / 32 patch Conv2d as one GEMM; weight grad mmu_gemm, bias grad
+#                 mmu_colsum), the reference's patch selection / interpolated positions in torch
+#   12 x layer    _ViltLayerFunction: the inference layer (f32 residual stream, bf16 GEMM
+#                 operands) plus its backward -- DGELU-epilogue data grads, f32 weight grads,
+#                 mmu_attention_bwd (+ fused Q/K/V bias grads), mmu_layernorm_bwd_f32; the stream
+#                 gradient stays f32
+#   final LN, pooler, classifier, loss   torch f32 on the [CLS] rows
+class _PatchGemm(torch.autograd.Function):
+    """x = rows W^T + b (f32 out): the patch Conv2d as one GEMM; grads for W and b only (the
+    pixels are data)."""
+
+    @staticmethod
+    def forward(ctx, rows, w, b):
+        M, Kp = rows.shape
+        H = w.shape[0]
+        x = torch.empty(M, H, dtype=torch.float32, device=rows.device)
+        K.gemm(rows, Kp, True, w.reshape(H, -1).to(bf16).contiguous(), Kp, True, x, H, M, H, Kp,
+               epi=K.epilogue(K.EPI_STORE, bias=b.float().contiguous()))
+        ctx.save_for_backward(rows)
+        ctx.wshape = w.shape
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        (rows,) = ctx.saved_tensors
+        M, Kp = rows.shape
+        dxb = dx.contiguous().to(bf16)
+        H = dxb.shape[1]
+        gw = torch.empty(H, Kp, dtype=torch.float32, device=rows.device)
+        K.gemm(dxb, H, False, rows, Kp, False, gw, Kp, H, Kp, M, epi=K.epilogue(K.EPI_STORE))
+        return None, gw.view(ctx.wshape), dx.sum(0)
+
+
+class _ViltLayerFunction(torch.autograd.Function):
+    """One pre-LN ViltLayer (transformers modeling_vilt ViltLayer: x + attn(LN_before(x)), then
+    + FFN(LN_after(.))) on the f32 residual stream X [B*L, H]."""
+
+    @staticmethod
+    def forward(ctx, X, keymask, B, L, heads, eps1, eps2, wq, wk, wv, bq, bk, bv, wo, bo, l1w, l1b, w1, b1, w2, b2,
+                l2w, l2b):
+        M, H = X.shape
+        Fd = w1.shape[0]
+        dev, f32 = X.device, torch.float32
+        Wqkv = torch.cat([wq, wk, wv]).to(bf16).contiguous()
+        bqkv = torch.cat([bq, bk, bv]).float().contiguous()
+        Wo, W1, W2 = (w.to(bf16).contiguous() for w in (wo, w1, w2))
+        h1 = torch.empty(M, H, dtype=bf16, device=dev)
+        m1, r1 = torch.empty(M, dtype=f32, device=dev), torch.empty(M, dtype=f32, device=dev)
+        K.layernorm_fwd_f32(X, l1w, l1b, h1, None, m1, r1, eps=eps1)
+        qkv = torch.empty(M, 3 * H, dtype=bf16, device=dev)
+        K.gemm(h1, H, True, Wqkv, H, True, qkv, 3 * H, M, 3 * H, H, epi=K.epilogue(K.EPI_STORE, bias=bqkv))
+        O = torch.empty(M, H, dtype=bf16, device=dev)
+        lse = torch.empty(B * heads, L, dtype=f32, device=dev)
+        K.attention_fwd(qkv, keymask, O, lse, B, L, heads, 0.0, 0, None)
+        S = torch.empty(M, H, dtype=f32, device=dev)
+        K.gemm(O, H, True, Wo, H, True, S, H, M, H, H, epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=bo, residual=X))
+        h2 = torch.empty(M, H, dtype=bf16, device=dev)
+        m2, r2 = torch.empty(M, dtype=f32, device=dev), torch.empty(M, dtype=f32, device=dev)
+        K.layernorm_fwd_f32(S, l2w, l2b, h2, None, m2, r2, eps=eps2)
+        G = torch.empty(M, Fd, dtype=bf16, device=dev)
+        Z = torch.empty(M, Fd, dtype=bf16, device=dev)  # gelu'(.) for the backward's DGELU epilogue
+        K.gemm(h2, H, True, W1, H, True, G, Fd, M, Fd, H, epi=K.epilogue(K.EPI_BIAS_GELU, bias=b1, aux=Z))
+        Y = torch.empty(M, H, dtype=f32, device=dev)
+        K.gemm(G, Fd, True, W2, Fd, True, Y, H, M, H, Fd, epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=b2, residual=S))
+        ctx.save_for_backward(X, keymask, h1, m1, r1, qkv, O, lse, S, h2, m2, r2, G, Z, Wqkv, Wo, W1, W2, l1w, l2w)
+        ctx.meta = (B, L, heads)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        (X, keymask, h1, m1, r1, qkv, O, lse, S, h2, m2, r2, G, Z, Wqkv, Wo, W1, W2, l1w, l2w) = ctx.saved_tensors
+        B, L, heads = ctx.meta
+        M, H = X.shape
+        Fd = W1.shape[0]
+        dev, f32 = X.device, torch.float32
+        st = K.epilogue(K.EPI_STORE)
+        dY = dY.contiguous().float()
+        dYb = dY.to(bf16)
+        # ---- FFN: Y = S + gelu(LN2(S) W1^T + b1) W2^T + b2
+        g_w2 = torch.empty(H, Fd, dtype=f32, device=dev)
+        K.gemm(dYb, H, False, G, Fd, False, g_w2, Fd, H, Fd, M, epi=st)
+        dZ = torch.empty(M, Fd, dtype=bf16, device=dev)
+        g_b1 = torch.zeros(Fd, dtype=f32, device=dev)
+        K.gemm(dYb, H, True, W2.t().contiguous(), H, True, dZ, Fd, M, Fd, H,
+               epi=K.epilogue(K.EPI_DGELU, aux=Z, colsum=g_b1))
+        g_w1 = torch.empty(Fd, H, dtype=f32, device=dev)
+        K.gemm(dZ, Fd, False, h2, H, False, g_w1, H, Fd, H, M, epi=st)
+        dh2 = torch.empty(M, H, dtype=bf16, device=dev)
+        K.gemm(dZ, Fd, True, W1.t().contiguous(), Fd, True, dh2, H, M, H, Fd)
+        P = K.ln_parts(M)
+        pw, pb = (torch.empty(P, H, dtype=f32, device=dev) for _ in range(2))
+        dln = torch.empty(M, H, dtype=bf16, device=dev)
+        K.layernorm_bwd(dh2, S, m2, r2, l2w, dln, None, 0.0, 0, pw, pb, None)
+        g_l2w, g_l2b = torch.empty(H, dtype=f32, device=dev), torch.empty(H, dtype=f32, device=dev)
+        K.colsum_reduce(pw, g_l2w)
+        K.colsum_reduce(pb, g_l2b)
+        dS = dY + dln.float()  # the stream gradient stays f32
+        dSb = dS.to(bf16)
+        # ---- attention: S = X + attn(LN1(X)) Wo^T + bo
+        g_wo = torch.empty(H, H, dtype=f32, device=dev)
+        K.gemm(dSb, H, False, O, H, False, g_wo, H, H, H, M, epi=st)
+        dO = torch.empty(M, H, dtype=bf16, device=dev)
+        K.gemm(dSb, H, True, Wo.t().contiguous(), H, True, dO, H, M, H, H)
+        dqkv = torch.empty(M, 3 * H, dtype=bf16, device=dev)
+        delta = torch.empty(B * heads, L, dtype=f32, device=dev)
+        parts = K.attention_dbias_parts(B, L, heads, dev)
+        K.attention_bwd(qkv, keymask, O, dO, lse, delta, dqkv, B, L, heads, 0.0, 0, None, parts)
+        g_bqkv = torch.zeros(3 * H, dtype=f32, device=dev)
+        K.attention_dbias_reduce(parts, B, L, g_bqkv, heads)
+        g_wqkv = torch.empty(3 * H, H, dtype=f32, device=dev)
+        K.gemm(dqkv, 3 * H, False, h1, H, False, g_wqkv, H, 3 * H, H, M, epi=st)
+        dh1 = torch.empty(M, H, dtype=bf16, device=dev)
+        K.gemm(dqkv, 3 * H, True, Wqkv.t().contiguous(), 3 * H, True, dh1, H, M, H, 3 * H)
+        pw1, pb1 = (torch.empty(P, H, dtype=f32, device=dev) for _ in range(2))
+        K.layernorm_bwd(dh1, X, m1, r1, l1w, dln, None, 0.0, 0, pw1, pb1, None)
+        g_l1w, g_l1b = torch.empty(H, dtype=f32, device=dev), torch.empty(H, dtype=f32, device=dev)
+        K.colsum_reduce(pw1, g_l1w)
+        K.colsum_reduce(pb1, g_l1b)
+        dX = dS + dln.float()
+        gq, gk, gv = g_wqkv.split(H)
+        gbq, gbk, gbv = g_bqkv.split(H)
+        return (dX, None, None, None, None, None, None, gq, gk, gv, gbq, gbk, gbv, g_wo, dS.sum(0), g_l1w, g_l1b,
+                g_w1, g_b1, g_w2, dY.sum(0), g_l2w, g_l2b)
+
+
+class ViltTrainHIP(nn.Module):
+    """``ViltForImagesAndTextClassification`` forward + backward on the HIP kernels for training
+    (the reference's ``outputs = model(**batch); outputs.loss.backward()``).  ``model`` is the
+    transformers module itself: its parameters are the ones trained (optimize ``model``'s
+    parameters, save ``model.state_dict()``).  ``forward(**batch)`` returns the transformers
+    output type (``loss``, ``logits``).  Dropout-free configurations only (ViltConfig's default
+    hidden / attention-probs dropout is 0.0); the patch selection draws from the global CPU
+    generator in the reference's order (select_patches)."""
+
+    def __init__(self, model):
+        super().__init__()
+        cfg = model.config
+        if cfg.hidden_dropout_prob or cfg.attention_probs_dropout_prob:
+            raise NotImplementedError("ViltTrainHIP: hidden / attention-probs dropout > 0 is not built "
+                                      "(ViltConfig's defaults are 0.0)")
+        if cfg.hidden_act != "gelu":
+            raise NotImplementedError(f"ViltTrainHIP: hidden_act {cfg.hidden_act!r} (the GEMM epilogue is erf GELU)")
+        self.model = model
+        self.config = cfg
+
+    def _text(self, emb, input_ids, token_type_ids):
+        te = emb.text_embeddings
+        Lt = input_ids.shape[1]
+        if token_type_ids is None:
+            token_type_ids = torch.zeros_like(input_ids)
+        E = te.word_embeddings.weight[input_ids] + te.token_type_embeddings.weight[token_type_ids] \
+            + te.position_embeddings.weight[:Lt].unsqueeze(0)
+        ln = te.LayerNorm
+        X = F.layer_norm(E.float(), (E.shape[-1],), ln.weight, ln.bias, ln.eps)
+        return X + emb.token_type_embeddings.weight[0]
+
+    def _visual(self, emb, pixel_values, pixel_mask, type_idx):
+        cfg = self.config
+        B, C, Hh, Ww = pixel_values.shape
+        proj = emb.patch_embeddings.projection
+        p = proj.kernel_size[0]
+        gh, gw = Hh // p, Ww // p
+        H = proj.weight.shape[0]
+        rows = patchify(pixel_values.float(), p).to(bf16).contiguous()
+        x = _PatchGemm.apply(rows, proj.weight, proj.bias).view(B, gh * gw, H)
+        xm = patch_mask(pixel_mask, gh, gw)
+        x_h, x_w = xm.sum(1)[:, 0], xm.sum(2)[:, 0]
+        pd = cfg.image_size // cfg.patch_size
+        pos_img = emb.position_embeddings
+        spatial = pos_img[:, 1:, :].transpose(1, 2).reshape(1, H, pd, pd)
+        ext = [(int(h), int(w)) for h, w in zip(x_h, x_w)]
+        uniq = sorted(set(ext))
+        grids = torch.cat([F.pad(F.interpolate(spatial, size=e, mode="bilinear", align_corners=True),
+                                 (0, gw - e[1], 0, gh - e[0])) for e in uniq], 0)
+        grids = grids.flatten(2).transpose(1, 2)
+        max_len = image_length(xm, cfg.max_image_length)
+        P = gh * gw
+        flat, mask = select_patches(xm.flatten(1), max_len)
+        mask, flat = mask.to(x.device), flat.to(x.device)
+        x = x.reshape(B * P, H)[flat].view(B, -1, H)
+        gid = torch.tensor([uniq.index(e) for e in ext], device=x.device)
+        pos = grids.reshape(-1, H)[(gid * P).repeat_interleave(max_len) + flat % P].view(B, -1, H)
+        x = torch.cat([emb.cls_token.expand(B, -1, -1), x], 1)
+        pos = torch.cat([pos_img[:, :1].expand(B, -1, -1), pos], 1)
+        mask = torch.cat([torch.ones(B, 1, dtype=mask.dtype, device=x.device), mask], 1)
+        return x + pos + emb.token_type_embeddings.weight[type_idx], mask
+
+    def _pooled(self, input_ids, attention_mask, token_type_ids, pixel_values, pixel_mask, type_idx):
+        vm = self.model.vilt if hasattr(self.model, "vilt") else self.model
+        emb = vm.embeddings
+        B = input_ids.shape[0]
+        if attention_mask is None:
+            attention_mask = torch.ones_like(input_ids)
+        if pixel_mask is None:
+            pixel_mask = torch.ones(B, pixel_values.shape[-2], pixel_values.shape[-1], device=input_ids.device)
+        txt = self._text(emb, input_ids, token_type_ids)
+        img, img_mask = self._visual(emb, pixel_values, pixel_mask, type_idx)
+        X = torch.cat([txt, img], 1)
+        L, H = X.shape[1], X.shape[2]
+        mask = torch.cat([attention_mask.to(img_mask.dtype), img_mask], 1)
+        keymask = ((1.0 - mask.float()) * MASK_NEG).contiguous()
+        X = X.reshape(B * L, H).contiguous()
+        for lyr in vm.encoder.layer:
+            a = lyr.attention.attention
+            X = _ViltLayerFunction.apply(
+                X, keymask, B, L, a.num_attention_heads, lyr.layernorm_before.eps, lyr.layernorm_after.eps,
+                a.query.weight, a.key.weight, a.value.weight, a.query.bias, a.key.bias, a.value.bias,
+                lyr.attention.output.dense.weight, lyr.attention.output.dense.bias,
+                lyr.layernorm_before.weight, lyr.layernorm_before.bias,
+                lyr.intermediate.dense.weight, lyr.intermediate.dense.bias,
+                lyr.output.dense.weight, lyr.output.dense.bias,
+                lyr.layernorm_after.weight, lyr.layernorm_after.bias)
+        cls = X.view(B, L, H)[:, 0]  # only the [CLS] rows reach the pooler
+        fl = vm.layernorm
+        cls = F.layer_norm(cls, (H,), fl.weight, fl.bias, fl.eps)
+        return torch.tanh(F.linear(cls, vm.pooler.dense.weight, vm.pooler.dense.bias))
+
+    def forward(self, input_ids, attention_mask=None, token_type_ids=None, pixel_values=None, pixel_mask=None,
+                labels=None, **unused):
+        from transformers.models.vilt.modeling_vilt import ViltForImagesAndTextClassificationOutput
+        K._dev_check(input_ids)
+        if pixel_values.dim() == 4:
+            pixel_values = pixel_values[:, None]
+            pixel_mask = None if pixel_mask is None else pixel_mask[:, None]
+        n = pixel_values.shape[1]
+        if n != self.config.num_images:
+            raise ValueError("Make sure to match the number of images in the model with the number of images in the input.")
+        pooled = [self._pooled(input_ids, attention_mask, token_type_ids, pixel_values[:, i],
+                               None if pixel_mask is None else pixel_mask[:, i], i + 1) for i in range(n)]
+        logits = self.model.classifier(torch.cat(pooled, -1))
+        loss = None
+        if labels is not None:
+            loss = F.cross_entropy(logits.view(-1, self.model.num_labels), labels.to(logits.device).view(-1))
+        return ViltForImagesAndTextClassificationOutput(loss=loss, logits=logits)

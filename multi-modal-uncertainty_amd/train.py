@@ -11,7 +11,8 @@ Additions (all optional):
                      loss / metric sums combined over the ranks in Model_.eval_loop),
                      rank 0 writes history / checkpoints.
   --synthetic with --framework flava: seeded FLAVA embeddings (197 image + <= 77 text tokens)
-The ViLT branch (another model family, remote weights) is out of scope and refused.
+--framework vilt is refused: the reference's setup_vilt needs the remote dandelin/vilt-b32-mlm
+weights and ViltProcessor; the ViLT training step itself is src.vilt.ViltTrainHIP.
 """
 import argparse
 import logging
@@ -241,8 +242,10 @@ def main(argv=None):
         args.device = local
     print(args)
     if args.framework == "vilt":
-        raise NotImplementedError("--framework vilt: ViLT needs remote weights and is another model family "
-                                  "(SURVEY §2); the MMBT and FLAVA paths are built for MI355X")
+        raise NotImplementedError("--framework vilt: the reference's setup_vilt loads dandelin/vilt-b32-mlm and its "
+                                  "ViltProcessor data path (remote, not offline).  The ViLT training step itself is "
+                                  "built: wrap a ViltForImagesAndTextClassification in src.vilt.ViltTrainHIP and "
+                                  "pass it as the framework's model (Model_.train_loop(..., vilt=True))")
     if args.framework == "flava":
         train, valid, test = flava_data(args, rank, world)
         args, model, optimizer, scheduler = setup_flava(args, len(train))
