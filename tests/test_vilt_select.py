@@ -78,3 +78,17 @@ def test_batched_draws_match_visual_embed_at_bench_shape(max_image_length):
     assert torch.equal(got_idx, ref_idx[:, 1:] if ref_idx.shape[1] == L + 1 else ref_idx)
     assert torch.equal(mask, ref_mask[:, 1:])
     assert torch.equal(after, ref_after)
+
+
+def test_vilt_train_refuses_cpu_tensors():
+    """No CPU path: ViltTrainHIP on host tensors raises instead of falling back to torch."""
+    from transformers import ViltConfig, ViltForImagesAndTextClassification
+    from src._native import NativeError
+    from src.vilt import ViltTrainHIP
+    torch.manual_seed(0)
+    cfg = ViltConfig(num_hidden_layers=1, image_size=64, patch_size=32, max_position_embeddings=8, vocab_size=50,
+                     num_images=1, num_labels=2)
+    hip = ViltTrainHIP(ViltForImagesAndTextClassification(cfg))
+    with pytest.raises(NativeError, match="HIP"):
+        hip(input_ids=torch.randint(5, 50, (2, 8)), pixel_values=torch.randn(2, 1, 3, 64, 64),
+            labels=torch.tensor([0, 1]))
