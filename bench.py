@@ -614,10 +614,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MMU_BENCH_BACKEND=gloo MMU_BENCH_ONE_DEVICE=1: a one-GPU rehearsal of the N > 1 path (every
+    # rank on cuda:0, collectives over gloo) -- the glue, bucketing and timing code of an 8-GPU run,
+    # not its performance; the default is one rank per GPU over RCCL
+    backend = os.environ.get("MMU_BENCH_BACKEND", "nccl")
+    if os.environ.get("MMU_BENCH_ONE_DEVICE") == "1":
+        local = 0
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     if args.workload in ("flava", "uncertainty", "encoders", "vilt", "vilt_train"):
         fn = {"flava": bench_flava, "uncertainty": bench_uncertainty, "encoders": bench_encoders,
