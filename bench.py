@@ -43,9 +43,15 @@ RESNET152_FWD_FLOP = 23.0e9            # per 224x224 sample (11.5 GMAC)
 PEAK_BF16_TFLOPS = 2500.0              # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU). Without WORLD_SIZE in the environment and N > 1, bench.py starts "
+                         "N ranks itself under torch.distributed.run (a child process); under an external "
+                         "launcher N must equal WORLD_SIZE (default: WORLD_SIZE, else 1)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="start the ranks and the process group, print the JSON line's rank / world fields and "
+                         "stop (no GPU work: the launcher's CPU test)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--global-batch", type=int, default=None,
@@ -65,10 +71,11 @@ def parse():
     ap.add_argument("--side-cu-frac", type=float, default=None,
                     help="mmbt: restrict the side stream (weight-gradient GEMMs) to this fraction of the CUs "
                          "(hipExtStreamCreateWithCUMask), leaving the rest to the main stream's chain")
-    ap.add_argument("--graph", default="off", choices=["off", "on"],
+    ap.add_argument("--graph", default="auto", choices=["off", "on", "auto"],
                     help="mmbt: capture the whole step (forward, backward, fused BertAdam) once into a HIP graph "
                          "and replay it (src/graphs.py; the GEMM / block rooflines then come from 2 eager steps "
-                         "before the capture)")
+                         "before the capture); auto = on for a single process at per-rank batch <= 64, where the "
+                         "step is launch-bound (profiles/r5_graph_b32.txt), off otherwise")
     ap.add_argument("--no-stream-residue", action="store_true",
                     help="mmbt: the trunk's residual stream in plain bf16 (the round-4 trunk; for same-box A/Bs)")
     ap.add_argument("--workload", default="mmbt",
@@ -81,8 +88,38 @@ def parse():
     ap.add_argument("--flava-tokens", type=str, default="197,77", help="FLAVA image,text embedding lengths")
     ap.add_argument("--cpu-batch", type=int, default=8,
                     help="samples per oracle step of the CPU baseline (SURVEY §8(d): B = 8, 3 steps)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0: affinity, capped by OMP_NUM_THREADS")
-    return ap.parse_args()
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0: os.cpu_count(), SURVEY §8(d)'s torch.set_num_threads(os.cpu_count()))")
+    return ap.parse_args(argv)
+
+
+def rank_launch_cmd(n, argv, port):
+    """The child command that starts ``n`` ranks of this script on one node (the driver's own
+    form: torch.distributed.run, rendezvous on 127.0.0.1), passing ``argv`` through."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def resolve_world(args, env=None):
+    """-> (world, launch): the rank count this process belongs to, and whether it must first start
+    that many ranks itself.  Runs before anything touches the GPU (no HIP call, no exec)."""
+    env = os.environ if env is None else env
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+        return world, False
+    n = 1 if args.gpus is None else args.gpus
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus {n}")
+    return n, n > 1
 
 
 def _cpu_model():
@@ -95,15 +132,24 @@ def _cpu_model():
     return platform.processor() or "unknown"
 
 
+def _cgroup_cpus():
+    """CPUs the process's cgroup may run on at once (cpu.max quota / period), or None."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        return None
+
+
 def _cpu_threads(args):
-    """Host threads for the CPU baseline: --cpu-threads, else this process's CPU affinity
-    capped by OMP_NUM_THREADS (the GPU box grants 16 CPUs per GPU and exports
-    OMP_NUM_THREADS=16, while os.cpu_count() there reports the whole machine)."""
+    """Host threads for the CPU baseline: --cpu-threads, else SURVEY §8(d)'s os.cpu_count(),
+    capped only by the CPUs this process can actually run on (its affinity mask and its cgroup's
+    CPU quota): more threads than those would time OpenMP oversubscription, not the reference."""
     if args.cpu_threads:
         return args.cpu_threads
-    n = len(os.sched_getaffinity(0))
-    omp = os.environ.get("OMP_NUM_THREADS")
-    return min(n, int(omp)) if omp and omp.isdigit() else n
+    n = min(os.cpu_count() or 1, len(os.sched_getaffinity(0)))
+    q = _cgroup_cpus()
+    return min(n, q) if q else n
 
 
 def cpu_baseline(args, L_text):
@@ -157,6 +203,7 @@ def cpu_baseline(args, L_text):
         t_rob = timed(lambda: R.robustness(sd, txt[:1], mask[:1], mask[:1], img[:1], FULL, n_repeats=20), 1)
     return {"value": round(B / t_train, 4), "unit": "samples/s", "cores": threads, "kind": "port",
             "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_cpus": _cgroup_cpus(),
             "eval_forward": {"value": round(B / t_eval, 4), "unit": "samples/s"},
             "robustness_43": {"value": round(1 / t_rob, 4), "unit": "samples/s",
                               "sample": "1 sample x 43 variants (full, img-only, txt-only, 20+20 controls), "
@@ -611,7 +658,16 @@ def bench_encoders(args, world, rank, dev):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world, launch = resolve_world(args)
+    if launch:
+        # no launcher around us: start the N ranks (one per GPU) as a child torch.distributed.run
+        # and exit with its status -- a child process, never an exec, and before any HIP call
+        one_dev = os.environ.get("MMU_BENCH_ONE_DEVICE") == "1"
+        if not args.dry_run and not one_dev and torch.cuda.device_count() < world:
+            raise SystemExit(f"bench.py: --gpus {world} but {torch.cuda.device_count()} GPUs are visible")
+        import subprocess
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        sys.exit(subprocess.call(rank_launch_cmd(world, sys.argv[1:], _free_port()), env=env))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # MMU_BENCH_BACKEND=gloo MMU_BENCH_ONE_DEVICE=1: a one-GPU rehearsal of the N > 1 path (every
@@ -620,6 +676,20 @@ def main():
     backend = os.environ.get("MMU_BENCH_BACKEND", "nccl")
     if os.environ.get("MMU_BENCH_ONE_DEVICE") == "1":
         local = 0
+    if args.dry_run:
+        # the launcher's check: ranks, process group and the world size the backend reports
+        if world > 1:
+            dist.init_process_group(backend)
+        out = {"n_gpus": world, "world_size_reported": dist.get_world_size() if world > 1 else 1,
+               "rank": rank, "backend": backend if world > 1 else None, "dry_run": True}
+        if world > 1:
+            seen = [None] * world
+            dist.all_gather_object(seen, rank)
+            out["ranks_seen"] = seen
+            dist.destroy_process_group()
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        return
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
@@ -627,11 +697,14 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        if dist.get_world_size() != world:
+            raise SystemExit(f"bench.py: WORLD_SIZE {world} but the process group reports {dist.get_world_size()}")
     dev = torch.device("cuda", local)
     if args.workload in ("flava", "uncertainty", "encoders", "vilt", "vilt_train"):
         fn = {"flava": bench_flava, "uncertainty": bench_uncertainty, "encoders": bench_encoders,
               "vilt": bench_encoders, "vilt_train": bench_vilt_train}[args.workload]
         out = fn(args, world, rank, dev)
+        out["world_size_reported"] = dist.get_world_size() if dist.is_initialized() else 1
         if rank == 0:
             print(json.dumps(out), flush=True)
         if world > 1:
@@ -696,7 +769,7 @@ def main():
         opt.step()
         return loss
 
-    graph = args.graph == "on"
+    graph = args.graph == "on" or (args.graph == "auto" and world == 1 and B <= 64)
     if graph and world > 1:
         # (the bucketed all-reduce inside a captured backward needs RCCL graph capture, which the
         # one-GPU boxes this was developed on cannot exercise)
@@ -791,6 +864,7 @@ def main():
         "final_loss": round(float(loss.item()), 4),
         "hbm_peak_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1),
     }
+    out["world_size_reported"] = dist.get_world_size() if dist.is_initialized() else 1
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, T)
     if rank == 0:

@@ -30,6 +30,10 @@ typedef void* mmu_stream_t; /* hipStream_t */
 enum { MMU_BF16 = 0, MMU_F32 = 1 };
 
 /* ------------------------------------------------------------------ status */
+/* ABI version: bumped whenever an entry's argument list changes.  2 (round 5): the residual
+ * stream's residue pointers inside mmu_batchnorm_fwd / _fwd_sums and the grad_scale argument
+ * of mmu_bertadam_step.  Callers compare mmu_version() with the header they were built against. */
+#define MMU_ABI_VERSION 2
 int mmu_version(void);
 const char* mmu_last_error(void);
 
@@ -324,7 +328,10 @@ int mmu_stem_conv_wgrad(const void* dY, const void* X, float* dW, int64_t n_img,
  * activations X [rows = N*H*W, C] (C % 8 == 0, C <= 2048):
  *   Y = act(X * scale + shift [+ skip]),  act = ReLU when relu != 0.
  * training: batch statistics (biased variance), running_mean / running_var updated
- *   with momentum (unbiased variance), *num_batches_tracked += 1 (each may be NULL),
+ *   with momentum (unbiased variance), *num_batches_tracked += 1 (each may be NULL);
+ *   momentum < 0 = torch's momentum=None (cumulative moving average): the factor is
+ *   1 / *num_batches_tracked, which the caller has ALREADY incremented for this pass (required,
+ *   not incremented again here),
  *   save_mean / save_invstd [C] f32 written for the backward.
  * eval: running statistics.  weight / bias may be NULL (affine = False).
  * relu_mask (may be NULL; needs relu): [rows, C/8] u8 written with bit e of byte (r, c/8)

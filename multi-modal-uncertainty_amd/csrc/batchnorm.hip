@@ -193,11 +193,15 @@ __global__ __launch_bounds__(BN_THREADS) void bn_fwd_finalize_kernel(
   coef[C + c] = bb - (float)mean * scale;
   if (training) {
     if (smean) { smean[c] = (float)mean; sinvstd[c] = invstd; }
+    // momentum < 0: torch's cumulative moving average (momentum=None), factor 1 / num_batches_tracked
+    // read on the device -- the caller has already counted this pass, so there is no increment here
+    // (every channel reads the same count; no host sync, so the pass can be graph-captured)
+    const float mom = momentum < 0.f ? 1.0f / (float)*nbt : momentum;
     if (rmean) {
-      rmean[c] = (1.0f - momentum) * rmean[c] + momentum * (float)mean;
-      rvar[c] = (1.0f - momentum) * rvar[c] + momentum * (float)(var * n / (n - 1.0));
+      rmean[c] = (1.0f - mom) * rmean[c] + mom * (float)mean;
+      rvar[c] = (1.0f - mom) * rvar[c] + mom * (float)(var * n / (n - 1.0));
     }
-    if (nbt && c == 0) *nbt += 1;
+    if (nbt && c == 0 && momentum >= 0.f) *nbt += 1;
   }
 }
 

@@ -65,7 +65,7 @@ std::pair<hipEvent_t, hipEvent_t> take_events() {
 
 extern "C" {
 
-int mmu_version(void) { return 1; }
+int mmu_version(void) { return MMU_ABI_VERSION; }
 const char* mmu_last_error(void) { return g_err.c_str(); }
 
 int mmu_timing_enable(int on) {
@@ -631,6 +631,8 @@ int mmu_batchnorm_fwd(const void* X, const void* skip, void* Y, int64_t rows, in
     return fail("mmu_batchnorm_fwd: save_mean / save_invstd must both be given or NULL");
   if (training && rows < 2) return fail("mmu_batchnorm_fwd: training needs more than 1 value per channel");
   if (!training && !running_mean) return fail("mmu_batchnorm_fwd: eval needs running statistics");
+  if (training && momentum < 0.f && !num_batches_tracked)
+    return fail("mmu_batchnorm_fwd: momentum < 0 (cumulative average) needs num_batches_tracked");
   BnFwdParams q{};
   q.X = (const bf16*)X; q.skip = (const bf16*)skip; q.Y = (bf16*)Y; q.rows = rows; q.C = (int)C;
   q.w = weight; q.b = bias; q.rmean = running_mean; q.rvar = running_var; q.nbt = num_batches_tracked;
@@ -678,6 +680,8 @@ int mmu_batchnorm_fwd_sums(const void* X, const void* skip, void* Y, int64_t row
     return fail("mmu_batchnorm_fwd_sums: running_mean / running_var must both be given or NULL");
   if ((save_mean == nullptr) != (save_invstd == nullptr))
     return fail("mmu_batchnorm_fwd_sums: save_mean / save_invstd must both be given or NULL");
+  if (momentum < 0.f && !num_batches_tracked)
+    return fail("mmu_batchnorm_fwd_sums: momentum < 0 (cumulative average) needs num_batches_tracked");
   BnFwdParams q{};
   q.X = (const bf16*)X; q.skip = (const bf16*)skip; q.Y = (bf16*)Y; q.rows = rows; q.C = (int)C;
   q.w = weight; q.b = bias; q.rmean = running_mean; q.rvar = running_var; q.nbt = num_batches_tracked;

@@ -101,6 +101,10 @@ class NativeError(RuntimeError):
     pass
 
 
+# include/mmu.h MMU_ABI_VERSION: the argument lists SIGNATURES binds
+ABI_VERSION = 2
+
+
 def load():
     """Load (once) and return the library; raise NativeError if it is absent."""
     global _lib
@@ -115,6 +119,9 @@ def load():
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.restype, fn.argtypes = res, args
+        if lib.mmu_version() != ABI_VERSION:
+            raise NativeError(f"libmmu_hip.so ABI {lib.mmu_version()} != {ABI_VERSION} (include/mmu.h "
+                              "MMU_ABI_VERSION): rebuild the library")
         _lib = lib
     return _lib
 

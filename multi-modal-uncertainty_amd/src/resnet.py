@@ -55,7 +55,7 @@ class _BatchNormAct(torch.autograd.Function):
         sinv = torch.empty_like(smean)
         # the backward reads the ReLU mask (1 bit per element) instead of Y (16 bits)
         mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device) if relu else None
-        K.batchnorm_fwd(x, Y, weight, bias, bn.running_mean, bn.running_var, True, _momentum(bn), bn.eps,
+        K.batchnorm_fwd(x, Y, weight, bias, bn.running_mean, bn.running_var, True, _momentum_arg(bn), bn.eps,
                         relu=relu, skip=skip, num_batches_tracked=bn.num_batches_tracked, save_mean=smean,
                         save_invstd=sinv, relu_mask=mask, skip_res=skip_res, y_res=y_res)
         ctx.save_for_backward(x, mask, weight, smean, sinv)
@@ -85,10 +85,21 @@ class _BatchNormAct(torch.autograd.Function):
 
 def _momentum(bn):
     """the running-statistics factor of this training pass: bn.momentum, or for momentum=None
-    (torch's cumulative moving average) 1 / num_batches_tracked after this pass's increment"""
+    (torch's cumulative moving average) 1 / num_batches_tracked after this pass's increment
+    (host value: the torch-op sync path only)"""
     if bn.momentum is not None:
         return float(bn.momentum)
     return 1.0 / float(int(bn.num_batches_tracked) + 1)
+
+
+def _momentum_arg(bn):
+    """the kernels' momentum argument: bn.momentum, or for momentum=None -1 after counting this
+    pass in num_batches_tracked ON THE DEVICE (the kernel then uses 1 / num_batches_tracked): no
+    device-to-host read, so the pass stays asynchronous and graph-capturable"""
+    if bn.momentum is not None:
+        return float(bn.momentum)
+    bn.num_batches_tracked.add_(1)
+    return -1.0
 
 
 class _SyncBatchNormAct(torch.autograd.Function):
@@ -115,7 +126,7 @@ class _SyncBatchNormAct(torch.autograd.Function):
             smean = torch.empty(C, dtype=torch.float32, device=x.device)
             sinv = torch.empty_like(smean)
             mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device) if relu else None
-            K.batchnorm_fwd_sums(x, Y, sums, weight, bias, bn.running_mean, bn.running_var, _momentum(bn), bn.eps,
+            K.batchnorm_fwd_sums(x, Y, sums, weight, bias, bn.running_mean, bn.running_var, _momentum_arg(bn), bn.eps,
                                  relu=relu, skip=skip, num_batches_tracked=bn.num_batches_tracked, save_mean=smean,
                                  save_invstd=sinv, relu_mask=mask, skip_res=skip_res, y_res=y_res)
             ctx.save_for_backward(x, mask, weight, smean, sinv)

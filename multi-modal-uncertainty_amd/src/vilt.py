@@ -87,6 +87,15 @@ def select_patches(xm, max_len):
     return flat, xm.flatten()[flat].view(B, -1)
 
 
+
+def _check_head_dim(cfg, who):
+    """The attention kernels read head h's Q / K / V at columns 64 h of the fused QKV rows
+    (head_dim 64, as every BERT-base-shaped ViLT): another head width would pass the C-ABI's
+    row-stride check and read the wrong columns, so it is refused here."""
+    if cfg.hidden_size != cfg.num_attention_heads * 64:
+        raise NotImplementedError(f"{who}: hidden_size {cfg.hidden_size} / {cfg.num_attention_heads} heads is not "
+                                  "head_dim 64 (mmu_attention_fwd / _bwd)")
+
 class ViltHIP:
     """``ViltForImagesAndTextClassification`` (or a bare ``ViltModel``) on the HIP kernels.
 
@@ -100,6 +109,7 @@ class ViltHIP:
         dev = torch.device(device)
         vm = model.vilt if hasattr(model, "vilt") else model
         cfg = vm.config
+        _check_head_dim(cfg, "ViltHIP")
         self.config = cfg
         emb = vm.embeddings
         te = emb.text_embeddings
@@ -368,6 +378,7 @@ class ViltTrainHIP(nn.Module):
                                       "(ViltConfig's defaults are 0.0)")
         if cfg.hidden_act != "gelu":
             raise NotImplementedError(f"ViltTrainHIP: hidden_act {cfg.hidden_act!r} (the GEMM epilogue is erf GELU)")
+        _check_head_dim(cfg, "ViltTrainHIP")
         self.model = model
         self.config = cfg
 

@@ -91,8 +91,15 @@ GRAD_REL = 1e-2  # north star: 1e-2 for bf16
 TRUNK_MEDIAN = 1e-2
 TRUNK_MAX = 0.1
 # fixtures whose fp32 trunk is chaotic (tests/test_oracle.py::test_trunk_conditioning_of_the_
-# fixture_recipes): the bf16 trunk is compared there as a printed diagnostic only
+# fixture_recipes): no bf16 trunk can reach the absolute bars there, so the HIP trunk is held
+# RELATIVE to PyTorch's own bf16 trunk on the same step: trunk grad-norm errors
+# median <= CHAOS_MEDIAN_X x torch's, p90 and max <= CHAOS_TAIL_X x torch's; BN-fitted logits
+# <= max(1e-2, CHAOS_LOGIT_X x torch's) per variant (round 5 measured 1.08x / 1.05x / 1.97x and
+# img_only 0.64x: profiles/r5_parity.log)
 CHAOTIC = ("full_t508",)
+CHAOS_MEDIAN_X = 3.5
+CHAOS_TAIL_X = 2.5
+CHAOS_LOGIT_X = 2.0
 
 
 def fixture(tag):
@@ -154,7 +161,8 @@ def test_train_step_grads_match_reference_golden(dev, tag, cfgname, prec):
     invariance; the reference reads ~1e-9, bf16 arithmetic ~1e-5); the fp32 trunk's tensors
     within 1e-2 each; the bf16 trunk's tensors median <= TRUNK_MEDIAN and each <= TRUNK_MAX.
     On a CHAOTIC fixture (full_t508: its fp32 trunk moves 1e-2 for a 1e-4 input perturbation)
-    the bf16 trunk's tensors are printed, with PyTorch's own bf16 trunk beside them, not held."""
+    the bf16 trunk's tensors are held relative to PyTorch's own bf16 trunk on the same step
+    (CHAOS_* bars)."""
     g, cfg = fixture(tag)
     names = json.load(open(os.path.join(GOLD, f"mmbt_{tag}_keys.json")))["named_parameters"]
     ref = dict(zip(names, (float(v) for v in g["grad_norms"])))
@@ -182,9 +190,13 @@ def test_train_step_grads_match_reference_golden(dev, tag, cfgname, prec):
         _, tnorms, _, _ = _train_step(cfgname, g, dev, "torch_bf16", cfg)
         trows = [(n, _rel(tnorms[n], ref[n])) for n, _ in rows]
         tt = _trunk_summary(trows)
-        msg += (f"; PyTorch's own bf16 trunk (diagnostic): median {tt['median']:.2e} p90 {tt['p90']:.2e} max "
+        msg += (f"; PyTorch's own bf16 trunk (the comparator): median {tt['median']:.2e} p90 {tt['p90']:.2e} max "
                 f"{tt['max']:.2e}, > 1e-2: {tt['n_above_1e-2']} of {tt['n']}")
     print(msg)
+    if chaotic:
+        assert ts["median"] <= CHAOS_MEDIAN_X * tt["median"], msg
+        assert ts["p90"] <= CHAOS_TAIL_X * tt["p90"], msg
+        assert ts["max"] <= CHAOS_TAIL_X * tt["max"], msg
     assert lerr < 1e-2, f"train loss {loss:.6f} vs {float(g['loss_train']):.6f}"
     assert not bad, f"{len(bad)} of {len(names)} grad norms off: worst {sorted(bad, key=lambda r: -r[3])[:5]}"
     if prec == "bf16" and not chaotic:
@@ -229,8 +241,8 @@ def test_bnfit_eval_variants_bf16_trunk_match_reference_golden(dev, tag, cfgname
     train-mode pass: the fixture's bnfit_* entries, made the same way by the reference model),
     so the trunk's activations are normalised: logits of all 5 variants (full, image-only,
     text-only, both controls) within 1e-2 * max|logit| (north star, bf16), with the bf16 HIP
-    product trunk -- or, on the chaotic fixture full_t508, with the fp32 trunk (the bf16
-    trunk's errors printed beside PyTorch's own bf16 trunk's, as a diagnostic)."""
+    product trunk -- or, on the chaotic fixture full_t508, with the fp32 trunk, and the bf16
+    trunk within max(1e-2, CHAOS_LOGIT_X x PyTorch's own bf16 trunk's error) per variant."""
     g, cfg = fixture(tag)
     got, loss, rm = _bnfit_logits(cfgname, g, dev, prec, cfg)
     chaotic = prec == "bf16" and tag in CHAOTIC
@@ -245,6 +257,8 @@ def test_bnfit_eval_variants_bf16_trunk_match_reference_golden(dev, tag, cfgname
     print(f"\n[{tag} {prec} bnfit] logits rel err per variant" + (" (HIP bf16 trunk / torch bf16 trunk)" if chaotic else "")
           + ": " + ", ".join(f"{k} {e:.2e}" + (f" / {te:.2e}" if chaotic else "") for k, (e, te) in errs.items()))
     if chaotic:
+        for v, (e, te) in errs.items():
+            assert e <= max(1e-2, CHAOS_LOGIT_X * te), f"bnfit {v}: {e:.3e} (PyTorch's bf16 trunk {te:.3e})"
         return
     for v, (e, _) in errs.items():
         assert e <= 1e-2, f"bnfit {v}: {e:.3e}"

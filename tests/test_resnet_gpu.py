@@ -326,3 +326,23 @@ def test_stream_residue_carried_through_the_trunk(dev, monkeypatch, train):
     print(f"\n[stream residue, train={train}] trunk output rel err vs fp32: with {e_on:.3e}, without {e_off:.3e}")
     assert not torch.equal(on, off)
     assert e_on < e_off
+
+
+def test_batchnorm_momentum_none_cumulative_average_on_device(dev):
+    """momentum=None (torch's cumulative moving average): the HIP pass takes 1 / num_batches_tracked
+    on the device (no host read) and matches torch.nn.BatchNorm2d's running statistics
+    over three training passes."""
+    from src.resnet import BatchNorm2d
+    torch.manual_seed(0)
+    C = 64
+    hip = BatchNorm2d(C, momentum=None).to(dev).train()
+    ref = torch.nn.BatchNorm2d(C, momentum=None).to(dev).train()
+    for it in range(3):
+        x = torch.randn(4, C, 9, 7, device=dev) * (1 + it) + it
+        xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        with torch.no_grad():
+            hip(xb)
+            ref(xb.float())
+    assert int(hip.num_batches_tracked) == 3 == int(ref.num_batches_tracked)
+    torch.testing.assert_close(hip.running_mean, ref.running_mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(hip.running_var, ref.running_var, rtol=1e-4, atol=1e-5)

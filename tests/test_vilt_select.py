@@ -92,3 +92,17 @@ def test_vilt_train_refuses_cpu_tensors():
     with pytest.raises(NativeError, match="HIP"):
         hip(input_ids=torch.randint(5, 50, (2, 8)), pixel_values=torch.randn(2, 1, 3, 64, 64),
             labels=torch.tensor([0, 1]))
+
+
+@pytest.mark.parametrize("cls", ["ViltHIP", "ViltTrainHIP"])
+def test_vilt_refuses_head_dim_other_than_64(cls):
+    """the attention kernels assume head_dim 64: 768 / 6 heads is refused, not run"""
+    from transformers import ViltConfig, ViltForImagesAndTextClassification
+    from src import vilt
+    cfg = ViltConfig(num_hidden_layers=1, image_size=64, patch_size=32, max_position_embeddings=16, vocab_size=300,
+                     num_images=1, num_attention_heads=6)
+    with pytest.raises(NotImplementedError, match="head_dim 64"):
+        if cls == "ViltHIP":
+            vilt.ViltHIP(ViltForImagesAndTextClassification(cfg), "cpu")
+        else:
+            vilt.ViltTrainHIP(ViltForImagesAndTextClassification(cfg))
