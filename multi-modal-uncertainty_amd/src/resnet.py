@@ -25,7 +25,8 @@ _TORCH_ONLY = [False]
 # BatchNorm output carry an 8-bit residue (int8 of the map's size, csrc/batchnorm.hip), kept as
 # the ``_mmu_res`` attribute of the bf16 map; the next bn3 adds it to its skip, so the stream
 # is held to ~2^-15 of its value instead of bf16's 2^-8.  The convs read the bf16 map.
-STREAM_RESIDUE = True
+# MMU_STREAM_RESIDUE=0 turns it off process-wide (the parity A/B of profiles/r6_residue_parity_ab.txt).
+STREAM_RESIDUE = os.environ.get("MMU_STREAM_RESIDUE", "1") != "0"
 
 
 class torch_ops_only:
