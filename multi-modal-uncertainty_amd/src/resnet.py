@@ -411,6 +411,12 @@ def _conv_geo(w16, stride, padding):
     return k[0], stride[0]
 
 
+# Routing decisions (_mmu_conv / _mmu_1x1) are taken as if every map held ROUTE_M_SCALE times its
+# rows: a data-parallel rank running B / N samples sets N to route its convs exactly as the single
+# device does at the global batch B (tests/test_dp_gpu.py: the sync-BN root cause)
+ROUTE_M_SCALE = 1
+
+
 def _mmu_conv(geo, xshape, cout):
     """(forward, data gradient, filter gradient) of a conv on the gathered-operand MFMA
     products (mmu_conv_implicit / mmu_conv_wgrad) instead of MIOpen, from same-box timings
@@ -426,7 +432,7 @@ def _mmu_conv(geo, xshape, cout):
     ks, st = geo
     n, cin, h, w = xshape
     pad = ks // 2
-    M = n * ((h + 2 * pad - ks) // st + 1) * ((w + 2 * pad - ks) // st + 1)
+    M = ROUTE_M_SCALE * n * ((h + 2 * pad - ks) // st + 1) * ((w + 2 * pad - ks) // st + 1)
     if ks == 3 and st == 1:
         fwd = cin % 64 == 0 and cout % 128 == 0 and cout >= 256 and M >= 256
         dx = cout % 64 == 0 and cin % 128 == 0 and M >= 256
@@ -452,6 +458,7 @@ def _mmu_1x1(cin, cout, M, H):
     batch-128 ranks of config 4 -- since the short-K split-K of profiles/r3_wgrad_shortk_ab.txt
     brought it level with MIOpen's wrw, which also pays a bf16 -> f32 add into the store).
     mmu_gemm needs N % 128 == 0 for its output columns (and M-major A rows % 128 for dW)."""
+    M = M * ROUTE_M_SCALE
     fwd = cout % 128 == 0 and cin % 64 == 0 and 25088 <= M <= 50176 and (cin > cout or M < 50176)
     dx = cin % 128 == 0 and cout % 64 == 0 and (cin > cout or M >= 12544)
     dw = cin % 128 == 0 and cout % 128 == 0 and M <= 50176 and H <= 14

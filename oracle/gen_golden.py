@@ -450,7 +450,7 @@ def gen_framework():
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("--what", default="all", choices=["all", "small", "small_b8", "full", "full_c", "framework", "flava",
+    ap.add_argument("--what", default="all", choices=["all", "small", "small_b8", "full", "full_c", "full_c4", "framework", "flava",
                                                        "robustness", "fmnist", "a0"])
     a = ap.parse_args()
     sys.path.insert(0, REPO)
@@ -458,7 +458,7 @@ if __name__ == "__main__":
     # each generator imports the reference fresh with its own stub config -> run each in a subprocess
     if a.what == "all":
         import subprocess
-        for w in ("small", "small_b8", "full", "full_c", "framework", "flava", "robustness", "fmnist", "a0"):
+        for w in ("small", "small_b8", "full", "full_c", "full_c4", "framework", "flava", "robustness", "fmnist", "a0"):
             subprocess.check_call([sys.executable, "-m", "oracle.gen_golden", "--what", w], cwd=REPO)
     elif a.what == "small":
         gen_mmbt("small_t16", SMALL, B=2, T=16, lens=[16, 9], seed=0)
@@ -468,6 +468,8 @@ if __name__ == "__main__":
         gen_mmbt("full_t508", FULL, B=2, T=508, lens=[508, 300], seed=1)
     elif a.what == "full_c":  # the conditioned trunk recipe (oracle/weights.py FULL_C)
         gen_mmbt("full_t508c", FULL_C, B=2, T=508, lens=[508, 300], seed=1)
+    elif a.what == "full_c4":  # the same recipe at batch 4: another BatchNorm draw
+        gen_mmbt("full_t508c_b4", FULL_C, B=4, T=508, lens=[508, 300, 451, 117], seed=3)
     elif a.what == "flava":
         from oracle.flava_ref import FlavaConfig
         for tag, (kw, B, Li, Lt, seed) in FLAVA_CASES.items():

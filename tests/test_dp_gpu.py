@@ -207,7 +207,7 @@ def test_dp_two_ranks_equal_single_device_global_batch(reduce_dtype):
 
 
 
-def _sync_bn_worker(rank, world, port, q, precision, backend="gloo"):
+def _sync_bn_worker(rank, world, port, q, precision, backend="gloo", pin=False):
     """TRAINING-mode step (batch statistics) three ways: one device on the global batch; two
     ranks on its halves with the trunk's BatchNorms exchanging their sums; two ranks without
     the exchange (per-rank statistics).  Gradients are compared over the flat store without
@@ -248,7 +248,12 @@ def _sync_bn_worker(rank, world, port, q, precision, backend="gloo"):
 
         perm = torch.cat([torch.arange(B // 2, B), torch.arange(0, B // 2)]).to(dev)
 
+        from src import resnet as R
+
         def run(ranks, sync, permuted=False, prec=precision):
+            # pin: the ranks route their convs (engine, gathered / MIOpen) as the single device does
+            # at the global batch (resnet.ROUTE_M_SCALE)
+            R.ROUTE_M_SCALE = world if (pin and ranks) else 1
             m, o = make(prec)
             bk = None
             if ranks:
@@ -287,7 +292,7 @@ def _sync_bn_worker(rank, world, port, q, precision, backend="gloo"):
         else:  # the reference step: one device, the fp32 trunk
             _, gr, dr, _ = run(False, False, prec="fp32")
             q.put((rank, rel(g2, gr), rel(d2, dr), ((b2 - b1).norm() / b1.norm()).item(), rel(g3, g1), rel(g1, gr),
-                   rel(d1, dr), rel(g2, g1)))
+                   rel(d1, dr), rel(g2, g1), rel(g0, g1), rel(d2, d1), rel(d0, d1)))
         dist.destroy_process_group()
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
@@ -316,7 +321,7 @@ def test_dp_sync_batchnorm_two_ranks_equal_single_device_train_mode(precision):
     synchronised run, so the test sees the statistics.  Measured errors printed."""
     x = 2 if precision == "fp32" else 1.5
     what = "reordered batch" if precision == "fp32" else "single-device bf16 trunk"
-    for rank, gerr, perr, berr, gloc, gnoise, pnoise, gsd in _spawn(_sync_bn_worker, 2, precision):
+    for rank, gerr, perr, berr, gloc, gnoise, pnoise, gsd, *_ in _spawn(_sync_bn_worker, 2, precision):
         print(f"\n[dp sync-bn {precision} trunk] rank {rank}: grad rel err {gerr:.3e} ({what} {gnoise:.3e}), "
               f"post-step param-change rel err {perr:.3e} ({what} {pnoise:.3e}), running-stats rel err "
               f"{berr:.3e}; vs the single device: synchronised {gsd:.3e}, per-rank statistics {gloc:.3e}")
@@ -333,8 +338,22 @@ def test_dp_sync_batchnorm_two_ranks_rccl():
     buckets' all-reduces on the default one, through the bf16 HIP trunk -- the configuration
     train.py --sync_bn / bench.py --sync-bn use.  Bars as the gloo test's bf16 arm."""
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    for rank, gerr, perr, berr, gloc, gnoise, pnoise, gsd in _spawn(_sync_bn_worker, 2, "bf16", "nccl"):
+    for rank, gerr, perr, berr, gloc, gnoise, pnoise, gsd, *_ in _spawn(_sync_bn_worker, 2, "bf16", "nccl"):
         print(f"\n[dp sync-bn rccl] rank {rank}: grad rel err {gerr:.3e} (single-device bf16 trunk {gnoise:.3e}), "
               f"vs the single device: synchronised {gsd:.3e}, per-rank statistics {gloc:.3e}")
         assert gerr <= 1.5 * gnoise + 1e-6 and perr <= 1.5 * pnoise + 1e-6, (gerr, gnoise, perr, pnoise)
         assert berr <= 1e-3 and gloc >= 3 * gsd, (berr, gloc, gsd)
+
+
+def test_dp_sync_batchnorm_bf16_gap_is_conv_routing():
+    """Root cause of the bf16 sync-BN gap: with the trunk's convs routed per
+    rank at the per-rank batch, the synchronised 2-rank bf16 step sat 16x the reordered-batch
+    noise from the single device (9.5e-3 vs 6e-4, round 5).  Routing every conv as the single
+    device does at the global batch (resnet.ROUTE_M_SCALE = world) must bring the synchronised
+    step back to the single device's own noise: gradient and post-step change within 2x the
+    reordered batch's (bar written before the run)."""
+    for rank, _, _, _, _, _, _, gsd, g0, dsd, d0 in _spawn(_sync_bn_worker, 2, "bf16", "gloo", True):
+        print(f"\n[dp sync-bn bf16, routing pinned] rank {rank}: vs the single device: grad {gsd:.3e} (reordered "
+              f"batch {g0:.3e}), post-step change {dsd:.3e} (reordered batch {d0:.3e})")
+        assert gsd <= 2 * g0 + 1e-6, (gsd, g0)
+        assert dsd <= 2 * d0 + 1e-6, (dsd, d0)

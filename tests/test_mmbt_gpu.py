@@ -149,7 +149,7 @@ def _trunk_summary(rows):
 @pytest.mark.parametrize("tag,cfgname,prec", [("small_t16", "small", "fp32"), ("small_t16", "small", "bf16"),
                                               ("small_b8", "small", "bf16"), ("full_t508", "full", "fp32"),
                                               ("full_t508c", "full", "fp32"), ("full_t508c", "full", "bf16"),
-                                              ("full_t508", "full", "bf16")])
+                                              ("full_t508c_b4", "full", "bf16"), ("full_t508", "full", "bf16")])
 def test_train_step_grads_match_reference_golden(dev, tag, cfgname, prec):
     """Train mode (BN batch statistics), BERT dropout 0, against the reference's own train-mode
     loss and per-tensor gradient norms (oracle/gen_golden.py gen_mmbt).  prec "bf16" is the
@@ -234,8 +234,8 @@ def _bnfit_logits(cfgname, g, dev, prec, cfg=None):
 
 
 @pytest.mark.parametrize("tag,cfgname,prec", [("small_t16", "small", "bf16"), ("small_b8", "small", "bf16"),
-                                              ("full_t508c", "full", "bf16"), ("full_t508", "full", "fp32"),
-                                              ("full_t508", "full", "bf16")])
+                                              ("full_t508c", "full", "bf16"), ("full_t508c_b4", "full", "bf16"),
+                                              ("full_t508", "full", "fp32"), ("full_t508", "full", "bf16")])
 def test_bnfit_eval_variants_bf16_trunk_match_reference_golden(dev, tag, cfgname, prec):
     """Eval mode on BatchNorm running statistics fitted to the batch (momentum 1, one
     train-mode pass: the fixture's bnfit_* entries, made the same way by the reference model),

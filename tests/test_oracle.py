@@ -29,7 +29,7 @@ def _inputs(g, cfg):
     return x, y
 
 
-@pytest.mark.parametrize("tag", ["small_t16", "small_b8", "full_t508", "full_t508c"])
+@pytest.mark.parametrize("tag", ["small_t16", "small_b8", "full_t508", "full_t508c", "full_t508c_b4"])
 def test_oracle_matches_reference_golden(tag):
     from oracle import mmbt_ref as R
     from oracle.weights import make_state_dict, checksum, key_shapes

@@ -34,6 +34,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=256 * 513)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--cases", default="", help="comma-separated substrings: run only the matching cases")
+    ap.add_argument("--no-ref", action="store_true", help="skip the hipBLASLt yardstick")
     a = ap.parse_args()
     M, dev, bf = a.rows, "cuda", torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
@@ -134,10 +136,13 @@ def main():
          lambda: torch.matmul(dY.t(), O)),
     ]
     print(f"{'gemm':26s} {'M':>7s} {'N':>5s} {'K':>7s} {'mmu_gemm':>18s} {'hipBLASLt':>18s}")
+    want = [c for c in a.cases.split(",") if c]
     for name, m, n, k, f_mmu, f_ref in cases:
+        if want and not any(w in name for w in want):
+            continue
         fl = 2.0 * m * n * k
         t1 = min(timed(f_mmu, a.iters) for _ in range(3))
-        t2 = timed(f_ref, a.iters)
+        t2 = float("nan") if a.no_ref else timed(f_ref, a.iters)
         print(f"{name:26s} {m:7d} {n:5d} {k:7d} {t1:8.3f}ms {fl / t1 / 1e9:6.0f}T {t2:8.3f}ms {fl / t2 / 1e9:6.0f}T",
               flush=True)
 
