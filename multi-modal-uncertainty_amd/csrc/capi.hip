@@ -130,12 +130,6 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
   // (and 2 for the dGELU product dY2.W2, whose epilogue streams the [M, 3072] gelu' rows:
   // 0.888 -> 0.756 ms with a K-major B, profiles/r2_gemm_group_dz.txt)
   p.group_m = p.tiles_n <= 3 ? 1 : ((b_kmajor && kind != MMU_EPI_DGELU) ? 8 : 2);
-  {  // round-6 A/B switches (tools/gemm_bench.py): epilogue store policy, tile-order group height
-    static const int pol = getenv("MMU_GEMM_STORE_POL") ? atoi(getenv("MMU_GEMM_STORE_POL")) : 0;
-    static const int gm = getenv("MMU_GEMM_GROUP_M") ? atoi(getenv("MMU_GEMM_GROUP_M")) : 0;
-    p.store_pol = big ? pol : 0;
-    if (gm > 0 && p.tiles_n > 3) p.group_m = gm;
-  }
   if (epi) {
     kind = epi->kind;
     p.accumulate = epi->accumulate;

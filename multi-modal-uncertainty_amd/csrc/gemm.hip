@@ -105,21 +105,6 @@ static __device__ __forceinline__ bf16x8 s_frag(const char* s, int row0, int ks,
 // (residual / aux loads, bf16 or f32 stores, split-K slabs) is then a 16-B-per-lane
 // access covering full 128-B lines.
 
-// 16-B epilogue store with the product's cache policy: plain (the line stays in the XCD's L2) or
-// sc1 (write-through, the line is dropped from L2, so the output stream does not evict the operand
-// panels the next tiles re-read).  The buffer form carries the policy bits; its 32-bit offset is
-// relative to the wave block's first element (rb).
-typedef int mmu_v4i __attribute__((ext_vector_type(4)));
-static __device__ __forceinline__ void st16(int pol, void* ptr, __amdgpu_buffer_rsrc_t rb, uint32_t off, mmu_v4i v) {
-  if (pol == 16) __builtin_amdgcn_raw_buffer_store_b128(v, rb, off, 0, 16);
-  else *(mmu_v4i*)ptr = v;
-}
-struct EpiDst {
-  __amdgpu_buffer_rsrc_t rc, rx;  // wave-block bases of C and aux
-  uint32_t oc, ox;                // this octet's byte offsets from them
-  int pol;
-};
-
 // one (m, n..n+7) octet: epilogue math + store; v holds acc (+ bias) on entry.  The row's
 // addresses arrive precomputed (epilogue_block: a per-lane base + a wave-uniform row offset, so
 // no per-row 64-bit VALU multiplies): cdst = &C[z][m][n], xdst = &aux[z][m][n], qd = the
@@ -127,7 +112,7 @@ struct EpiDst {
 template <int EPI, bool OUT_F32>
 static __device__ __forceinline__ void epi_oct(const GemmParams& p, void* cdst, bf16* xdst, uint64_t qd,
                                                float (&v)[8], const float (&in)[8], float scale, uint32_t thr,
-                                               uint64_t seed, const EpiDst& ed) {
+                                               uint64_t seed) {
   if (EPI == MMU_EPI_BIAS_GELU) {  // C = gelu(z); aux (optional) = gelu'(z) for the backward
     float d[8];
 #pragma unroll
@@ -136,7 +121,7 @@ static __device__ __forceinline__ void epi_oct(const GemmParams& p, void* cdst, 
       bf16x8 o;
 #pragma unroll
       for (int r = 0; r < 8; ++r) o[r] = f2bf(d[r]);
-      st16(ed.pol, xdst, ed.rx, ed.ox, __builtin_bit_cast(mmu_v4i, o));
+      *(bf16x8*)xdst = o;
     }
   } else if (EPI == MMU_EPI_BIAS_DROP_RES) {
     if (thr) {  // counter over the whole batched output: batch item z, row m, column n (quads)
@@ -162,7 +147,7 @@ static __device__ __forceinline__ void epi_oct(const GemmParams& p, void* cdst, 
       bf16x8 o;
 #pragma unroll
       for (int r = 0; r < 8; ++r) o[r] = f2bf(d[r]);
-      st16(ed.pol, xdst, ed.rx, ed.ox, __builtin_bit_cast(mmu_v4i, o));
+      *(bf16x8*)xdst = o;
     }
   } else if (EPI == MMU_EPI_DGELU) {  // in = aux = gelu'(z) saved by the forward epilogue
 #pragma unroll
@@ -179,13 +164,13 @@ static __device__ __forceinline__ void epi_oct(const GemmParams& p, void* cdst, 
       lo.x += c0.x; lo.y += c0.y; lo.z += c0.z; lo.w += c0.w;
       hi.x += c1.x; hi.y += c1.y; hi.z += c1.z; hi.w += c1.w;
     }
-    st16(ed.pol, &C[0], ed.rc, ed.oc, __builtin_bit_cast(mmu_v4i, lo));
-    st16(ed.pol, &C[1], ed.rc, ed.oc + 16, __builtin_bit_cast(mmu_v4i, hi));
+    C[0] = lo;
+    C[1] = hi;
   } else {
     bf16x8 o;
 #pragma unroll
     for (int r = 0; r < 8; ++r) o[r] = f2bf(v[r]);
-    st16(ed.pol, cdst, ed.rc, ed.oc, __builtin_bit_cast(mmu_v4i, o));
+    *(bf16x8*)cdst = o;
   }
 }
 
@@ -234,17 +219,6 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
   const int64_t s_l = EPI == MMU_EPI_STORE ? m_l * p.N + n : 0;
   const int64_t q_l = DRP ? (z * p.M + m_l) * p.N + n : 0;
   const uint64_t seed = DRP && thr ? mmu_eff_seed(p.seed, p.seed_off) : 0;
-  EpiDst ed;
-  ed.pol = p.accumulate ? 0 : p.store_pol;  // (an accumulating C is read back here: keep it plain)
-  {
-    constexpr int ES = OUT_F32 ? 4 : 2;
-    ed.rc = __builtin_amdgcn_make_buffer_rsrc((char*)p.C + (z * p.sC + mw * p.ldc + nw) * ES, 0, 0x7FFFFFFF,
-                                              0x00020000);
-    ed.rx = __builtin_amdgcn_make_buffer_rsrc(aux ? (char*)(aux + mw * p.ldx + nw) : (char*)p.C, 0, 0x7FFFFFFF,
-                                              0x00020000);
-  }
-  const uint32_t oc_l = (uint32_t)((rr * p.ldc + 8 * q) * (OUT_F32 ? 4 : 2));
-  const uint32_t ox_l = XST ? (uint32_t)((rr * p.ldx + 8 * q) * 2) : 0u;
   // residual = LN(residual rows): per-column gamma / beta here, per-row mean / rstd per pass
   const bool res_ln = RES32 && p.res_ln_w != nullptr && !slab;
   float lw[8], lb[8];
@@ -327,10 +301,8 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
         for (int r = 0; r < 8; ++r) inf[r] = LOADS ? bf2f(in[RES32 ? 0 : it][r]) : 0.f;
       }
       void* cdst = OUT_F32 ? (void*)((float*)p.C + c_l + d * p.ldc) : (void*)((bf16*)p.C + c_l + d * p.ldc);
-      ed.oc = oc_l + (uint32_t)(d * p.ldc * (OUT_F32 ? 4 : 2));
-      ed.ox = XST ? ox_l + (uint32_t)(d * p.ldx * 2) : 0u;
       epi_oct<EPI, OUT_F32>(p, cdst, (XST && aux) ? aux + x_l + d * p.ldx : nullptr,
-                            DRP ? (uint64_t)(q_l + d * p.N) >> 2 : 0, v, inf, scale, thr, seed, ed);
+                            DRP ? (uint64_t)(q_l + d * p.N) >> 2 : 0, v, inf, scale, thr, seed);
       if (want_cs) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) cs[e] += v[e];

@@ -18,7 +18,6 @@ struct GemmParams {
   int64_t lda, ldb, ldc, M, N, K, sA, sB, sC;
   int tiles_m, tiles_n;
   int group_m;  // tile-order group height (gemm.hip tile_of)
-  int store_pol;  // epilogue C / aux store cache policy: 0 plain, 16 sc1 (write-through, dropped from L2)
   // epilogue (flattened mmu_epilogue)
   int kind, accumulate;
   const float* bias;
