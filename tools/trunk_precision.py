@@ -85,6 +85,10 @@ VARIANTS = {
     "f32 stream layer3+4": dict(stream_v=False, stages=(2, 3)),
     "bf16 grads only": dict(stream_v=False, conv_v=False, bn_v=False, w=False, c3=False, img=False),
     "bf16 values only": dict(stream_g=False, conv_g=False, bn_g=False),
+    "res8, f32 image": dict(res8=True, img=False),
+    "res8, f32 image + stem filter": dict(res8=True, img=False, stem_w=False),
+    "res8, f32 stem out": dict(res8=True, stem_out=False),
+    "res8, f32 image + stem filter + out": dict(res8=True, img=False, stem_w=False, stem_out=False),
 }
 
 
@@ -107,7 +111,8 @@ def trunk(sd, img, cfg, train, o, momentum=0.1):
                             training=train, momentum=momentum, eps=1e-5)
 
     x = Q(img, o.get("img", True), False)
-    x = Q(F.conv2d(x, W(RES + "0.weight"), stride=2, padding=3), cv, cg)
+    x = Q(F.conv2d(x, Q(sd[RES + "0.weight"], o.get("stem_w", wq), False), stride=2, padding=3),
+          cv and o.get("stem_out", True), cg)
     x = Q(F.relu(bn(RES + "1.", x)), bv, bg)
     x = F.max_pool2d(x, 3, 2, 1)
     for li, nblk in enumerate(cfg.resnet_blocks):
@@ -154,7 +159,7 @@ def _trunk_m(sd, img, cfg, train, momentum):
 def load(tag):
     g = np.load(os.path.join(GOLD, f"mmbt_{tag}.npz"))
     names = json.load(open(os.path.join(GOLD, f"mmbt_{tag}_keys.json")))["named_parameters"]
-    cfg = SMALL if tag.startswith("small") else FULL
+    cfg = SMALL if tag.startswith("small") else FULL  # (bn_last_gamma below: the FULL_C fixtures)
     if "bn_last_gamma" in g:
         cfg = dataclasses.replace(cfg, bn_last_gamma=float(g["bn_last_gamma"]))
     sd = make_state_dict(int(g["wseed"]), cfg)
