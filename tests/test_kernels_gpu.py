@@ -1089,3 +1089,54 @@ def test_attention_bwd_fused_bias_grad(dev, B, L, p):
     k.attention_dbias_reduce(parts, B, L, g)
     ref = dqkv.float().sum(0) + 0.5
     torch.testing.assert_close(g, ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+
+
+def _keep_bits_formula(seed, bh, q, L, p):
+    """the attention dropout stream restated (attention.hip seed_for / lowbias32 / pair_draw and the
+    tile body's register layout): keep decision of every key of query row q, head-row bh"""
+    M32 = 0xFFFFFFFF
+
+    def lowbias32(x):
+        x = np.asarray(x, dtype=np.uint64) & M32
+        x ^= x >> 16
+        x = (x * 0x7FEB352D) & M32
+        x ^= x >> 15
+        x = (x * 0x846CA68B) & M32
+        x ^= x >> 16
+        return x
+
+    mul = [0x9E3779, 0x85EBCB, 0xC2B2AF, 0xA7D4EB, 0x965667, 0xD3A265, 0xFD7047, 0xB55A4F]
+    sbh = int(lowbias32((seed & M32) ^ int(lowbias32(((seed >> 32) + 0x9E3779B9 * (bh + 1)) & M32))))
+    nkv = (L + 63) // 64
+    thr = int(p * 65536.0 + 0.5)
+    k = np.arange(nkv * 64, dtype=np.uint64)
+    hb = lowbias32(sbh + 4 * q * nkv + 2 * ((k >> 4) & 1) + 4 * (k >> 6) + ((k >> 5) & 1))
+    i = (k & 15) >> 1
+    src = np.where(i > 0, ((hb >> (4 * i)) | (hb << (32 - 4 * i))) & M32, hb)
+    x = ((src & 0xFFFFFF) * np.array(mul, dtype=np.uint64)[i]) & M32
+    hsh = x ^ (x >> 16)
+    return np.where(k & 1, hsh >= (thr << 16), (hsh & 0xFFFF) >= thr)[:L]
+
+
+@pytest.mark.parametrize("L", [513, 390])
+def test_attention_dropout_tail_rows_follow_the_stream(dev, L):
+    """L % 128 in 1..8: the rows past the last full 128-row block are computed by that block on
+    the VALU (attention.hip fwd_tail_rows).  Their keep words must be the dropout stream of the
+    tile body's layout, bit for bit: every row -- full blocks and tail -- against the restated
+    hash; and O / LSE of the tail rows against fp32 with the decoded mask."""
+    k = K()
+    B, p, seed = 2, 0.1, 0x5EED1234ABCD
+    qkv, km = make_attn_inputs(dev, B, L, pad=True, seed=31, scale=1.0)
+    O = torch.empty(B * L, 768, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(B * 12, L, device=dev)
+    dm = k.dropmask_empty(B, L, 12, dev)
+    k.attention_fwd(qkv, km, O, lse, B, L, drop_p=p, seed=seed, dropmask=dm)
+    mask = k.dropmask_dense(dm, L).view(B * 12, L, L).cpu().numpy().astype(bool)
+    tail0 = 128 * (L // 128)
+    for bh in (0, 13, B * 12 - 1):
+        for q in (0, 127, tail0 - 1) + tuple(range(tail0, L)):
+            assert np.array_equal(mask[bh, q], _keep_bits_formula(seed, bh, q, L, p)), (bh, q)
+    o_ref, lse_ref = attn_ref(qkv, km, B, L, dropmask=torch.from_numpy(mask).to(dev).view(B, 12, L, L).float(), p=p)
+    rows = torch.cat([torch.arange(b * L + tail0, (b + 1) * L) for b in range(B)]).to(dev)
+    close(O[rows], o_ref[rows], atol_frac=2e-2)
+    torch.testing.assert_close(lse[:, tail0:], lse_ref[:, tail0:], rtol=1e-4, atol=2e-3)
