@@ -236,137 +236,6 @@ static __device__ __forceinline__ void drop_pair_apply(uint32_t hsh, uint32_t th
       : "vcc");
 }
 
-// ---------------------------------------------------------------- forward: folded tail rows
-// L = 513 = 4 x 128 + 1: a 5th query block per head-row would hold ONE live query yet occupy a
-// block slot for a whole pass over K / V (the L = 513 forward ran +25 % over L = 512,
-// profiles/r4_attn_w3n_ab.txt).  When 1..FWD_TAIL_MAX rows are left past the last full block,
-// the grid stops at the full blocks and that head-row's last block computes the tail rows on the
-// VALU after its own tiles, streaming K / V from L2 (its head-row's blocks just read them: the
-// XCD remap keeps them on one L2).  Thread t: d-chunk c = t & 7 (8 columns), key group g = t >> 3
-// (keys g, g + 32, ...); a key's score is its 8 lanes' partial dot products summed by 3 xor
-// shuffles.  Same arithmetic as the MFMA path (S' = (Q / 8) K^T + mask, p = exp(S' - m), O =
-// sum keep p V / ((1 - drop) l), LSE = m + log l; P enters P V unrounded here) and the SAME
-// dropout stream: key k of row q draws from hash (seed_bh + 4 q nkv + 2 h + 4 j + s2), pair
-// (k & 15) / 2 of pair_draw, with j = k / 64, s2 = (k / 32) & 1, h = (k / 16) & 1 -- the register
-// layout of the tile body -- so the keep words the backward reads are the ones the full blocks'
-// layout would have stored.
-constexpr int FWD_TAIL_MAX = 8;
-constexpr int FWD_TAIL_NI = (FWD_MAX_NKV * 64 + 31) / 32;  // keys per thread group (<= 18)
-
-template <bool DROP, bool STORE>
-static __device__ __forceinline__ void fwd_tail_rows(const AttnParams& p, int b, int hd, int bh, int q_begin,
-                                                     char* smem) {
-  const int t = threadIdx.x, c = t & 7, g = t >> 3, w = t >> 6, lane = t & 63;
-  const int L = p.L, HD = p.heads * 64, nkv = (L + 63) / 64;
-  float* red = (float*)(smem + 16384);         // [0..3] max partials, [4..7] sum partials
-  float* ored = red + 8;                       // [4 waves][64 d]
-  uint8_t* kflag = (uint8_t*)(ored + 4 * 64);  // keep flag per key
-  const bf16* kvb = p.qkv + (int64_t)b * L * p.ld_qkv + hd * 64 + 8 * c;
-  const float* mrow = p.keymask + (int64_t)b * L;
-  const uint32_t thr = drop_thr(p.drop_p), thr_hi = thr << 16;
-  const uint32_t sbh = DROP ? seed_for(mmu_eff_seed(p.seed, p.seed_off), bh) : 0u;
-  constexpr int CH = 6;  // keys per thread group in flight (K and V rows: 2 x 6 x 16 B per lane)
-  for (int q = q_begin; q < L; ++q) {
-    float qv[8];
-    {
-      const uint4 u = *(const uint4*)(kvb + (int64_t)q * p.ld_qkv);
-      const bf16x8 v = *(const bf16x8*)&u;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) qv[e] = bf2f(f2bf(bf2f(v[e]) * 0.125f));
-    }
-    const uint32_t rbase = sbh + 4u * (uint32_t)q * (uint32_t)nkv;
-    // one pass, online softmax per thread group (the 8 lanes of a group hold the same m / l)
-    float m = NEG_INF, ls = 0.f;
-    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int i0 = 0; i0 < FWD_TAIL_NI; i0 += CH) {
-      uint4 kr[CH], vr[CH];
-#pragma unroll
-      for (int u = 0; u < CH; ++u) {
-        const int k = g + 32 * (i0 + u);
-        kr[u] = k < L ? *(const uint4*)(kvb + (int64_t)k * p.ld_qkv + HD) : make_uint4(0, 0, 0, 0);
-        vr[u] = k < L ? *(const uint4*)(kvb + (int64_t)k * p.ld_qkv + 2 * HD) : make_uint4(0, 0, 0, 0);
-      }
-      float sv[CH];
-      float cm = m;
-#pragma unroll
-      for (int u = 0; u < CH; ++u) {
-        const bf16x8 kv = *(const bf16x8*)&kr[u];
-        float d = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) d = fmaf(qv[e], bf2f(kv[e]), d);
-        d += __shfl_xor(d, 1, 64);
-        d += __shfl_xor(d, 2, 64);
-        d += __shfl_xor(d, 4, 64);
-        const int k = g + 32 * (i0 + u);
-        sv[u] = k < L ? d + mrow[k] : NEG_INF;
-        cm = __builtin_fmaxf(cm, sv[u]);
-      }
-      if (cm > NEG_INF) {  // (a group whose keys are all past L keeps m = -inf, l = o = 0)
-        const float alpha = __builtin_amdgcn_exp2f((m - cm) * LOG2E);  // exp2(-inf) = 0 on the first chunk
-        ls *= alpha;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] *= alpha;
-        m = cm;
-      }
-      const float nml = -m * LOG2E;
-#pragma unroll
-      for (int u = 0; u < CH; ++u) {
-        const int k = g + 32 * (i0 + u);
-        float pe = __builtin_amdgcn_exp2f(fmaf(sv[u], LOG2E, nml));  // 0 past L
-        ls += pe;
-        bool keep = true;
-        if (DROP) {  // the tile body's stream: row q, tile k / 64, half (k / 32) & 1, half-wave (k / 16) & 1
-          const uint32_t hb = lowbias32(rbase + 2u * (uint32_t)((k >> 4) & 1) + 4u * (uint32_t)(k >> 6) +
-                                        (uint32_t)((k >> 5) & 1));
-          const uint32_t hsh = pair_draw(hb, (k & 15) >> 1);
-          keep = (k & 1) ? hsh >= thr_hi : (hsh & 0xFFFFu) >= thr;
-          pe = keep ? pe : 0.f;
-        }
-        if (STORE && DROP && c == 0 && k < nkv * 64) kflag[k] = keep ? 1 : 0;
-        const bf16x8 vv = *(const bf16x8*)&vr[u];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = fmaf(pe, bf2f(vv[e]), o[e]);
-      }
-    }
-    // combine the 32 groups: block max, rescale, then sums
-    float mx = wave_max(m);
-    if (lane == 0) red[w] = mx;
-    __syncthreads();
-    mx = __builtin_fmaxf(__builtin_fmaxf(red[0], red[1]), __builtin_fmaxf(red[2], red[3]));
-    const float sc = m > NEG_INF ? __builtin_amdgcn_exp2f((m - mx) * LOG2E) : 0.f;
-    ls = c == 0 ? ls * sc : 0.f;  // one copy of each group's row sum
-    ls = wave_sum(ls);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {  // over the 8 key groups of the wave (lane bits 3..5)
-      float v = o[e] * sc;
-      v += __shfl_xor(v, 8, 64);
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      o[e] = v;
-    }
-    if (lane == 0) red[4 + w] = ls;
-    if (lane < 8) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) ored[w * 64 + 8 * c + e] = o[e];
-    }
-    __syncthreads();
-    const float lsum = (red[4] + red[5]) + (red[6] + red[7]);
-    if (t < 64) {
-      const float inv = (DROP ? 1.0f / (1.0f - p.drop_p) : 1.0f) / lsum;
-      const float od = (ored[t] + ored[64 + t]) + (ored[128 + t] + ored[192 + t]);
-      p.out[((int64_t)b * L + q) * p.ld_out + hd * 64 + t] = f2bf(od * inv);
-      if (t == 0) p.lse[(int64_t)bh * L + q] = mx + logf(lsum);
-    }
-    if (STORE && DROP && p.dropmask != nullptr && t < nkv) {
-      uint64_t wd = 0;
-      for (int e = 0; e < 64; ++e) wd |= (uint64_t)(kflag[64 * t + e] & 1) << e;
-      p.dropmask[((int64_t)bh * L + q) * nkv + t] = wd;
-    }
-    __syncthreads();  // red / ored / kflag are reused by the next tail row
-  }
-}
-
 // STORE = false: dropout without the keep-bit words (p.dropmask ignored): MC-dropout
 // inference, where no backward reads them; fewer live registers -> 3 waves / SIMD
 template <bool DROP, int WPE, bool NOHOIST, bool STORE = true>
@@ -596,16 +465,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     if (q0w + r < L)
       *(uint4*)(ob + ((int64_t)b * L + q0w + r) * p.ld_out + 8 * c) = *(const uint4*)(os + r * 128 + ((c ^ (r & 7)) << 4));
   }
-  // the rows past the last full block (grid folded by attention_fwd_launch): this head-row's
-  // last block computes them (its O staging above stays below smem + 16 KiB)
-  if (bx == (int)gridDim.x - 1 && 128 * (int)gridDim.x < L) fwd_tail_rows<DROP, STORE>(p, b, hd, bh, 128 * gridDim.x, smem);
 }
 
 void attention_fwd_launch(const AttnParams& p, hipStream_t s) {
-  // 1..FWD_TAIL_MAX rows past the last full 128-row block fold into it (fwd_tail_rows)
-  const int rem = p.L % 128;
-  const bool fold = p.L > 128 && rem != 0 && rem <= FWD_TAIL_MAX;
-  dim3 grid(fold ? p.L / 128 : (p.L + 127) / 128, p.batch * p.heads);
+  dim3 grid((p.L + 127) / 128, p.batch * p.heads);
   if (drop_thr(p.drop_p) && !p.dropmask) {
     // inference dropout (MC-dropout passes): no keep bits to store, 3 waves / SIMD
     hipLaunchKernelGGL((attn_fwd_v2_kernel<true, 3, true, false>), grid, dim3(256), 0, s, p);

@@ -1120,10 +1120,11 @@ def _keep_bits_formula(seed, bh, q, L, p):
 
 @pytest.mark.parametrize("L", [513, 390])
 def test_attention_dropout_tail_rows_follow_the_stream(dev, L):
-    """L % 128 in 1..8: the rows past the last full 128-row block are computed by that block on
-    the VALU (attention.hip fwd_tail_rows).  Their keep words must be the dropout stream of the
-    tile body's layout, bit for bit: every row -- full blocks and tail -- against the restated
-    hash; and O / LSE of the tail rows against fp32 with the decoded mask."""
+    """The forward's keep words are the restated dropout stream bit for bit (attention.hip
+    seed_for / pair_draw over the tile body's register layout), for rows of full query blocks and
+    for the rows past the last full 128-row block (L = 513: one; 390: six); O / LSE of those tail
+    rows against fp32 with the decoded mask.  (Round 6 used it to check a folded-tail forward,
+    profiles/r6_attn_tailfold_ab.txt: the stream is what the backward's bits must match.)"""
     k = K()
     B, p, seed = 2, 0.1, 0x5EED1234ABCD
     qkv, km = make_attn_inputs(dev, B, L, pad=True, seed=31, scale=1.0)
