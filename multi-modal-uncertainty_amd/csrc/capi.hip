@@ -118,14 +118,7 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
   // 32-bit buffer offsets of those out-of-range reads never wrap back into the operand)
   const int64_t a_span = 2 * (a_kmajor ? (M + 256) * lda : (K + 64) * lda);
   const int64_t b_span = 2 * (b_kmajor ? (N + 256) * ldb : (K + 64) * ldb);
-  bool big = M >= 256 && N >= 256 && a_span < (1ll << 32) - 4096 && b_span < (1ll << 32) - 4096;
-  {  // round-6 A/B: split-K weight-gradient products on the 128x128 / 4-wave tiles (room for the
-     // main stream's chain kernels beside them on a CU)
-    static const bool ws_small = getenv("MMU_WGRAD_SMALL") && atoi(getenv("MMU_WGRAD_SMALL")) == 1;
-    if (ws_small && big && epi && epi->workspace && K >= 1024 && c_dtype == MMU_F32 && epi->kind == MMU_EPI_STORE &&
-        !epi->bias && !epi->colsum)
-      big = false;
-  }
+  const bool big = M >= 256 && N >= 256 && a_span < (1ll << 32) - 4096 && b_span < (1ll << 32) - 4096;
   const int tile = big ? 256 : 128;
   p.tiles_m = (int)((M + tile - 1) / tile);
   p.tiles_n = (int)((N + tile - 1) / tile);
