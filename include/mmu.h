@@ -30,10 +30,11 @@ typedef void* mmu_stream_t; /* hipStream_t */
 enum { MMU_BF16 = 0, MMU_F32 = 1 };
 
 /* ------------------------------------------------------------------ status */
-/* ABI version: bumped whenever an entry's argument list changes.  2 (round 5): the residual
- * stream's residue pointers inside mmu_batchnorm_fwd / _fwd_sums and the grad_scale argument
- * of mmu_bertadam_step.  Callers compare mmu_version() with the header they were built against. */
-#define MMU_ABI_VERSION 2
+/* ABI version: bumped whenever an entry's argument list or buffer contract changes.  2 (round 5):
+ * the residual stream's residue pointers inside mmu_batchnorm_fwd / _fwd_sums and the grad_scale
+ * argument of mmu_bertadam_step.  3 (round 6): mmu_embed_bwd's workspace size is
+ * mmu_embed_bwd_ws_floats().  Callers compare mmu_version() with the header they were built against. */
+#define MMU_ABI_VERSION 3
 int mmu_version(void);
 const char* mmu_last_error(void);
 
@@ -238,7 +239,9 @@ int mmu_embed_fwd(const int64_t* ids, const int64_t* seg, const int64_t* txt_mas
 /* Backward of mmu_embed_fwd for the identity variant (training): recomputes the
  * pre-LN sums, LN backward, then scatters: word rows by atomics, position / type
  * / [CLS] / [SEP] by batch reduction, image rows to dproj f32 [B, n_img, H].
- * ws: f32 workspace of B*S*H + 2*ceil(B*S/64)*H floats. */
+ * ws: f32 workspace of at least mmu_embed_bwd_ws_floats(B, T, n_img) floats (ABI 3; ABI 2 took
+ * B*S*H + 2*ceil(B*S/64)*H, which is larger for every B > 1). */
+int64_t mmu_embed_bwd_ws_floats(int64_t B, int64_t T, int64_t n_img);
 int mmu_embed_bwd(const void* dX, const int64_t* ids, const int64_t* seg,
                   const float* proj, const float* word, const float* pos, const float* type,
                   const float* ln_w, const float* mean, const float* rstd,

@@ -388,6 +388,10 @@ int mmu_embed_fwd(const int64_t* ids, const int64_t* seg, const int64_t* txt_mas
   return check_launch("mmu_embed_fwd");
 }
 
+int64_t mmu_embed_bwd_ws_floats(int64_t B, int64_t T, int64_t n_img) {
+  return 4 * embed_bwd_blocks(B, n_img + 2 + T) * 768;
+}
+
 int mmu_embed_bwd(const void* dX, const int64_t* ids, const int64_t* seg, const float* proj, const float* word,
                   const float* pos, const float* type, const float* ln_w, const float* mean, const float* rstd,
                   int64_t cls_id, int64_t sep_id, int64_t B, int64_t T, int64_t n_img, int64_t H, float drop_txt,

@@ -100,29 +100,43 @@ void embed_fwd_launch(const EmbedParams& p, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- backward
-// phase 1: per row LN backward -> dsum (ws), word-row atomics for text rows, dproj for image rows,
-//          per-64-row partial sums of dgamma / dbeta
+// One pass over the rows, position-major: a block = 4 consecutive source positions (one per wave)
+// x EBW_B samples, so each wave sums its position's gradient over its samples in registers.  Per
+// row: LN backward (dropout of the forward regenerated), the word-row scatter for text rows (f32
+// atomics, 256 contiguous bytes per instruction), the image rows' dproj.  Per wave: its position
+// sum into the position row / [CLS] / [SEP] word rows (f32 atomics, ceil(B / EBW_B) adds per
+// address).  Per block: partial rows of dgamma, dbeta and the two token-type rows, folded by
+// colsum_reduce.  (Round 6: the batch sums used to go through an f32 [B, S, H] copy of the row
+// gradients and a second kernel walking it column-wise: 0.69 ms at B = 256 for 0.4 GB.)
+constexpr int EBW_B = 16;  // samples per block
 __global__ __launch_bounds__(256) void embed_bwd_rows_kernel(EmbedBwdParams q, EmbedParams p) {
-  __shared__ float red[2][4][768];
+  __shared__ float red[4][4][768];                            // aw, ab, type-0, type-1 per wave
   __shared__ __attribute__((aligned(16))) float xch[4][768];  // per wave: a text row's dx, re-read lane-contiguous
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t S = q.n_img + 2 + q.T, rows = q.B * S, H = 768;
-  float* dsum = q.ws;
-  float* part = q.ws + rows * H;
-  const int64_t nparts = (rows + 63) / 64;
-  float aw[3][4], ab[3][4], w[3][4];
+  const int64_t S = q.n_img + 2 + q.T, H = 768;
+  const int64_t nblk = (int64_t)gridDim.x * gridDim.y;
+  const int64_t blk = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  float* part = q.ws;
+  const int64_t s = (int64_t)blockIdx.x * 4 + wv;
+  const int64_t b0 = (int64_t)blockIdx.y * EBW_B;
+  const bool live = s < S;
+  const bool text = s >= q.n_img + 2, img = s >= 1 && s <= q.n_img;
+  const float dp = s <= q.n_img + 1 ? q.drop_img : q.drop_txt;
+  const uint32_t thr = (uint32_t)(dp * 65536.0f + 0.5f);
+  const float dsc = dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f;
+  float aw[3][4], ab[3][4], w[3][4], tot[3][4], t1[3][4];
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { aw[i][k] = ab[i][k] = 0.f; w[i][k] = q.ln_w[256 * i + 4 * l + k]; }
-  for (int64_t row = (int64_t)blockIdx.x * 64 + wv; row < (int64_t)blockIdx.x * 64 + 64 && row < rows; row += 4) {
-    const int64_t b = row / S, s = row % S;
+    for (int k = 0; k < 4; ++k) {
+      aw[i][k] = ab[i][k] = tot[i][k] = t1[i][k] = 0.f;
+      w[i][k] = q.ln_w[256 * i + 4 * l + k];
+    }
+  for (int64_t b = b0; live && b < b0 + EBW_B && b < q.B; ++b) {
+    const int64_t row = b * S + s;
     float e[3][4], km;
     embed_sum(e, p, b, s, l, km);
     const float mu = q.mean[row], rs = q.rstd[row];
-    const float dp = s <= q.n_img + 1 ? q.drop_img : q.drop_txt;
-    const uint32_t thr = (uint32_t)(dp * 65536.0f + 0.5f);
-    const float dsc = dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f;
     float g[3][4], xh[3][4], s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -141,15 +155,18 @@ __global__ __launch_bounds__(256) void embed_bwd_rows_kernel(EmbedBwdParams q, E
     }
     s1 = wave_sum(s1) / 768.f;
     s2 = wave_sum(s2) / 768.f;
-    const bool text = s >= q.n_img + 2, img = s >= 1 && s <= q.n_img;
+    const bool seg1 = text && q.seg[b * q.T + (s - q.n_img - 2)] != 0;
     float* wrow = text ? q.d_word + q.ids[b * q.T + (s - q.n_img - 2)] * H : nullptr;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int c = 256 * i + 4 * l;
       float dx[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) dx[k] = rs * (g[i][k] - s1 - xh[i][k] * s2);
-      *(float4*)(dsum + row * H + c) = make_float4(dx[0], dx[1], dx[2], dx[3]);
+      for (int k = 0; k < 4; ++k) {
+        dx[k] = rs * (g[i][k] - s1 - xh[i][k] * s2);
+        tot[i][k] += dx[k];
+        if (seg1) t1[i][k] += dx[k];
+      }
       if (text) {
         *(float4*)(&xch[wv][c]) = make_float4(dx[0], dx[1], dx[2], dx[3]);
       } else if (img) {
@@ -165,41 +182,36 @@ __global__ __launch_bounds__(256) void embed_bwd_rows_kernel(EmbedBwdParams q, E
       __builtin_amdgcn_wave_barrier();
     }
   }
+  if (live) {  // this position's sum over the block's samples: position row, [CLS] / [SEP] word rows
+    const int64_t posr = text ? s - q.n_img - 2 : s;
+    float* wr = s == 0 ? q.d_word + q.cls_id * H : (s == q.n_img + 1 ? q.d_word + q.sep_id * H : nullptr);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = 256 * i + 4 * l + k;
+        atomicAdd(q.d_pos + posr * H + c, tot[i][k]);
+        if (wr) atomicAdd(wr + c, tot[i][k]);
+      }
+  }
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      red[0][wv][256 * i + 4 * l + k] = aw[i][k];
-      red[1][wv][256 * i + 4 * l + k] = ab[i][k];
+      const int c = 256 * i + 4 * l + k;
+      red[0][wv][c] = aw[i][k];
+      red[1][wv][c] = ab[i][k];
+      red[2][wv][c] = tot[i][k] - t1[i][k];  // token type 0 (every image-segment row, text rows with seg 0)
+      red[3][wv][c] = t1[i][k];
     }
   __syncthreads();
-  for (int c = threadIdx.x; c < 768; c += 256) {
-    part[(int64_t)blockIdx.x * H + c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
-    part[(nparts + blockIdx.x) * H + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
-  }
+  for (int c = threadIdx.x; c < 768; c += 256)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      part[(r * nblk + blk) * H + c] = (red[r][0][c] + red[r][1][c]) + (red[r][2][c] + red[r][3][c]);
 }
 
-// phase 2: per source position s, sum dsum over the batch into position / token-type / [CLS]/[SEP] rows
-__global__ __launch_bounds__(256) void embed_bwd_batch_kernel(EmbedBwdParams q) {
-  const int64_t S = q.n_img + 2 + q.T, H = 768;
-  const int64_t s = blockIdx.x;
-  const int c = blockIdx.y * 256 + threadIdx.x;
-  if (c >= H) return;
-  const float* dsum = q.ws;
-  float tot = 0.f, t1 = 0.f;
-  const bool text = s >= q.n_img + 2;
-  for (int64_t b = 0; b < q.B; ++b) {
-    const float v = dsum[(b * S + s) * H + c];
-    tot += v;
-    if (text && q.seg[b * q.T + (s - q.n_img - 2)] != 0) t1 += v;
-  }
-  const int64_t posr = text ? s - q.n_img - 2 : s;
-  atomicAdd(q.d_pos + posr * H + c, tot);
-  atomicAdd(q.d_type + c, tot - t1);
-  if (text) atomicAdd(q.d_type + H + c, t1);
-  if (s == 0) atomicAdd(q.d_word + q.cls_id * H + c, tot);
-  if (s == q.n_img + 1) atomicAdd(q.d_word + q.sep_id * H + c, tot);
-}
+int64_t embed_bwd_blocks(int64_t B, int64_t S) { return ((S + 3) / 4) * ((B + EBW_B - 1) / EBW_B); }
 
 void embed_bwd_launch(const EmbedBwdParams& q, hipStream_t s) {
   EmbedParams p{};
@@ -207,12 +219,14 @@ void embed_bwd_launch(const EmbedBwdParams& q, hipStream_t s) {
   p.proj = q.proj; p.word = q.word; p.pos = q.pos; p.type = q.type;
   p.cls_id = q.cls_id; p.sep_id = q.sep_id; p.V = 1; p.B = q.B; p.T = q.T; p.n_img = q.n_img;
   p.Lout = q.n_img + 2 + q.T; p.H = 768;
-  const int64_t rows = q.B * p.Lout, nparts = (rows + 63) / 64;
-  hipLaunchKernelGGL(embed_bwd_rows_kernel, dim3((unsigned)nparts), dim3(256), 0, s, q, p);
-  hipLaunchKernelGGL(embed_bwd_batch_kernel, dim3((unsigned)p.Lout, 3), dim3(256), 0, s, q);
-  float* part = q.ws + rows * 768;
-  colsum_reduce_launch(part, nparts, 768, q.d_ln_w, 1, s);
-  colsum_reduce_launch(part + nparts * 768, nparts, 768, q.d_ln_b, 1, s);
+  const int64_t nblk = embed_bwd_blocks(q.B, p.Lout);
+  hipLaunchKernelGGL(embed_bwd_rows_kernel, dim3((unsigned)((p.Lout + 3) / 4), (unsigned)((q.B + EBW_B - 1) / EBW_B)),
+                     dim3(256), 0, s, q, p);
+  const float* part = q.ws;
+  colsum_reduce_launch(part, nblk, 768, q.d_ln_w, 1, s);
+  colsum_reduce_launch(part + nblk * 768, nblk, 768, q.d_ln_b, 1, s);
+  colsum_reduce_launch(part + 2 * nblk * 768, nblk, 768, q.d_type, 1, s);
+  colsum_reduce_launch(part + 3 * nblk * 768, nblk, 768, q.d_type + 768, 1, s);
 }
 
 // ---------------------------------------------------------------- AdaptiveAvgPool2d((n,1))

@@ -141,6 +141,7 @@ struct EmbedBwdParams {
   float *d_word, *d_pos, *d_type, *d_ln_w, *d_ln_b, *d_proj, *ws;
 };
 void embed_bwd_launch(const EmbedBwdParams& p, hipStream_t s);
+int64_t embed_bwd_blocks(int64_t B, int64_t S);
 void image_normalize_launch(const uint8_t* in, int64_t n, const float* mean, const float* stdv, void* out,
                             bool out_bf16, hipStream_t s);
 void maxpool3s2_fwd_launch(const bf16* x, int64_t B, int H, int W, int C, int OH, int OW, bf16* y, uint8_t* am,

@@ -30,6 +30,7 @@ class Epilogue(ctypes.Structure):
 # name -> (restype, argtypes); every entry must be exported by the library (tested on CPU)
 SIGNATURES = {
     "mmu_version": (c_i32, []),
+    "mmu_embed_bwd_ws_floats": (c_i64, [c_i64, c_i64, c_i64]),
     "mmu_last_error": (ctypes.c_char_p, []),
     "mmu_set_seed_offset": (c_i32, [c_vp]),
     "mmu_gemm": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_i64, c_i64, c_i64,
@@ -102,7 +103,7 @@ class NativeError(RuntimeError):
 
 
 # include/mmu.h MMU_ABI_VERSION: the argument lists SIGNATURES binds
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 def load():

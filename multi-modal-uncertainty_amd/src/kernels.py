@@ -318,9 +318,7 @@ def embed_fwd(ids, seg, txt_mask, proj, word, pos, typ, ln_w, ln_b, eps, cls_id,
 def embed_bwd(dX, ids, seg, proj, word, pos, typ, ln_w, mean, rstd, cls_id, sep_id, B, T, n_img, d_word, d_pos,
               d_type, d_ln_w, d_ln_b, d_proj, drop_txt=0.0, drop_img=0.0, seed=0):
     _dev_check(dX, proj, word, d_word, d_proj)
-    S = n_img + 2 + T
-    rows = B * S
-    ws = torch.empty(rows * 768 + 2 * ((rows + 63) // 64) * 768, dtype=torch.float32, device=dX.device)
+    ws = torch.empty(N.load().mmu_embed_bwd_ws_floats(B, T, n_img), dtype=torch.float32, device=dX.device)
     N.call("mmu_embed_bwd", _ptr(dX), _ptr(ids), _ptr(seg), _ptr(proj), _ptr(word), _ptr(pos), _ptr(typ),
            _ptr(ln_w), _ptr(mean), _ptr(rstd), int(cls_id), int(sep_id), B, T, n_img, 768, float(drop_txt),
            float(drop_img), int(seed), _ptr(d_word),

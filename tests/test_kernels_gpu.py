@@ -1141,3 +1141,48 @@ def test_attention_dropout_tail_rows_follow_the_stream(dev, L):
     rows = torch.cat([torch.arange(b * L + tail0, (b + 1) * L) for b in range(B)]).to(dev)
     close(O[rows], o_ref[rows], atol_frac=2e-2)
     torch.testing.assert_close(lse[:, tail0:], lse_ref[:, tail0:], rtol=1e-4, atol=2e-3)
+
+
+@pytest.mark.parametrize("B,T", [(1, 16), (3, 17), (20, 9)])
+def test_embed_bwd_matches_autograd(dev, B, T):
+    """mmu_embed_bwd (round 6: position-major, position / type / [CLS] / [SEP] sums per wave and
+    per block, no f32 copy of the row gradients) against autograd of the same embedding + LN in
+    fp32: word (incl. [CLS] / [SEP] rows), position, token-type, LN weight / bias and image
+    projection gradients.  (1, 16): S = 21 positions, a 1-wave last position group; (20, 9): two
+    sample chunks per position group."""
+    k = K()
+    torch.manual_seed(B * 100 + T)
+    n, V, H, cls_id, sep_id, eps = 3, 300, 768, 101, 102, 1e-12
+    word, pos, typ = (torch.randn(V, H, device=dev) * 0.05, torch.randn(512, H, device=dev) * 0.05,
+                      torch.randn(2, H, device=dev) * 0.05)
+    lw, lb = 1 + 0.1 * torch.randn(H, device=dev), 0.1 * torch.randn(H, device=dev)
+    proj = torch.randn(B, n, H, device=dev) * 0.05
+    ids = torch.randint(200, V, (B, T), device=dev)
+    seg = torch.randint(0, 2, (B, T), device=dev)
+    S = n + 2 + T
+    X = torch.empty(B * S, H, dtype=torch.bfloat16, device=dev)
+    km = torch.empty(B, S, device=dev)
+    mean, rstd = torch.empty(B * S, device=dev), torch.empty(B * S, device=dev)
+    k.embed_fwd(ids, seg, torch.ones_like(ids), proj, word, pos, typ, lw, lb, eps, cls_id, sep_id, None, 1, B, T, n, S,
+                X, km, mean, rstd)
+    G = (torch.randn(B * S, H, device=dev)).to(torch.bfloat16)
+    grads = [torch.zeros_like(t) for t in (word, pos, typ, lw, lb)]
+    d_proj = torch.empty_like(proj)
+    k.embed_bwd(G, ids, seg, proj, word, pos, typ, lw, mean, rstd, cls_id, sep_id, B, T, n, *grads, d_proj)
+    # fp32 autograd reference of the same rows
+    leaves = [t.clone().requires_grad_(True) for t in (word, pos, typ, lw, lb, proj)]
+    w_, p_, t_, lw_, lb_, pr_ = leaves
+    rows = []
+    for b in range(B):
+        rows.append(w_[cls_id] + p_[0] + t_[0])
+        for s in range(n):
+            rows.append(pr_[b, s] + p_[1 + s] + t_[0])
+        rows.append(w_[sep_id] + p_[n + 1] + t_[0])
+        for t in range(T):
+            rows.append(w_[ids[b, t]] + p_[t] + t_[seg[b, t]])
+    e = torch.stack(rows)
+    y = torch.nn.functional.layer_norm(e, (H,), lw_, lb_, eps)
+    (y * G.float()).sum().backward()
+    for got, ref, name in zip(grads + [d_proj], [l_.grad for l_ in leaves], ("word", "pos", "type", "ln_w", "ln_b",
+                                                                          "proj")):
+        torch.testing.assert_close(got, ref, rtol=2e-3, atol=2e-3 * ref.abs().max().item(), msg=name)
