@@ -65,9 +65,14 @@ enum {
                                residual is f32 too (the encoder's f32 hidden stream)    */
   MMU_EPI_DGELU = 3,        /* C = acc * aux   (aux = the forward's gelu'(z))            */
   MMU_EPI_ADD_RES = 4,      /* C = acc + residual                                        */
-  MMU_EPI_BIAS_DROP_QGELU = 5 /* u = dropout(acc+bias); C = u*sigmoid(1.702u); aux (optional)
+  MMU_EPI_BIAS_DROP_QGELU = 5,/* u = dropout(acc+bias); C = u*sigmoid(1.702u); aux (optional)
                                = keep/(1-p) * d(u*sigmoid(1.702u))/du: FLAVA ResidualAttentionBlock
                                mlp c_fc -> Dropout -> QuickGELU (src/model.py:183-185,196-198) */
+  MMU_EPI_STORE_STATS = 6     /* C = acc (+bias) in bf16, and `colsum` = a float2 table
+                               [ceil(M/64)][N] of {sum, sum of squares} of the stored C per column
+                               and 64-row block: the training BatchNorm statistics of a conv
+                               output, produced by the conv's own epilogue (round 6;
+                               mmu_batchnorm_fwd_parts consumes it).  batch 1, no split-K. */
 };
 typedef struct mmu_epilogue {
   int32_t kind;
@@ -306,6 +311,12 @@ int mmu_conv3x3_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, 
 int mmu_conv_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
                       int64_t N, int64_t ksize, int64_t stride, float* ws, int64_t ws_floats,
                       mmu_stream_t stream);
+/* mmu_conv_implicit that also writes the training BatchNorm statistics of Y: stats = float2
+ * [ceil(Npix / 64)][N] {sum, sum of squares} per output channel and 64-pixel block of the bf16
+ * Y (MMU_EPI_STORE_STATS; with split-K they come from a pass over Y after its reduction). */
+int mmu_conv_implicit_stats(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
+                            int64_t N, int64_t ksize, int64_t stride, float* stats, float* ws, int64_t ws_floats,
+                            mmu_stream_t stream);
 int mmu_conv_wgrad(const void* dY, const void* X, float* dW, int64_t n_img, int64_t H, int64_t W, int64_t Cin,
                    int64_t Cout, int64_t ksize, int64_t stride, int accumulate, float* ws, int64_t ws_floats,
                    mmu_stream_t stream);
@@ -353,6 +364,15 @@ int mmu_batchnorm_fwd(const void* X, const void* skip, void* Y, int64_t rows, in
                       int64_t* num_batches_tracked, int training, float momentum, float eps, int relu,
                       float* save_mean, float* save_invstd, void* relu_mask, const void* skip_res, void* y_res,
                       void* ws, int64_t ws_bytes, mmu_stream_t stream);
+/* Training-mode forward whose batch statistics were produced by the conv before it
+ * (MMU_EPI_STORE_STATS / mmu_conv_implicit_stats: parts = float2 [nparts][C] block partials of
+ * X's {sum, sum of squares} per channel): no statistics pass; finalize (running stats,
+ * save_mean / save_invstd) and apply as mmu_batchnorm_fwd with training = 1. */
+int mmu_batchnorm_fwd_parts(const void* X, const void* skip, void* Y, int64_t rows, int64_t C, const float* parts,
+                            int64_t nparts, const float* weight, const float* bias, float* running_mean,
+                            float* running_var, int64_t* num_batches_tracked, float momentum, float eps, int relu,
+                            float* save_mean, float* save_invstd, void* relu_mask, const void* skip_res, void* y_res,
+                            void* ws, int64_t ws_bytes, mmu_stream_t stream);
 /* Training-mode backward.  g = dY * [Y > 0] when relu, from relu_mask when given (the
  * forward's mask), else from Y (the forward's output); g = dY without relu;
  * dX [rows, C] bf16; dSkip (may be NULL) = g, the gradient of the residual input;

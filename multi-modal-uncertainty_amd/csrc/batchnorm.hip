@@ -414,12 +414,15 @@ int64_t batchnorm_ws_bytes(int64_t C) { return BN_MAX_PART_ELEMS * 8 + ((3 * C +
 
 void batchnorm_fwd_launch(const BnFwdParams& q, hipStream_t s) {
   const BnGrid G = bn_grid(q.rows, q.C);
-  const int nparts = (int)G.grid.x;
   float* coef = (float*)q.ws;
-  float2* part = (float2*)(coef + ((3 * q.C + 3) & ~3));
+  // the statistics: the producing conv's table (q.parts, its epilogue's 64-row blocks), or this
+  // launch's own stats pass into the workspace
+  const float2* part = q.parts ? (const float2*)q.parts : (const float2*)(coef + ((3 * q.C + 3) & ~3));
+  const int nparts = q.parts ? (int)q.nparts : (int)G.grid.x;
   const dim3 fin((q.C + BN_FIN_CH - 1) / BN_FIN_CH);
-  if (q.training && !q.gsum)
-    hipLaunchKernelGGL(bn_stats_kernel, G.grid, dim3(BN_THREADS), 0, s, q.X, q.rows, q.C, G.CH, G.rpb, part);
+  if (q.training && !q.gsum && !q.parts)
+    hipLaunchKernelGGL(bn_stats_kernel, G.grid, dim3(BN_THREADS), 0, s, q.X, q.rows, q.C, G.CH, G.rpb,
+                       (float2*)part);
   if (q.lsum) {  // cross-rank statistics, first half: the local sums for the exchange
     hipLaunchKernelGGL(bn_local_sums_kernel, fin, dim3(BN_THREADS), 0, s, part, nparts, q.rows, q.C, q.lsum,
                        nullptr, nullptr, nullptr);

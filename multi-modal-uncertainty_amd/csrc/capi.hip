@@ -142,7 +142,9 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
     p.res_ln_w = epi->res_ln_w; p.res_ln_b = epi->res_ln_b; p.res_ln_bstride = epi->res_ln_bstride;
   }
   p.kind = kind;
-  if (kind < 0 || kind > MMU_EPI_BIAS_DROP_QGELU) return fail("mmu_gemm: bad epilogue kind %d", kind);
+  if (kind < 0 || kind > MMU_EPI_STORE_STATS) return fail("mmu_gemm: bad epilogue kind %d", kind);
+  if (kind == MMU_EPI_STORE_STATS && (!p.colsum || batch != 1 || !a_kmajor || !b_kmajor || p.accumulate))
+    return fail("mmu_gemm: STORE_STATS needs the stats table (colsum), batch 1, K-major A and B, no accumulate");
   if (kind != MMU_EPI_STORE && kind != MMU_EPI_BIAS_DROP_RES && c_dtype != MMU_BF16)
     return fail("mmu_gemm: fused epilogues other than BIAS_DROP_RES write bf16");
   if (kind == MMU_EPI_BIAS_DROP_RES && c_dtype == MMU_F32 && (ldc % 4 || (epi && epi->ldr % 4)))
@@ -552,8 +554,9 @@ int mmu_stem_conv_wgrad(const void* dY, const void* X, float* dW, int64_t n_img,
   return check_launch("mmu_stem_conv_wgrad");
 }
 
-int mmu_conv_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
-                      int64_t N, int64_t ksize, int64_t stride, float* ws, int64_t ws_floats, mmu_stream_t stream) {
+static int conv_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
+                         int64_t N, int64_t ksize, int64_t stride, float* stats, float* ws, int64_t ws_floats,
+                         mmu_stream_t stream) {
   if (!X || !Wk || !Y) return fail("mmu_conv_implicit: null pointer");
   if (C % 64 || N % 64 || N <= 0)
     return fail("mmu_conv_implicit: needs C %% 64 == 0, N %% 64 == 0 (C=%ld N=%ld)", C, N);
@@ -574,7 +577,8 @@ int mmu_conv_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int
   p.tiles_m = (int)((M + tm_ - 1) / tm_);
   p.tiles_n = (int)((N + tn_ - 1) / tn_);
   p.group_m = 1;
-  p.kind = MMU_EPI_STORE;
+  p.kind = stats ? MMU_EPI_STORE_STATS : MMU_EPI_STORE;
+  p.colsum = stats;
   p.splitk = 1;
   p.kchunk = p.K;
   // split K (taps x channels) when the map has fewer tiles than half the CUs: ~512 blocks, >= 4
@@ -595,9 +599,21 @@ int mmu_conv_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int
   return check_launch("mmu_conv_implicit");
 }
 
+int mmu_conv_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
+                      int64_t N, int64_t ksize, int64_t stride, float* ws, int64_t ws_floats, mmu_stream_t stream) {
+  return conv_implicit(X, Wk, Y, n_img, H, W, C, N, ksize, stride, nullptr, ws, ws_floats, stream);
+}
+
+int mmu_conv_implicit_stats(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
+                            int64_t N, int64_t ksize, int64_t stride, float* stats, float* ws, int64_t ws_floats,
+                            mmu_stream_t stream) {
+  if (!stats) return fail("mmu_conv_implicit_stats: null stats table");
+  return conv_implicit(X, Wk, Y, n_img, H, W, C, N, ksize, stride, stats, ws, ws_floats, stream);
+}
+
 int mmu_conv3x3_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
                          int64_t N, float* ws, int64_t ws_floats, mmu_stream_t stream) {
-  return mmu_conv_implicit(X, Wk, Y, n_img, H, W, C, N, 3, 1, ws, ws_floats, stream);
+  return conv_implicit(X, Wk, Y, n_img, H, W, C, N, 3, 1, nullptr, ws, ws_floats, stream);
 }
 
 int64_t mmu_batchnorm_ws_bytes(int64_t C) { return batchnorm_ws_bytes(C); }
@@ -694,6 +710,33 @@ int mmu_batchnorm_fwd_sums(const void* X, const void* skip, void* Y, int64_t row
   q.skip_res = (const int8_t*)skip_res; q.y_res = (int8_t*)y_res;
   batchnorm_fwd_launch(q, (hipStream_t)stream);
   return check_launch("mmu_batchnorm_fwd_sums");
+}
+
+int mmu_batchnorm_fwd_parts(const void* X, const void* skip, void* Y, int64_t rows, int64_t C, const float* parts,
+                            int64_t nparts, const float* weight, const float* bias, float* running_mean,
+                            float* running_var, int64_t* num_batches_tracked, float momentum, float eps, int relu,
+                            float* save_mean, float* save_invstd, void* relu_mask, const void* skip_res, void* y_res,
+                            void* ws, int64_t ws_bytes, mmu_stream_t stream) {
+  if (!X || !Y || !parts || nparts <= 0) return fail("mmu_batchnorm_fwd_parts: null pointer / no partials");
+  if (relu_mask && !relu) return fail("mmu_batchnorm_fwd_parts: relu_mask needs relu");
+  if (bn_res_check(skip, relu, relu_mask, skip_res, y_res, "mmu_batchnorm_fwd_parts")) return 1;
+  if (bn_common(rows, C, ws, ws_bytes, "mmu_batchnorm_fwd_parts")) return 1;
+  if ((running_mean == nullptr) != (running_var == nullptr))
+    return fail("mmu_batchnorm_fwd_parts: running_mean / running_var must both be given or NULL");
+  if ((save_mean == nullptr) != (save_invstd == nullptr))
+    return fail("mmu_batchnorm_fwd_parts: save_mean / save_invstd must both be given or NULL");
+  if (rows < 2) return fail("mmu_batchnorm_fwd_parts: training needs more than 1 value per channel");
+  if (momentum < 0.f && !num_batches_tracked)
+    return fail("mmu_batchnorm_fwd_parts: momentum < 0 (cumulative average) needs num_batches_tracked");
+  BnFwdParams q{};
+  q.X = (const bf16*)X; q.skip = (const bf16*)skip; q.Y = (bf16*)Y; q.rows = rows; q.C = (int)C;
+  q.w = weight; q.b = bias; q.rmean = running_mean; q.rvar = running_var; q.nbt = num_batches_tracked;
+  q.training = 1; q.relu = relu; q.momentum = momentum; q.eps = eps;
+  q.smean = save_mean; q.sinvstd = save_invstd; q.ws = ws; q.mask = (uint8_t*)relu_mask;
+  q.skip_res = (const int8_t*)skip_res; q.y_res = (int8_t*)y_res;
+  q.parts = parts; q.nparts = nparts;
+  batchnorm_fwd_launch(q, (hipStream_t)stream);
+  return check_launch("mmu_batchnorm_fwd_parts");
 }
 
 int mmu_batchnorm_bwd_reduce(const void* dY, const void* Y, const void* relu_mask, const void* X, int64_t rows,

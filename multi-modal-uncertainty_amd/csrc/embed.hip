@@ -183,16 +183,20 @@ __global__ __launch_bounds__(256) void embed_bwd_rows_kernel(EmbedBwdParams q, E
     }
   }
   if (live) {  // this position's sum over the block's samples: position row, [CLS] / [SEP] word rows
+               // (through the wave's LDS slice: lane-contiguous 256-B atomic instructions)
     const int64_t posr = text ? s - q.n_img - 2 : s;
     float* wr = s == 0 ? q.d_word + q.cls_id * H : (s == q.n_img + 1 ? q.d_word + q.sep_id * H : nullptr);
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int i = 0; i < 3; ++i)
+      *(float4*)(&xch[wv][256 * i + 4 * l]) = make_float4(tot[i][0], tot[i][1], tot[i][2], tot[i][3]);
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int c = 256 * i + 4 * l + k;
-        atomicAdd(q.d_pos + posr * H + c, tot[i][k]);
-        if (wr) atomicAdd(wr + c, tot[i][k]);
-      }
+    for (int j = 0; j < 12; ++j) {
+      const float v = xch[wv][64 * j + l];
+      atomicAdd(q.d_pos + posr * H + 64 * j + l, v);
+      if (wr) atomicAdd(wr + 64 * j + l, v);
+    }
   }
 #pragma unroll
   for (int i = 0; i < 3; ++i)

@@ -198,7 +198,10 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
     if (bias) { b0 = *(const float4*)(bias + n); b1 = *(const float4*)(bias + n + 4); }
     bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w; bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
   }
-  const bool want_cs = p.colsum != nullptr && !slab;
+  // STORE_STATS: the BatchNorm statistics of the bf16 output, {sum, sum of squares} per column
+  // and 64-row block into the float2 table p.colsum [ceil(M / 64)][N] (one pass = 64 rows)
+  constexpr bool STATS = EPI == MMU_EPI_STORE_STATS;
+  const bool want_cs = !STATS && p.colsum != nullptr && !slab;
   float cs[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) cs[r] = 0.f;
@@ -233,8 +236,14 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
     lw[0] = w0.x; lw[1] = w0.y; lw[2] = w0.z; lw[3] = w0.w; lw[4] = w1.x; lw[5] = w1.y; lw[6] = w1.z; lw[7] = w1.w;
     lb[0] = b0.x; lb[1] = b0.y; lb[2] = b0.z; lb[3] = b0.w; lb[4] = b1.x; lb[5] = b1.y; lb[6] = b1.z; lb[7] = b1.w;
   }
+  static_assert(!STATS || PJ == 4, "STORE_STATS: one epilogue pass = one 64-row statistics block");
 #pragma unroll
   for (int pass = 0; pass < NJ / PJ; ++pass) {
+    float st1[8], st2[8];
+    if (STATS) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) st1[e] = st2[e] = 0.f;
+    }
     // the pass's residual / aux rows are requested up front: one memory latency per pass
     bf16x8 in[RES32 ? 1 : 2 * PJ];
     float4 in32[RES32 ? 2 * PJ : 1][2];
@@ -306,6 +315,30 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
       if (want_cs) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) cs[e] += v[e];
+      }
+      if (STATS) {  // over the values as stored (bf16), as the statistics pass would read them
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float y = bf2f(f2bf(v[e]));
+          st1[e] += y;
+          st2[e] = fmaf(y, y, st2[e]);
+        }
+      }
+    }
+    if (STATS) {  // lanes sharing q hold the same 8 columns: reduce over rr (8 rows each)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+#pragma unroll
+        for (int o = 8; o < 64; o <<= 1) {
+          st1[e] += __shfl_xor(st1[e], o, 64);
+          st2[e] += __shfl_xor(st2[e], o, 64);
+        }
+      }
+      const int64_t prow = (mw + 64 * pass) >> 6;
+      if (rr == 0 && mw + 64 * pass < p.M) {
+        float4* d = (float4*)(p.colsum + 2 * (prow * p.N + n));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) d[e] = make_float4(st1[2 * e], st2[2 * e], st1[2 * e + 1], st2[2 * e + 1]);
       }
     }
   }
@@ -444,6 +477,7 @@ static __device__ __forceinline__ void conva_g_load(uint4 (&r)[4], const bf16* _
   }
 }
 
+template <int EPI>
 __global__ __launch_bounds__(256) void gemm_conva_small_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * S_STAGE];
   const int t = threadIdx.x, l = t & 63, w = t >> 6, wm = w >> 1, wn = w & 1;
@@ -507,7 +541,7 @@ __global__ __launch_bounds__(256) void gemm_conva_small_kernel(GemmParams p) {
     }
     __syncthreads();
   }
-  epilogue_block<MMU_EPI_STORE, false, 4>(p, z, slice, m0 + 64 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
+  epilogue_block<EPI, false, 4>(p, z, slice, m0 + 64 * wm, n0 + 64 * wn, acc, l, smem + w * 16384);
 }
 
 // ================================================================ big: 256x256, LDS-DMA
@@ -705,8 +739,45 @@ __global__ __launch_bounds__(512) void gemm_convw_kernel(GemmParams p) {
 }
 
 // Y[pixel][n] = sum over (tap, c) of X[pixel shifted by tap][c] * Wk[n][tap * C + c] (bf16 out)
+template <int EPI>
 __global__ __launch_bounds__(512) void gemm_conva_kernel(GemmParams p) {
-  gemm_big_body<true, true, MMU_EPI_STORE, false, 2>(p);
+  gemm_big_body<true, true, EPI, false, 2>(p);
+}
+
+// {sum, sum of squares} per column and 64-row block of a bf16 [M][N] map into part (float2
+// [ceil(M / 64)][N]): the statistics table of MMU_EPI_STORE_STATS for a product whose epilogue
+// could not produce it (a split-K conv: its output is formed by splitk_reduce_bf16_kernel)
+__global__ __launch_bounds__(256) void stats64_kernel(const bf16* __restrict__ Y, int64_t M, int64_t N,
+                                                      float* __restrict__ part) {
+  __shared__ float red[2][8][256];
+  const int t = threadIdx.x, oc = t & 31, rs = t >> 5;
+  const int64_t n = (int64_t)blockIdx.y * 256 + 8 * oc, r0 = (int64_t)blockIdx.x * 64;
+  float a[8], b[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = b[e] = 0.f;
+  if (n < N) {
+    for (int r = rs; r < 64 && r0 + r < M; r += 8) {
+      const bf16x8 v = *(const bf16x8*)(Y + (r0 + r) * N + n);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float y = bf2f(v[e]);
+        a[e] += y;
+        b[e] = fmaf(y, y, b[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][e][t] = a[e]; red[1][e][t] = b[e]; }
+  __syncthreads();
+  if (rs == 0 && n < N) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float sa = 0.f, sb = 0.f;
+      for (int k = 0; k < 8; ++k) { sa += red[0][e][32 * k + oc]; sb += red[1][e][32 * k + oc]; }
+      part[2 * ((int64_t)blockIdx.x * N + n + e)] = sa;
+      part[2 * ((int64_t)blockIdx.x * N + n + e) + 1] = sb;
+    }
+  }
 }
 
 // sum of the split-K slabs of one (M x N) product into a bf16 C (slice order: deterministic)
@@ -727,12 +798,24 @@ __global__ __launch_bounds__(256) void splitk_reduce_bf16_kernel(const float* __
 }
 
 void conv3x3_implicit_launch(const GemmParams& p, bool small, hipStream_t s) {
-  if (small) hipLaunchKernelGGL(gemm_conva_small_kernel, dim3(p.tiles_m * p.tiles_n, p.splitk, 1), dim3(256), 0, s, p);
-  else hipLaunchKernelGGL(gemm_conva_kernel, dim3(p.tiles_m * p.tiles_n, p.splitk, 1), dim3(512), 0, s, p);
+  // p.kind == MMU_EPI_STORE_STATS: the epilogue also writes the output's BatchNorm statistics
+  // table (p.colsum); split-K forms the output in the reduce kernel, so a stats pass follows it
+  const bool stats = p.kind == MMU_EPI_STORE_STATS && p.splitk == 1;
+  const dim3 grid(p.tiles_m * p.tiles_n, p.splitk, 1);
+  if (small) {
+    if (stats) hipLaunchKernelGGL(gemm_conva_small_kernel<MMU_EPI_STORE_STATS>, grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(gemm_conva_small_kernel<MMU_EPI_STORE>, grid, dim3(256), 0, s, p);
+  } else {
+    if (stats) hipLaunchKernelGGL(gemm_conva_kernel<MMU_EPI_STORE_STATS>, grid, dim3(512), 0, s, p);
+    else hipLaunchKernelGGL(gemm_conva_kernel<MMU_EPI_STORE>, grid, dim3(512), 0, s, p);
+  }
   if (p.splitk > 1) {
     const int64_t q = p.M * p.N / 8;
     hipLaunchKernelGGL(splitk_reduce_bf16_kernel, dim3((unsigned)((q + 255) / 256)), dim3(256), 0, s, p.ws,
                        (bf16*)p.C, p.M, p.N, p.ldc, p.splitk);
+    if (p.kind == MMU_EPI_STORE_STATS)
+      hipLaunchKernelGGL(stats64_kernel, dim3((unsigned)((p.M + 63) / 64), (unsigned)((p.N + 255) / 256)), dim3(256),
+                         0, s, (const bf16*)p.C, p.M, p.N, p.colsum);
   }
 }
 
@@ -774,6 +857,10 @@ void gemm_launch(const GemmParams& p, bool ak, bool bk, bool f32out, bool big, i
     case MMU_EPI_DGELU: launch_e<MMU_EPI_DGELU, false>(p, ak, bk, big, batch, s); break;
     case MMU_EPI_ADD_RES: launch_e<MMU_EPI_ADD_RES, false>(p, ak, bk, big, batch, s); break;
     case MMU_EPI_BIAS_DROP_QGELU: launch_e<MMU_EPI_BIAS_DROP_QGELU, false>(p, ak, bk, big, batch, s); break;
+    case MMU_EPI_STORE_STATS:  // (the 1x1 conv forward: X rows . W^T, both K-major)
+      if (big) launch_t<true, true, MMU_EPI_STORE_STATS, false>(p, true, batch, s);
+      else launch_t<true, true, MMU_EPI_STORE_STATS, false>(p, false, batch, s);
+      break;
   }
 }
 

@@ -183,6 +183,8 @@ struct BnFwdParams {
   int8_t* y_res;           // write Y's 8-bit residue (the block output / the downsample's output)
   double* lsum;        // cross-rank statistics: write the local sums {s1[C], s2[C], rows} and stop
   const double* gsum;  // cross-rank statistics: finalize + apply from the exchanged sums
+  const float* parts;  // the producing conv's statistics table (float2 [nparts][C]): no stats pass
+  int64_t nparts;
 };
 void batchnorm_fwd_launch(const BnFwdParams& q, hipStream_t s);
 struct BnBwdParams {

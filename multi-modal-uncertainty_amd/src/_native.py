@@ -15,7 +15,7 @@ c_i64, c_i32, c_f32, c_u64, c_vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_floa
 c_f32p, c_i64p, c_dp = ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)
 
 MMU_BF16, MMU_F32 = 0, 1
-EPI_STORE, EPI_BIAS_GELU, EPI_BIAS_DROP_RES, EPI_DGELU, EPI_ADD_RES, EPI_BIAS_DROP_QGELU = range(6)
+EPI_STORE, EPI_BIAS_GELU, EPI_BIAS_DROP_RES, EPI_DGELU, EPI_ADD_RES, EPI_BIAS_DROP_QGELU, EPI_STORE_STATS = range(7)
 
 
 class Epilogue(ctypes.Structure):
@@ -69,6 +69,8 @@ SIGNATURES = {
     "mmu_conv3x3_wgrad": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp]),
     "mmu_conv_implicit": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64,
                                   c_vp]),
+    "mmu_conv_implicit_stats": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp,
+                                        c_i64, c_vp]),
     "mmu_conv_wgrad": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64,
                                c_vp]),
     "mmu_stem_conv_fwd": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
@@ -82,6 +84,8 @@ SIGNATURES = {
     "mmu_batchnorm_stats": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "mmu_batchnorm_fwd_sums": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32,
                                        c_f32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "mmu_batchnorm_fwd_parts": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                        c_f32, c_f32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "mmu_batchnorm_bwd_reduce": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp,
                                          c_vp, c_i64, c_vp]),
     "mmu_batchnorm_bwd_sums": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp,

@@ -10,7 +10,14 @@ import torch
 
 from . import _native as N
 from ._native import (Epilogue, EPI_STORE, EPI_BIAS_GELU, EPI_BIAS_DROP_RES, EPI_DGELU, EPI_ADD_RES,  # noqa: F401
-                      EPI_BIAS_DROP_QGELU)
+                      EPI_BIAS_DROP_QGELU, EPI_STORE_STATS)
+
+
+def bn_stats_table(rows, C, device):
+    """the float2 [ceil(rows / 64)][C] BatchNorm statistics table a conv's STORE_STATS epilogue
+    writes (include/mmu.h MMU_EPI_STORE_STATS) -> (table, nparts)"""
+    nparts = (rows + 63) // 64
+    return torch.empty(nparts * C * 2, dtype=torch.float32, device=device), nparts
 
 
 def _dev_check(*ts):
@@ -389,11 +396,12 @@ def _conv_out(h, w, ksize, stride):
     return (h + 2 * pad - ksize) // stride + 1, (w + 2 * pad - ksize) // stride + 1
 
 
-def conv_implicit(X, Wk, Y, ksize=3, stride=1):
+def conv_implicit(X, Wk, Y, ksize=3, stride=1, stats=None):
     """Y[p, n] = sum_{tap, c} X[input pixel of (p, tap), c] Wk[n, tap * C + c]: a ksize x ksize
     (3: pad 1, 1: pad 0) / stride conv as one implicit-im2col GEMM.  X [N, C, H, W] and Y
     [N, Nout, Ho, Wo] channels-last bf16, Wk bf16 with memory [Nout][ksize][ksize][C] (a
-    channels-last [Nout, C, k, k] filter, or the flipped-transposed 3x3 one for dX)."""
+    channels-last [Nout, C, k, k] filter, or the flipped-transposed 3x3 one for dX).
+    stats (optional, bn_stats_table of Y's rows): Y's BatchNorm statistics, written too."""
     _dev_check(X, Wk, Y)
     _want(X, torch.bfloat16, "conv_implicit X")
     _want(Wk, torch.bfloat16, "conv_implicit Wk")
@@ -412,6 +420,12 @@ def conv_implicit(X, Wk, Y, ksize=3, stride=1):
         raise N.NativeError(f"conv_implicit: X channels-last bf16 [N, C, H, W], Y [N, Nout, {ho}, {wo}], "
                             f"Wk [Nout][{k}][{k}][C] bf16")
     ws = _splitk_workspace(Y.device)  # split-K slabs for small maps (few tiles)
+    if stats is not None:
+        if stats.dtype != torch.float32 or stats.numel() < ((n * ho * wo + 63) // 64) * nout * 2:
+            raise N.NativeError("conv_implicit: stats table too small (kernels.bn_stats_table)")
+        N.call("mmu_conv_implicit_stats", _ptr(X), _ptr(Wk), _ptr(Y), n, h, w, c, nout, ksize, stride, _ptr(stats),
+               _ptr(ws), ws.numel(), _stream(X))
+        return
     N.call("mmu_conv_implicit", _ptr(X), _ptr(Wk), _ptr(Y), n, h, w, c, nout, ksize, stride, _ptr(ws), ws.numel(),
            _stream(X))
 
@@ -536,11 +550,12 @@ def _bn_res_check(name, X, *ts):
 
 def batchnorm_fwd(X, Y, weight, bias, running_mean, running_var, training, momentum, eps, relu=False, skip=None,
                   num_batches_tracked=None, save_mean=None, save_invstd=None, relu_mask=None, skip_res=None,
-                  y_res=None):
+                  y_res=None, parts=None):
     """X, Y, skip: channels-last bf16 [N, C, H, W] (contiguous as [N*H*W, C]).  relu_mask
     (optional, relu only): uint8 [N*H*W*C/8] written with the bits Y > 0 for batchnorm_bwd.
     y_res / skip_res (optional, int8 of X's size): the residual stream's 8-bit residue of Y /
-    of skip (include/mmu.h)."""
+    of skip (include/mmu.h).  parts (training only): (table, nparts) of X's statistics from the
+    conv that produced X (bn_stats_table): no statistics pass (mmu_batchnorm_fwd_parts)."""
     _dev_check(X, Y)
     _want(X, torch.bfloat16, "batchnorm X")
     _bn_mask_check(relu_mask, X, "batchnorm_fwd")
@@ -552,6 +567,15 @@ def batchnorm_fwd(X, Y, weight, bias, running_mean, running_var, training, momen
         raise N.NativeError("batchnorm_fwd: num_batches_tracked must be int64")
     rows = X.numel() // C
     ws = _bn_workspace(X.device)
+    if parts is not None:
+        table, nparts = parts
+        if not training or table.numel() < nparts * C * 2 or nparts != (rows + 63) // 64:
+            raise N.NativeError("batchnorm_fwd: parts must be X's training statistics table (bn_stats_table)")
+        N.call("mmu_batchnorm_fwd_parts", _ptr(X), _ptr(skip), _ptr(Y), rows, C, _ptr(table), nparts, _ptr(weight),
+               _ptr(bias), _ptr(running_mean), _ptr(running_var), _ptr(num_batches_tracked), float(momentum),
+               float(eps), int(bool(relu)), _ptr(save_mean), _ptr(save_invstd), _ptr(relu_mask), _ptr(skip_res),
+               _ptr(y_res), _ptr(ws), ws.numel() * 4, _stream(X))
+        return
     N.call("mmu_batchnorm_fwd", _ptr(X), _ptr(skip), _ptr(Y), rows, C, _ptr(weight), _ptr(bias), _ptr(running_mean),
            _ptr(running_var), _ptr(num_batches_tracked), int(bool(training)), float(momentum), float(eps),
            int(bool(relu)), _ptr(save_mean), _ptr(save_invstd), _ptr(relu_mask), _ptr(skip_res), _ptr(y_res),

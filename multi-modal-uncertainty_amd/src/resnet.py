@@ -27,6 +27,18 @@ _TORCH_ONLY = [False]
 # is held to ~2^-15 of its value instead of bf16's 2^-8.  The convs read the bf16 map.
 # MMU_STREAM_RESIDUE=0 turns it off process-wide (the parity A/B of profiles/r6_residue_parity_ab.txt).
 STREAM_RESIDUE = os.environ.get("MMU_STREAM_RESIDUE", "1") != "0"
+# A training conv on the gathered / mmu_gemm products writes its output's BatchNorm statistics in
+# its own epilogue (MMU_EPI_STORE_STATS), so the BatchNorm after it skips its statistics pass
+# (round 6; MMU_BN_STATS_FUSION=0: the BatchNorms compute them, for A/Bs)
+BN_STATS_FUSION = os.environ.get("MMU_BN_STATS_FUSION", "1") != "0"
+
+
+class _BnStats:
+    """filled by a conv Function's forward with (table, nparts) of its output's statistics"""
+    __slots__ = ("parts",)
+
+    def __init__(self):
+        self.parts = None
 
 
 class torch_ops_only:
@@ -48,7 +60,7 @@ class _BatchNormAct(torch.autograd.Function):
     mmu_batchnorm_fwd / mmu_batchnorm_bwd (batch statistics, running stats updated)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, skip, bn, relu, sink=None, skip_res=None, y_res=None):
+    def forward(ctx, x, weight, bias, skip, bn, relu, sink=None, skip_res=None, y_res=None, parts=None):
         ctx.bias_ref, ctx.sink = bias, sink
         Y = torch.empty_like(x)
         C = x.shape[1]
@@ -58,7 +70,7 @@ class _BatchNormAct(torch.autograd.Function):
         mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device) if relu else None
         K.batchnorm_fwd(x, Y, weight, bias, bn.running_mean, bn.running_var, True, _momentum_arg(bn), bn.eps,
                         relu=relu, skip=skip, num_batches_tracked=bn.num_batches_tracked, save_mean=smean,
-                        save_invstd=sinv, relu_mask=mask, skip_res=skip_res, y_res=y_res)
+                        save_invstd=sinv, relu_mask=mask, skip_res=skip_res, y_res=y_res, parts=parts)
         ctx.save_for_backward(x, mask, weight, smean, sinv)
         ctx.relu, ctx.has_skip = relu, skip is not None
         return Y
@@ -81,7 +93,7 @@ class _BatchNormAct(torch.autograd.Function):
         rb = db if (want_b and ctx.bias_ref.grad is None) else None
         if ctx.sink is not None and dS is not None:  # conv1's dX GEMM adds it (EPI_ADD_RES)
             ctx.sink.g, dS = dS, None
-        return dX, rw, rb, dS, None, None, None, None, None
+        return dX, rw, rb, dS, None, None, None, None, None, None
 
 
 def _momentum(bn):
@@ -233,8 +245,10 @@ class BatchNorm2d(nn.BatchNorm2d):
             return _with_res(y, y_res)
         if hip:
             if self.training and self.track_running_stats:
+                # the statistics the producing conv's epilogue wrote (BN_STATS_FUSION), if any
+                parts = x.__dict__.pop("_mmu_bnparts", None)
                 return _with_res(_BatchNormAct.apply(x, self.weight, self.bias, skip, self, relu, skip_sink, skip_res,
-                                                     y_res), y_res)
+                                                     y_res, parts), y_res)
             if not self.training and not (torch.is_grad_enabled() and (
                     x.requires_grad or self.weight.requires_grad or (skip is not None and skip.requires_grad))):
                 # the one-pass running-statistics kernel has no backward: a graph through an
@@ -307,7 +321,7 @@ class _ConvBF16(torch.autograd.Function):
     plus an AccumulateGrad add)."""
 
     @staticmethod
-    def forward(ctx, x, w, w16, stride, padding, flipped=None):
+    def forward(ctx, x, w, w16, stride, padding, flipped=None, stats=None):
         ctx.save_for_backward(x, w16)
         ctx.w, ctx.conf, ctx.flipped = w, (stride, padding), flipped
         cout = w16.shape[0]
@@ -324,7 +338,11 @@ class _ConvBF16(torch.autograd.Function):
             n, _, h, wd = x.shape
             ho, wo = (h + 2 * (ks // 2) - ks) // st + 1, (wd + 2 * (ks // 2) - ks) // st + 1
             y = torch.empty((n, cout, ho, wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
-            K.conv_implicit(x, w16, y, ks, st)
+            if stats is not None:  # + the BatchNorm statistics of y, from the epilogue
+                stats.parts = K.bn_stats_table(n * ho * wo, cout, x.device)
+                K.conv_implicit(x, w16, y, ks, st, stats=stats.parts[0])
+            else:
+                K.conv_implicit(x, w16, y, ks, st)
             return y
         return torch.ops.aten.convolution(x, w16, None, stride, padding, (1, 1), False, (0, 0), 1)
 
@@ -357,7 +375,7 @@ class _ConvBF16(torch.autograd.Function):
             dx, gw, _ = torch.ops.aten.convolution_backward(dy, x, w16, None, stride, padding, (1, 1), False, (0, 0),
                                                             1, (True, True, False))
             g.add_(gw)
-            return dx, None, None, None, None, None
+            return dx, None, None, None, None, None, None
         if need_x and not mmu_x:
             dx = torch.ops.aten.convolution_backward(dy, x, w16, None, stride, padding, (1, 1), False, (0, 0), 1,
                                                      (True, False, False))[0]
@@ -385,7 +403,7 @@ class _ConvBF16(torch.autograd.Function):
             if g is not None:
                 g.add_(rw)
                 rw = None
-        return dx, rw, None, None, None, None
+        return dx, rw, None, None, None, None, None
 
 
 class _SkipGrad:
@@ -472,15 +490,19 @@ class _Conv1x1(torch.autograd.Function):
     The GEMMs are excluded from bench.py's BERT-layer GEMM timing (timing_paused)."""
 
     @staticmethod
-    def forward(ctx, x, w, w16, sink):
+    def forward(ctx, x, w, w16, sink, stats=None):
         Nb, C, H, W = x.shape
         Co = w16.shape[0]
         M = Nb * H * W
         use_f, use_d, use_w = _mmu_1x1(C, Co, M, H)
         if use_f:
             y = torch.empty((Nb, Co, H, W), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+            epi = None
+            if stats is not None:  # + the BatchNorm statistics of y, from the epilogue
+                stats.parts = K.bn_stats_table(M, Co, x.device)
+                epi = K.epilogue(K.EPI_STORE_STATS, colsum=stats.parts[0])
             with K.timing_paused():
-                K.gemm(_rows(x), C, 1, w16.view(Co, C), C, 1, _rows(y), Co, M, Co, C)
+                K.gemm(_rows(x), C, 1, w16.view(Co, C), C, 1, _rows(y), Co, M, Co, C, epi=epi)
         else:
             y = torch.ops.aten.convolution(x, w16, None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1)
         ctx.save_for_backward(x, w16)
@@ -513,7 +535,7 @@ class _Conv1x1(torch.autograd.Function):
                 dx = gx if skip is None else gx + skip
                 if both:  # (one MIOpen call for both products when neither goes elsewhere)
                     ctx.w.grad.add_(gw)
-                    return dx, None, None, None
+                    return dx, None, None, None, None
             if need_w:
                 g = ctx.w.grad
                 if g is None:
@@ -531,7 +553,7 @@ class _Conv1x1(torch.autograd.Function):
                     _wgrad_run(dw, dy, x)
                 else:
                     dw()
-        return dx, rw, None, None
+        return dx, rw, None, None, None
 
 
 class StoreConv2d(nn.Conv2d):
@@ -582,9 +604,16 @@ class StoreConv2d(nn.Conv2d):
         w16 = self._compute_weight(x)
         if w16 is not None:
             x = x.contiguous(memory_format=torch.channels_last)
+            # a training forward (the BatchNorm after this conv uses batch statistics): the conv's
+            # epilogue writes them when it runs on the mmu products (BN_STATS_FUSION)
+            st = _BnStats() if BN_STATS_FUSION and self.training and torch.is_grad_enabled() else None
             if self._is_1x1():
-                return _Conv1x1.apply(x, self.weight, w16, sink)
-            return _ConvBF16.apply(x, self.weight, w16, self.stride, self.padding, self._flipped_getter())
+                y = _Conv1x1.apply(x, self.weight, w16, sink, st)
+            else:
+                y = _ConvBF16.apply(x, self.weight, w16, self.stride, self.padding, self._flipped_getter(), st)
+            if st is not None and st.parts is not None:
+                y._mmu_bnparts = st.parts
+            return y
         if sink is not None:
             raise RuntimeError("StoreConv2d: a skip-gradient sink needs the bf16 1x1 path")
         return super().forward(x)

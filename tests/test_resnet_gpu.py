@@ -346,3 +346,60 @@ def test_batchnorm_momentum_none_cumulative_average_on_device(dev):
     assert int(hip.num_batches_tracked) == 3 == int(ref.num_batches_tracked)
     torch.testing.assert_close(hip.running_mean, ref.running_mean, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(hip.running_var, ref.running_var, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("n,cin,cout,h,ks,st", [(256, 256, 256, 14, 3, 1), (4, 256, 256, 14, 3, 1),
+                                               (6, 128, 128, 28, 3, 1), (8, 512, 512, 13, 3, 2),
+                                               (16, 1024, 2048, 14, 1, 2)])
+def test_conv_stats_epilogue_matches_output(dev, n, cin, cout, h, ks, st):
+    """mmu_conv_implicit_stats (MMU_EPI_STORE_STATS, round 6): the BatchNorm statistics table the
+    conv's epilogue writes -- {sum, sum of squares} per channel and 64-row block of the bf16
+    output -- against the output itself; the big-tile, small-tile (128 channels) and split-K
+    (few tiles: a stats pass after the reduction) paths."""
+    from src import kernels as K
+    torch.manual_seed(n + cin)
+    cl = torch.channels_last
+    x = torch.randn(n, cin, h, h, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (torch.randn(cout, cin, ks, ks, device=dev) * (cin * ks * ks) ** -0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=cl)
+    ho = (h + 2 * (ks // 2) - ks) // st + 1
+    y = torch.empty(n, cout, ho, ho, dtype=torch.bfloat16, device=dev, memory_format=cl)
+    M = n * ho * ho
+    table, nparts = K.bn_stats_table(M, cout, dev)
+    K.conv_implicit(x, w, y, ks, st, stats=table)
+    yr = y.permute(0, 2, 3, 1).reshape(M, cout).float()
+    t = table.view(nparts, cout, 2)
+    blocks = torch.nn.functional.pad(yr, (0, 0, 0, nparts * 64 - M)).view(nparts, 64, cout)
+    torch.testing.assert_close(t[..., 0], blocks.sum(1), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(t[..., 1], (blocks * blocks).sum(1), rtol=1e-4, atol=1e-3)
+
+
+def test_gemm_stats_epilogue_and_bn_parts(dev):
+    """the 1x1 conv forward's STORE_STATS GEMM, then mmu_batchnorm_fwd_parts on its table: the same
+    BatchNorm output / saved statistics / running statistics as mmu_batchnorm_fwd's own pass."""
+    from src import kernels as K
+    torch.manual_seed(3)
+    M, C, Co = 25088, 1024, 256
+    x = torch.randn(M, C, device=dev).to(torch.bfloat16)
+    w = (torch.randn(Co, C, device=dev) * C ** -0.5).to(torch.bfloat16)
+    y = torch.empty(M, Co, dtype=torch.bfloat16, device=dev)
+    table, nparts = K.bn_stats_table(M, Co, dev)
+    K.gemm(x, C, 1, w, C, 1, y, Co, M, Co, C, epi=K.epilogue(K.EPI_STORE_STATS, colsum=table))
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), rtol=2e-2, atol=2e-2)
+    t = table.view(nparts, Co, 2).sum(0)
+    torch.testing.assert_close(t[:, 0], y.float().sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(t[:, 1], (y.float() ** 2).sum(0), rtol=1e-4, atol=1e-2)
+    Y4 = y.view(32, 28, 28, Co).permute(0, 3, 1, 2)  # channels-last [N, C, H, W] view of the rows
+    outs = []
+    for parts in (None, (table, nparts)):
+        Yo = torch.empty_like(Y4)
+        wgt, bias = 1 + 0.1 * torch.randn(Co, device=dev), 0.1 * torch.randn(Co, device=dev)
+        torch.manual_seed(5)
+        wgt, bias = 1 + 0.1 * torch.randn(Co, device=dev), 0.1 * torch.randn(Co, device=dev)
+        rm, rv = torch.zeros(Co, device=dev), torch.ones(Co, device=dev)
+        sm, si = torch.empty(Co, device=dev), torch.empty(Co, device=dev)
+        K.batchnorm_fwd(Y4, Yo, wgt, bias, rm, rv, True, 0.1, 1e-5, relu=True, save_mean=sm, save_invstd=si,
+                        parts=parts)
+        outs.append((Yo.float(), rm, rv, sm, si))
+    for a, b in zip(outs[0], outs[1]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-2 if a.dim() == 4 else 1e-6)
