@@ -349,7 +349,7 @@ def test_batchnorm_momentum_none_cumulative_average_on_device(dev):
 
 
 @pytest.mark.parametrize("n,cin,cout,h,ks,st", [(256, 256, 256, 14, 3, 1), (4, 256, 256, 14, 3, 1),
-                                               (6, 128, 128, 28, 3, 1), (8, 512, 512, 13, 3, 2),
+                                               (24, 128, 128, 28, 3, 1), (8, 512, 512, 13, 3, 2),
                                                (16, 1024, 2048, 14, 1, 2)])
 def test_conv_stats_epilogue_matches_output(dev, n, cin, cout, h, ks, st):
     """mmu_conv_implicit_stats (MMU_EPI_STORE_STATS, round 6): the BatchNorm statistics table the
@@ -393,7 +393,6 @@ def test_gemm_stats_epilogue_and_bn_parts(dev):
     outs = []
     for parts in (None, (table, nparts)):
         Yo = torch.empty_like(Y4)
-        wgt, bias = 1 + 0.1 * torch.randn(Co, device=dev), 0.1 * torch.randn(Co, device=dev)
         torch.manual_seed(5)
         wgt, bias = 1 + 0.1 * torch.randn(Co, device=dev), 0.1 * torch.randn(Co, device=dev)
         rm, rv = torch.zeros(Co, device=dev), torch.ones(Co, device=dev)
