@@ -33,8 +33,10 @@ enum { MMU_BF16 = 0, MMU_F32 = 1 };
 /* ABI version: bumped whenever an entry's argument list or buffer contract changes.  2 (round 5):
  * the residual stream's residue pointers inside mmu_batchnorm_fwd / _fwd_sums and the grad_scale
  * argument of mmu_bertadam_step.  3 (round 6): mmu_embed_bwd's workspace size is
- * mmu_embed_bwd_ws_floats().  Callers compare mmu_version() with the header they were built against. */
-#define MMU_ABI_VERSION 3
+ * mmu_embed_bwd_ws_floats().  4 (round 6): mmu_epilogue grows bn_x / bn_mask / bn_mean (the
+ * BatchNorm-backward epilogues STORE_BNB / ADD_RES_BNB).  Callers compare mmu_version() with the
+ * header they were built against. */
+#define MMU_ABI_VERSION 4
 int mmu_version(void);
 const char* mmu_last_error(void);
 
@@ -68,11 +70,22 @@ enum {
   MMU_EPI_BIAS_DROP_QGELU = 5,/* u = dropout(acc+bias); C = u*sigmoid(1.702u); aux (optional)
                                = keep/(1-p) * d(u*sigmoid(1.702u))/du: FLAVA ResidualAttentionBlock
                                mlp c_fc -> Dropout -> QuickGELU (src/model.py:183-185,196-198) */
-  MMU_EPI_STORE_STATS = 6     /* C = acc (+bias) in bf16, and `colsum` = a float2 table
+  MMU_EPI_STORE_STATS = 6,    /* C = acc (+bias) in bf16, and `colsum` = a float2 table
                                [ceil(M/64)][N] of {sum, sum of squares} of the stored C per column
                                and 64-row block: the training BatchNorm statistics of a conv
                                output, produced by the conv's own epilogue (round 6;
                                mmu_batchnorm_fwd_parts consumes it).  batch 1, no split-K. */
+  MMU_EPI_STORE_BNB = 7,
+  MMU_EPI_ADD_RES_BNB = 8,  /* STORE / ADD_RES into a bf16 C that is the output gradient dY of a
+                               training BatchNorm (+ReLU) whose input was bn_x [M, N] bf16 (ReLU
+                               mask bn_mask [M, N/8] u8 as mmu_batchnorm_fwd wrote it, or NULL =
+                               no ReLU; batch mean bn_mean [N] f32), and `colsum` = a float2 table
+                               [ceil(M/64)][N] of {sum g, sum g (bn_x - mean)} per column and
+                               64-row block, g = the stored C * mask: the reduction of that
+                               BatchNorm's backward, produced by the epilogue of the product that
+                               forms its dY (the next conv's data gradient; round 6,
+                               mmu_batchnorm_bwd_parts consumes it).  batch 1, ldc == N, A K-major
+                               and B N-major (the 1x1 conv dX = dY_next . W).                  */
 };
 typedef struct mmu_epilogue {
   int32_t kind;
@@ -103,6 +116,9 @@ typedef struct mmu_epilogue {
   const float* res_ln_b;
   int64_t res_ln_bstride;   /* batched products: w / b of batch item z at + z * res_ln_bstride
                                (mean / rstd at + z * M)                                  */
+  const void* bn_x;         /* STORE_BNB / ADD_RES_BNB only (ABI 4): see those kinds      */
+  const uint8_t* bn_mask;
+  const float* bn_mean;
 } mmu_epilogue;
 
 int mmu_gemm(const void* A, int64_t lda, int a_kmajor,
@@ -317,6 +333,14 @@ int mmu_conv_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int
 int mmu_conv_implicit_stats(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
                             int64_t N, int64_t ksize, int64_t stride, float* stats, float* ws, int64_t ws_floats,
                             mmu_stream_t stream);
+/* mmu_conv3x3_implicit whose output is the data gradient dX of a 3x3 conv that a training
+ * BatchNorm (+ReLU) fed: also writes that BatchNorm's backward reduction table (stats = float2
+ * [ceil(Npix / 64)][N] {sum g, sum g (bn_x - bn_mean)}, g = dX * bn_mask; see
+ * MMU_EPI_STORE_BNB).  bn_x [Npix, N] bf16, bn_mask [Npix, N/8] u8 or NULL, bn_mean [N] f32.
+ * With split-K the table comes from a pass over dX after its reduction. */
+int mmu_conv3x3_implicit_bnb(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
+                             int64_t N, const void* bn_x, const uint8_t* bn_mask, const float* bn_mean,
+                             float* stats, float* ws, int64_t ws_floats, mmu_stream_t stream);
 int mmu_conv_wgrad(const void* dY, const void* X, float* dW, int64_t n_img, int64_t H, int64_t W, int64_t Cin,
                    int64_t Cout, int64_t ksize, int64_t stride, int accumulate, float* ws, int64_t ws_floats,
                    mmu_stream_t stream);
@@ -381,6 +405,15 @@ int mmu_batchnorm_bwd(const void* dY, const void* Y, const void* relu_mask, cons
                       int64_t C, const float* weight, const float* save_mean, const float* save_invstd, int relu,
                       void* dX, void* dSkip, float* dweight, float* dbias, void* ws, int64_t ws_bytes,
                       mmu_stream_t stream);
+
+/* Training-mode backward whose reduction {sum g, sum g (x - mean)} was produced by the product
+ * that formed dY (MMU_EPI_STORE_BNB / ADD_RES_BNB, mmu_conv3x3_implicit_bnb: parts = float2
+ * [nparts][C] block partials): no reduction pass; finalize (dweight / dbias +=) and apply as
+ * mmu_batchnorm_bwd. */
+int mmu_batchnorm_bwd_parts(const void* dY, const void* Y, const void* relu_mask, const void* X, int64_t rows,
+                            int64_t C, const float* parts, int64_t nparts, const float* weight,
+                            const float* save_mean, const float* save_invstd, int relu, void* dX, void* dSkip,
+                            float* dweight, float* dbias, void* ws, int64_t ws_bytes, mmu_stream_t stream);
 
 /* Cross-rank (synchronised) BatchNorm: data-parallel training that keeps the reference's
  * whole-batch statistics (src/mmbt.py:19-21 normalises the trunk over the full batch of one

@@ -450,15 +450,16 @@ void batchnorm_fwd_launch(const BnFwdParams& q, hipStream_t s) {
 
 void batchnorm_bwd_launch(const BnBwdParams& q, hipStream_t s) {
   const BnGrid G = bn_grid(q.rows, q.C);
-  const int nparts = (int)G.grid.x;
   float* coef = (float*)q.ws;
-  float2* part = (float2*)(coef + ((3 * q.C + 3) & ~3));
+  // the reduction: the table of the product that formed dY (q.parts), or this launch's own pass
+  const float2* part = q.parts ? (const float2*)q.parts : (const float2*)(coef + ((3 * q.C + 3) & ~3));
+  const int nparts = q.parts ? (int)q.nparts : (int)G.grid.x;
   const bool mk = q.relu && q.mask != nullptr;
   const dim3 fin((q.C + BN_FIN_CH - 1) / BN_FIN_CH);
-  if (!q.gsum) {
+  if (!q.gsum && !q.parts) {
 #define BN_BREDUCE(RL, MK)                                                                                   \
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<RL, MK>), G.grid, dim3(BN_THREADS), 0, s, q.dY, q.Y, q.mask, q.X, \
-                     q.rows, q.C, G.CH, G.rpb, q.smean, part)
+                     q.rows, q.C, G.CH, G.rpb, q.smean, (float2*)part)
     if (mk) BN_BREDUCE(true, true);
     else if (q.relu) BN_BREDUCE(true, false);
     else BN_BREDUCE(false, false);

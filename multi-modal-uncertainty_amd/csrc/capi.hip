@@ -140,9 +140,15 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
     p.drop_p = epi->drop_p; p.seed = epi->seed; p.seed_off = g_seed_off;
     p.res_ln_mean = epi->res_ln_mean; p.res_ln_rstd = epi->res_ln_rstd;
     p.res_ln_w = epi->res_ln_w; p.res_ln_b = epi->res_ln_b; p.res_ln_bstride = epi->res_ln_bstride;
+    p.bn_x = (const bf16*)epi->bn_x; p.bn_mask = epi->bn_mask; p.bn_mean = epi->bn_mean;
   }
   p.kind = kind;
-  if (kind < 0 || kind > MMU_EPI_STORE_STATS) return fail("mmu_gemm: bad epilogue kind %d", kind);
+  if (kind < 0 || kind > MMU_EPI_ADD_RES_BNB) return fail("mmu_gemm: bad epilogue kind %d", kind);
+  if ((kind == MMU_EPI_STORE_BNB || kind == MMU_EPI_ADD_RES_BNB) &&
+      (!p.colsum || !p.bn_x || !p.bn_mean || batch != 1 || !a_kmajor || b_kmajor || p.accumulate || p.bias ||
+       ldc != N || c_dtype != MMU_BF16))
+    return fail("mmu_gemm: *_BNB needs the table (colsum), bn_x, bn_mean, batch 1, K-major A, N-major B, "
+                "bf16 C with ldc == N, no bias / accumulate");
   if (kind == MMU_EPI_STORE_STATS && (!p.colsum || batch != 1 || !a_kmajor || !b_kmajor || p.accumulate))
     return fail("mmu_gemm: STORE_STATS needs the stats table (colsum), batch 1, K-major A and B, no accumulate");
   if (kind != MMU_EPI_STORE && kind != MMU_EPI_BIAS_DROP_RES && c_dtype != MMU_BF16)
@@ -155,7 +161,7 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
       return fail("mmu_gemm: res_ln_* (all four) only with BIAS_DROP_RES into an f32 C");
   }
   if (kind == MMU_EPI_DGELU && !p.aux) return fail("mmu_gemm: DGELU epilogue needs aux");
-  if ((kind == MMU_EPI_BIAS_DROP_RES || kind == MMU_EPI_ADD_RES) && !p.residual)
+  if ((kind == MMU_EPI_BIAS_DROP_RES || kind == MMU_EPI_ADD_RES || kind == MMU_EPI_ADD_RES_BNB) && !p.residual)
     return fail("mmu_gemm: epilogue needs residual");
   if (p.accumulate && c_dtype != MMU_F32) return fail("mmu_gemm: accumulate needs f32 C");
   if (p.drop_p < 0.f || p.drop_p >= 1.f) return fail("mmu_gemm: drop_p out of range");
@@ -556,7 +562,8 @@ int mmu_stem_conv_wgrad(const void* dY, const void* X, float* dW, int64_t n_img,
 
 static int conv_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
                          int64_t N, int64_t ksize, int64_t stride, float* stats, float* ws, int64_t ws_floats,
-                         mmu_stream_t stream) {
+                         mmu_stream_t stream, const void* bn_x = nullptr, const uint8_t* bn_mask = nullptr,
+                         const float* bn_mean = nullptr) {
   if (!X || !Wk || !Y) return fail("mmu_conv_implicit: null pointer");
   if (C % 64 || N % 64 || N <= 0)
     return fail("mmu_conv_implicit: needs C %% 64 == 0, N %% 64 == 0 (C=%ld N=%ld)", C, N);
@@ -577,8 +584,9 @@ static int conv_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, 
   p.tiles_m = (int)((M + tm_ - 1) / tm_);
   p.tiles_n = (int)((N + tn_ - 1) / tn_);
   p.group_m = 1;
-  p.kind = stats ? MMU_EPI_STORE_STATS : MMU_EPI_STORE;
+  p.kind = !stats ? MMU_EPI_STORE : bn_x ? MMU_EPI_STORE_BNB : MMU_EPI_STORE_STATS;
   p.colsum = stats;
+  p.bn_x = (const bf16*)bn_x; p.bn_mask = bn_mask; p.bn_mean = bn_mean;
   p.splitk = 1;
   p.kchunk = p.K;
   // split K (taps x channels) when the map has fewer tiles than half the CUs: ~512 blocks, >= 4
@@ -614,6 +622,13 @@ int mmu_conv_implicit_stats(const void* X, const void* Wk, void* Y, int64_t n_im
 int mmu_conv3x3_implicit(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
                          int64_t N, float* ws, int64_t ws_floats, mmu_stream_t stream) {
   return conv_implicit(X, Wk, Y, n_img, H, W, C, N, 3, 1, nullptr, ws, ws_floats, stream);
+}
+
+int mmu_conv3x3_implicit_bnb(const void* X, const void* Wk, void* Y, int64_t n_img, int64_t H, int64_t W, int64_t C,
+                             int64_t N, const void* bn_x, const uint8_t* bn_mask, const float* bn_mean,
+                             float* stats, float* ws, int64_t ws_floats, mmu_stream_t stream) {
+  if (!stats || !bn_x || !bn_mean) return fail("mmu_conv3x3_implicit_bnb: null table / bn_x / bn_mean");
+  return conv_implicit(X, Wk, Y, n_img, H, W, C, N, 3, 1, stats, ws, ws_floats, stream, bn_x, bn_mask, bn_mean);
 }
 
 int64_t mmu_batchnorm_ws_bytes(int64_t C) { return batchnorm_ws_bytes(C); }
@@ -675,6 +690,23 @@ int mmu_batchnorm_bwd(const void* dY, const void* Y, const void* relu_mask, cons
   q.dw = dweight; q.db = dbias; q.ws = ws; q.mask = (const uint8_t*)relu_mask;
   batchnorm_bwd_launch(q, (hipStream_t)stream);
   return check_launch("mmu_batchnorm_bwd");
+}
+
+int mmu_batchnorm_bwd_parts(const void* dY, const void* Y, const void* relu_mask, const void* X, int64_t rows,
+                            int64_t C, const float* parts, int64_t nparts, const float* weight,
+                            const float* save_mean, const float* save_invstd, int relu, void* dX, void* dSkip,
+                            float* dweight, float* dbias, void* ws, int64_t ws_bytes, mmu_stream_t stream) {
+  if (!dY || !X || !dX || !save_mean || !save_invstd || !parts || nparts <= 0)
+    return fail("mmu_batchnorm_bwd_parts: null pointer / no partials");
+  if (relu && !Y && !relu_mask) return fail("mmu_batchnorm_bwd_parts: relu needs the forward output Y or its relu_mask");
+  if (bn_common(rows, C, ws, ws_bytes, "mmu_batchnorm_bwd_parts")) return 1;
+  BnBwdParams q{};
+  q.dY = (const bf16*)dY; q.Y = (const bf16*)Y; q.X = (const bf16*)X; q.rows = rows; q.C = (int)C; q.w = weight;
+  q.smean = save_mean; q.sinvstd = save_invstd; q.relu = relu; q.dX = (bf16*)dX; q.dS = (bf16*)dSkip;
+  q.dw = dweight; q.db = dbias; q.ws = ws; q.mask = (const uint8_t*)relu_mask;
+  q.parts = parts; q.nparts = nparts;
+  batchnorm_bwd_launch(q, (hipStream_t)stream);
+  return check_launch("mmu_batchnorm_bwd_parts");
 }
 
 int mmu_batchnorm_stats(const void* X, int64_t rows, int64_t C, double* sums, void* ws, int64_t ws_bytes,

@@ -177,9 +177,13 @@ static __device__ __forceinline__ void epi_oct(const GemmParams& p, void* cdst, 
 // the epilogue of a wave's 16*NJ-row x 64-col block acc[4][NJ] (n-subtile i, m-subtile j)
 // through the wave-private LDS region ws (PJ * 4 KiB: passes of 16*PJ rows; the caller has
 // passed a barrier that retires every staging read of it)
-template <int EPI, bool OUT_F32, int NJ, int PJ = 4>
+template <int EPI_, bool OUT_F32, int NJ, int PJ = 4>
 static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64_t z, int slice, int64_t mw,
                                                       int64_t nw, f32x4 (&acc)[4][NJ], int l, char* ws) {
+  // STORE_BNB / ADD_RES_BNB: the STORE / ADD_RES epilogue + the backward reduction of the
+  // BatchNorm whose dY this C is, {sum g, sum g (x - mean)} with g = C (as stored) * ReLU mask
+  constexpr bool BNB = EPI_ == MMU_EPI_STORE_BNB || EPI_ == MMU_EPI_ADD_RES_BNB;
+  constexpr int EPI = EPI_ == MMU_EPI_STORE_BNB ? MMU_EPI_STORE : EPI_ == MMU_EPI_ADD_RES_BNB ? MMU_EPI_ADD_RES : EPI_;
   if (nw >= p.N) return;  // (N % 128 == 0: a 64-column wave block is all in or all out)
   const int q = l & 7, rr = l >> 3;
   const int64_t n = nw + 8 * q;
@@ -201,7 +205,14 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
   // STORE_STATS: the BatchNorm statistics of the bf16 output, {sum, sum of squares} per column
   // and 64-row block into the float2 table p.colsum [ceil(M / 64)][N] (one pass = 64 rows)
   constexpr bool STATS = EPI == MMU_EPI_STORE_STATS;
-  const bool want_cs = !STATS && p.colsum != nullptr && !slab;
+  const bool want_cs = !STATS && !BNB && p.colsum != nullptr && !slab;
+  constexpr bool TAB = STATS || BNB;  // a float2 [ceil(M / 64)][N] table row per pass
+  float mu[8];
+  const int64_t b_l = BNB ? (mw + rr) * p.N + n : 0;  // bn_x / bn_mask (>> 3) offset of the lane's row
+  if (BNB) {
+    const float4 m0 = *(const float4*)(p.bn_mean + n), m1 = *(const float4*)(p.bn_mean + n + 4);
+    mu[0] = m0.x; mu[1] = m0.y; mu[2] = m0.z; mu[3] = m0.w; mu[4] = m1.x; mu[5] = m1.y; mu[6] = m1.z; mu[7] = m1.w;
+  }
   float cs[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) cs[r] = 0.f;
@@ -236,11 +247,11 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
     lw[0] = w0.x; lw[1] = w0.y; lw[2] = w0.z; lw[3] = w0.w; lw[4] = w1.x; lw[5] = w1.y; lw[6] = w1.z; lw[7] = w1.w;
     lb[0] = b0.x; lb[1] = b0.y; lb[2] = b0.z; lb[3] = b0.w; lb[4] = b1.x; lb[5] = b1.y; lb[6] = b1.z; lb[7] = b1.w;
   }
-  static_assert(!STATS || PJ == 4, "STORE_STATS: one epilogue pass = one 64-row statistics block");
+  static_assert(!TAB || PJ == 4, "STORE_STATS / *_BNB: one epilogue pass = one 64-row table block");
 #pragma unroll
   for (int pass = 0; pass < NJ / PJ; ++pass) {
     float st1[8], st2[8];
-    if (STATS) {
+    if (TAB) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) st1[e] = st2[e] = 0.f;
     }
@@ -279,6 +290,23 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
       for (int i = 0; i < 4; ++i) {
         const int ch = 4 * i + (l >> 4);
         *(f32x4*)(ws + r * 256 + ((ch ^ (r & 15)) << 4)) = acc[i][PJ * pass + jj];
+      }
+    }
+    // the BatchNorm input rows + mask bytes (after the acc spill: those registers are free)
+    bf16x8 bx[BNB ? 2 * PJ : 1];
+    uint32_t bm[BNB ? 2 * PJ : 1];
+    if (BNB) {
+#pragma unroll
+      for (int it = 0; it < 2 * PJ; ++it) {
+        const int d = 16 * PJ * pass + 8 * it;
+        if (!slab && m_l + d < p.M) {
+          const int64_t o = b_l + (int64_t)d * p.N;
+          bx[it] = *(const bf16x8*)(p.bn_x + o);
+          bm[it] = p.bn_mask ? (uint32_t)p.bn_mask[o >> 3] : 0xFFu;
+        } else {
+          bx[it] = bf16x8{};
+          bm[it] = 0;
+        }
       }
     }
 #pragma unroll
@@ -324,8 +352,16 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
           st2[e] = fmaf(y, y, st2[e]);
         }
       }
+      if (BNB) {  // g over the stored (bf16) values, as the reduction pass would read them
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float g = ((bm[BNB ? it : 0] >> e) & 1) ? bf2f(f2bf(v[e])) : 0.f;
+          st1[e] += g;
+          st2[e] = fmaf(g, bf2f(bx[BNB ? it : 0][e]) - mu[e], st2[e]);
+        }
+      }
     }
-    if (STATS) {  // lanes sharing q hold the same 8 columns: reduce over rr (8 rows each)
+    if (TAB) {  // lanes sharing q hold the same 8 columns: reduce over rr (8 rows each)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
 #pragma unroll
@@ -780,6 +816,47 @@ __global__ __launch_bounds__(256) void stats64_kernel(const bf16* __restrict__ Y
   }
 }
 
+// the MMU_EPI_STORE_BNB table of a split-K product, after its reduction: {sum g, sum g (x - mean)}
+// per column and 64-row block, g = dY * mask (stats64_kernel's layout)
+__global__ __launch_bounds__(256) void bnb64_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ X,
+                                                    const uint8_t* __restrict__ mask, const float* __restrict__ mean,
+                                                    int64_t M, int64_t N, float* __restrict__ part) {
+  __shared__ float red[2][8][256];
+  const int t = threadIdx.x, oc = t & 31, rs = t >> 5;
+  const int64_t n = (int64_t)blockIdx.y * 256 + 8 * oc, r0 = (int64_t)blockIdx.x * 64;
+  float a[8], b[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = b[e] = 0.f;
+  if (n < N) {
+    float mu[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) mu[e] = mean[n + e];
+    for (int r = rs; r < 64 && r0 + r < M; r += 8) {
+      const int64_t o = (r0 + r) * N + n;
+      const bf16x8 v = *(const bf16x8*)(dY + o), x = *(const bf16x8*)(X + o);
+      const uint32_t mk = mask ? (uint32_t)mask[o >> 3] : 0xFFu;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float g = ((mk >> e) & 1) ? bf2f(v[e]) : 0.f;
+        a[e] += g;
+        b[e] = fmaf(g, bf2f(x[e]) - mu[e], b[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][e][t] = a[e]; red[1][e][t] = b[e]; }
+  __syncthreads();
+  if (rs == 0 && n < N) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float sa = 0.f, sb = 0.f;
+      for (int k = 0; k < 8; ++k) { sa += red[0][e][32 * k + oc]; sb += red[1][e][32 * k + oc]; }
+      part[2 * ((int64_t)blockIdx.x * N + n + e)] = sa;
+      part[2 * ((int64_t)blockIdx.x * N + n + e) + 1] = sb;
+    }
+  }
+}
+
 // sum of the split-K slabs of one (M x N) product into a bf16 C (slice order: deterministic)
 __global__ __launch_bounds__(256) void splitk_reduce_bf16_kernel(const float* __restrict__ ws, bf16* __restrict__ C,
                                                                  int64_t M, int64_t N, int64_t ldc, int splitk) {
@@ -800,13 +877,17 @@ __global__ __launch_bounds__(256) void splitk_reduce_bf16_kernel(const float* __
 void conv3x3_implicit_launch(const GemmParams& p, bool small, hipStream_t s) {
   // p.kind == MMU_EPI_STORE_STATS: the epilogue also writes the output's BatchNorm statistics
   // table (p.colsum); split-K forms the output in the reduce kernel, so a stats pass follows it
+  // (p.kind == MMU_EPI_STORE_BNB, a data gradient: the reduction table of the BatchNorm before it)
   const bool stats = p.kind == MMU_EPI_STORE_STATS && p.splitk == 1;
+  const bool bnb = p.kind == MMU_EPI_STORE_BNB && p.splitk == 1;
   const dim3 grid(p.tiles_m * p.tiles_n, p.splitk, 1);
   if (small) {
     if (stats) hipLaunchKernelGGL(gemm_conva_small_kernel<MMU_EPI_STORE_STATS>, grid, dim3(256), 0, s, p);
+    else if (bnb) hipLaunchKernelGGL(gemm_conva_small_kernel<MMU_EPI_STORE_BNB>, grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL(gemm_conva_small_kernel<MMU_EPI_STORE>, grid, dim3(256), 0, s, p);
   } else {
     if (stats) hipLaunchKernelGGL(gemm_conva_kernel<MMU_EPI_STORE_STATS>, grid, dim3(512), 0, s, p);
+    else if (bnb) hipLaunchKernelGGL(gemm_conva_kernel<MMU_EPI_STORE_BNB>, grid, dim3(512), 0, s, p);
     else hipLaunchKernelGGL(gemm_conva_kernel<MMU_EPI_STORE>, grid, dim3(512), 0, s, p);
   }
   if (p.splitk > 1) {
@@ -816,6 +897,9 @@ void conv3x3_implicit_launch(const GemmParams& p, bool small, hipStream_t s) {
     if (p.kind == MMU_EPI_STORE_STATS)
       hipLaunchKernelGGL(stats64_kernel, dim3((unsigned)((p.M + 63) / 64), (unsigned)((p.N + 255) / 256)), dim3(256),
                          0, s, (const bf16*)p.C, p.M, p.N, p.colsum);
+    if (p.kind == MMU_EPI_STORE_BNB)
+      hipLaunchKernelGGL(bnb64_kernel, dim3((unsigned)((p.M + 63) / 64), (unsigned)((p.N + 255) / 256)), dim3(256),
+                         0, s, (const bf16*)p.C, p.bn_x, p.bn_mask, p.bn_mean, p.M, p.N, p.colsum);
   }
 }
 
@@ -860,6 +944,12 @@ void gemm_launch(const GemmParams& p, bool ak, bool bk, bool f32out, bool big, i
     case MMU_EPI_STORE_STATS:  // (the 1x1 conv forward: X rows . W^T, both K-major)
       if (big) launch_t<true, true, MMU_EPI_STORE_STATS, false>(p, true, batch, s);
       else launch_t<true, true, MMU_EPI_STORE_STATS, false>(p, false, batch, s);
+      break;
+    case MMU_EPI_STORE_BNB:  // (the 1x1 conv data gradient: dY rows . W, B N-major)
+      launch_t<true, false, MMU_EPI_STORE_BNB, false>(p, big, batch, s);
+      break;
+    case MMU_EPI_ADD_RES_BNB:
+      launch_t<true, false, MMU_EPI_ADD_RES_BNB, false>(p, big, batch, s);
       break;
   }
 }

@@ -44,6 +44,11 @@ struct GemmParams {
   // forward / data gradient (gemm_conva_kernel): A[out pixel][tap * conv_c + c] gathered
   int conv_h, conv_w, conv_c, conv_ho, conv_wo, conv_ks, conv_s, conv_pad;
   int64_t conv_in_bytes;
+  // STORE_BNB / ADD_RES_BNB: the BatchNorm whose dY this product forms (input rows [M][N],
+  // ReLU mask [M][N/8] or null, batch mean [N]); its backward reduction table goes to colsum
+  const bf16* bn_x;
+  const uint8_t* bn_mask;
+  const float* bn_mean;
 };
 void conv3x3_wgrad_launch(const GemmParams& p, hipStream_t s);
 void conv3x3_implicit_launch(const GemmParams& p, bool small, hipStream_t s);  // small: 128x128 tiles
@@ -199,6 +204,8 @@ struct BnBwdParams {
   const uint8_t* mask;  // optional ReLU mask (read instead of Y)
   double* lsum;        // as BnFwdParams: {sum g, sum g*(x-mean), rows} (+= dweight / dbias) and stop
   const double* gsum;  // finalize + apply from the exchanged sums
+  const float* parts;  // or the reduction table of the product that formed dY (float2 [nparts][C])
+  int64_t nparts;
 };
 void batchnorm_bwd_launch(const BnBwdParams& q, hipStream_t s);
 int64_t batchnorm_ws_bytes(int64_t C);

@@ -15,7 +15,8 @@ c_i64, c_i32, c_f32, c_u64, c_vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_floa
 c_f32p, c_i64p, c_dp = ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)
 
 MMU_BF16, MMU_F32 = 0, 1
-EPI_STORE, EPI_BIAS_GELU, EPI_BIAS_DROP_RES, EPI_DGELU, EPI_ADD_RES, EPI_BIAS_DROP_QGELU, EPI_STORE_STATS = range(7)
+(EPI_STORE, EPI_BIAS_GELU, EPI_BIAS_DROP_RES, EPI_DGELU, EPI_ADD_RES, EPI_BIAS_DROP_QGELU, EPI_STORE_STATS,
+ EPI_STORE_BNB, EPI_ADD_RES_BNB) = range(9)
 
 
 class Epilogue(ctypes.Structure):
@@ -24,7 +25,8 @@ class Epilogue(ctypes.Structure):
                 ("residual", c_vp), ("ldr", c_i64), ("res_bstride", c_i64), ("aux", c_vp), ("ldx", c_i64),
                 ("aux_bstride", c_i64), ("colsum", c_vp), ("colsum_bstride", c_i64), ("drop_p", c_f32),
                 ("seed", c_u64), ("workspace", c_vp), ("workspace_floats", c_i64), ("res_ln_mean", c_vp),
-                ("res_ln_rstd", c_vp), ("res_ln_w", c_vp), ("res_ln_b", c_vp), ("res_ln_bstride", c_i64)]
+                ("res_ln_rstd", c_vp), ("res_ln_w", c_vp), ("res_ln_b", c_vp), ("res_ln_bstride", c_i64),
+                ("bn_x", c_vp), ("bn_mask", c_vp), ("bn_mean", c_vp)]
 
 
 # name -> (restype, argtypes); every entry must be exported by the library (tested on CPU)
@@ -66,6 +68,8 @@ SIGNATURES = {
     "mmu_row_pool_fwd": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "mmu_row_pool_bwd": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "mmu_conv3x3_implicit": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp]),
+    "mmu_conv3x3_implicit_bnb": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp,
+                                         c_vp, c_vp, c_i64, c_vp]),
     "mmu_conv3x3_wgrad": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp]),
     "mmu_conv_implicit": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64,
                                   c_vp]),
@@ -81,6 +85,8 @@ SIGNATURES = {
                                   c_f32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "mmu_batchnorm_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp,
                                   c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "mmu_batchnorm_bwd_parts": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i32,
+                                        c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "mmu_batchnorm_stats": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "mmu_batchnorm_fwd_sums": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32,
                                        c_f32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
@@ -107,7 +113,7 @@ class NativeError(RuntimeError):
 
 
 # include/mmu.h MMU_ABI_VERSION: the argument lists SIGNATURES binds
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 def load():

@@ -10,7 +10,7 @@ import torch
 
 from . import _native as N
 from ._native import (Epilogue, EPI_STORE, EPI_BIAS_GELU, EPI_BIAS_DROP_RES, EPI_DGELU, EPI_ADD_RES,  # noqa: F401
-                      EPI_BIAS_DROP_QGELU, EPI_STORE_STATS)
+                      EPI_BIAS_DROP_QGELU, EPI_STORE_STATS, EPI_STORE_BNB, EPI_ADD_RES_BNB)
 
 
 def bn_stats_table(rows, C, device):
@@ -47,9 +47,11 @@ def _want(t, dtype, name):
 
 def epilogue(kind=EPI_STORE, bias=None, residual=None, aux=None, colsum=None, drop_p=0.0, seed=0, accumulate=False,
              ldr=0, ldx=0, bias_bstride=0, res_bstride=0, aux_bstride=0, colsum_bstride=0, res_ln=None,
-             res_ln_bstride=0):
+             res_ln_bstride=0, bn=None):
     """res_ln = (mean, rstd, w, b): with BIAS_DROP_RES into an f32 C, the residual is the LayerNorm
-    output recomputed from the f32 ``residual`` rows (the previous LayerNorm's input)."""
+    output recomputed from the f32 ``residual`` rows (the previous LayerNorm's input).
+    bn = (x, relu_mask or None, mean): with STORE_BNB / ADD_RES_BNB, the BatchNorm whose dY the
+    product forms; colsum is then its backward reduction table (bn_stats_table of x's rows)."""
     e = Epilogue()
     e.kind, e.accumulate = kind, int(accumulate)
     e.bias, e.bias_bstride = _ptr(bias), bias_bstride
@@ -66,7 +68,17 @@ def epilogue(kind=EPI_STORE, bias=None, residual=None, aux=None, colsum=None, dr
                 raise N.NativeError("epilogue res_ln tensors must be contiguous")
         e.res_ln_mean, e.res_ln_rstd, e.res_ln_w, e.res_ln_b = (_ptr(t) for t in res_ln)
         e.res_ln_bstride = res_ln_bstride
+    if bn is not None:
+        _bnb_check(*bn, "epilogue bn")
+        e.bn_x, e.bn_mask, e.bn_mean = (_ptr(t) for t in bn)
     return e
+
+
+def _bnb_check(x, mask, mean, what):
+    if (x.dtype != torch.bfloat16 or mean.dtype != torch.float32 or not mean.is_contiguous()
+            or mean.numel() != x.shape[1] or not x.is_contiguous(memory_format=torch.channels_last)):
+        raise N.NativeError(f"{what}: (x channels-last bf16, relu_mask, mean f32 [C]) of a training BatchNorm")
+    _bn_mask_check(mask, x, what)
 
 
 SPLITK_WS_FLOATS = 16 << 20  # 64 MiB per (device, stream), reused stream-ordered by every split-K product
@@ -430,9 +442,28 @@ def conv_implicit(X, Wk, Y, ksize=3, stride=1, stats=None):
            _stream(X))
 
 
-def conv3x3_implicit(X, Wk, Y):
-    """the 3x3 / stride-1 / pad-1 case of conv_implicit (Y and X share H, W)"""
-    conv_implicit(X, Wk, Y, 3, 1)
+def conv3x3_implicit(X, Wk, Y, bnb=None, table=None):
+    """the 3x3 / stride-1 / pad-1 case of conv_implicit (Y and X share H, W).  bnb = (x, relu_mask,
+    mean) with table (bn_stats_table of Y's rows): Y is the data gradient dY of that training
+    BatchNorm, and the table receives its backward reduction (mmu_conv3x3_implicit_bnb)."""
+    if bnb is None:
+        conv_implicit(X, Wk, Y, 3, 1)
+        return
+    _dev_check(X, Wk, Y, table)
+    x, mask, mean = bnb
+    _bnb_check(x, mask, mean, "conv3x3_implicit bnb")
+    n, c, h, w = X.shape
+    nout = Y.shape[1]
+    cl = torch.channels_last
+    if (Y.shape != (n, nout, h, w) or x.shape != Y.shape or Y.dtype != torch.bfloat16 or X.dtype != torch.bfloat16
+            or Wk.dtype != torch.bfloat16 or tuple(Wk.shape) != (nout, 3, 3, c) or not Wk.is_contiguous()
+            or not X.is_contiguous(memory_format=cl) or not Y.is_contiguous(memory_format=cl)):
+        raise N.NativeError("conv3x3_implicit bnb: X / Y / x channels-last bf16, Wk [Nout][3][3][C] bf16")
+    if table.dtype != torch.float32 or table.numel() < ((n * h * w + 63) // 64) * nout * 2:
+        raise N.NativeError("conv3x3_implicit bnb: table too small (kernels.bn_stats_table)")
+    ws = _splitk_workspace(Y.device)
+    N.call("mmu_conv3x3_implicit_bnb", _ptr(X), _ptr(Wk), _ptr(Y), n, h, w, c, nout, _ptr(x), _ptr(mask),
+           _ptr(mean), _ptr(table), _ptr(ws), ws.numel(), _stream(X))
 
 
 def _stem_check(X, what):
@@ -583,8 +614,10 @@ def batchnorm_fwd(X, Y, weight, bias, running_mean, running_var, training, momen
 
 
 def batchnorm_bwd(dY, Y, X, weight, save_mean, save_invstd, relu, dX, dSkip=None, dweight=None, dbias=None,
-                  relu_mask=None):
-    """relu: g = dY * [Y > 0] from relu_mask (batchnorm_fwd's) when given, else from Y."""
+                  relu_mask=None, parts=None):
+    """relu: g = dY * [Y > 0] from relu_mask (batchnorm_fwd's) when given, else from Y.  parts:
+    (table, nparts) of the reduction the product that formed dY wrote (STORE_BNB / ADD_RES_BNB,
+    conv3x3_implicit bnb): no reduction pass (mmu_batchnorm_bwd_parts)."""
     _dev_check(dY, X, dX)
     _want(X, torch.bfloat16, "batchnorm_bwd X")
     _bn_mask_check(relu_mask, X, "batchnorm_bwd")
@@ -593,6 +626,14 @@ def batchnorm_bwd(dY, Y, X, weight, save_mean, save_invstd, relu, dX, dSkip=None
     _bn_map_check("batchnorm_bwd", X, dY, Y, dX, dSkip)
     rows = X.numel() // C
     ws = _bn_workspace(X.device)
+    if parts is not None:
+        table, nparts = parts
+        if table.numel() < nparts * C * 2 or nparts != (rows + 63) // 64:
+            raise N.NativeError("batchnorm_bwd: parts must be dY's reduction table (bn_stats_table)")
+        N.call("mmu_batchnorm_bwd_parts", _ptr(dY), _ptr(Y), _ptr(relu_mask), _ptr(X), rows, C, _ptr(table), nparts,
+               _ptr(weight), _ptr(save_mean), _ptr(save_invstd), int(bool(relu)), _ptr(dX), _ptr(dSkip),
+               _ptr(dweight), _ptr(dbias), _ptr(ws), ws.numel() * 4, _stream(X))
+        return
     N.call("mmu_batchnorm_bwd", _ptr(dY), _ptr(Y), _ptr(relu_mask), _ptr(X), rows, C, _ptr(weight), _ptr(save_mean),
            _ptr(save_invstd), int(bool(relu)), _ptr(dX), _ptr(dSkip), _ptr(dweight), _ptr(dbias), _ptr(ws),
            ws.numel() * 4, _stream(X))

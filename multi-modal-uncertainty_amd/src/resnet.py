@@ -31,6 +31,12 @@ STREAM_RESIDUE = os.environ.get("MMU_STREAM_RESIDUE", "1") != "0"
 # its own epilogue (MMU_EPI_STORE_STATS), so the BatchNorm after it skips its statistics pass
 # (round 6; MMU_BN_STATS_FUSION=0: the BatchNorms compute them, for A/Bs)
 BN_STATS_FUSION = os.environ.get("MMU_BN_STATS_FUSION", "1") != "0"
+# ... and the backward: the data-gradient product of the conv that is a training BatchNorm's only
+# consumer (a Bottleneck's conv2 / conv3, an identity block's conv1) writes that BatchNorm's
+# backward reduction {sum g, sum g (x - mean)} in its epilogue (MMU_EPI_STORE_BNB / ADD_RES_BNB,
+# mmu_conv3x3_implicit_bnb), so the BatchNorm backward skips its reduction pass
+# (round 6; MMU_BN_BWD_FUSION=0 turns it off, for A/Bs)
+BN_BWD_FUSION = os.environ.get("MMU_BN_BWD_FUSION", "1") != "0"
 
 
 class _BnStats:
@@ -39,6 +45,24 @@ class _BnStats:
 
     def __init__(self):
         self.parts = None
+
+
+class _BnLink:
+    """A training BatchNorm's hand-off to the conv that consumes its output (BN_BWD_FUSION): the
+    BatchNorm's forward fills x / mask / mean (its input, ReLU mask, batch mean), the conv's
+    backward fills ``parts`` (table, nparts) from its data-gradient epilogue, the BatchNorm's
+    backward consumes them.  Carried as the ``_mmu_bnb`` attribute of the BatchNorm output."""
+    __slots__ = ("x", "mask", "mean", "parts")
+
+    def __init__(self):
+        self.x = self.mask = self.mean = self.parts = None
+
+    def operands(self):
+        """(x, mask, mean) for the epilogue, or None once the BatchNorm's backward has run"""
+        return None if self.x is None else (self.x, self.mask, self.mean)
+
+    def release(self):
+        self.x = self.mask = self.mean = self.parts = None
 
 
 class torch_ops_only:
@@ -60,8 +84,8 @@ class _BatchNormAct(torch.autograd.Function):
     mmu_batchnorm_fwd / mmu_batchnorm_bwd (batch statistics, running stats updated)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, skip, bn, relu, sink=None, skip_res=None, y_res=None, parts=None):
-        ctx.bias_ref, ctx.sink = bias, sink
+    def forward(ctx, x, weight, bias, skip, bn, relu, sink=None, skip_res=None, y_res=None, parts=None, link=None):
+        ctx.bias_ref, ctx.sink, ctx.link = bias, sink, link
         Y = torch.empty_like(x)
         C = x.shape[1]
         smean = torch.empty(C, dtype=torch.float32, device=x.device)
@@ -73,6 +97,8 @@ class _BatchNormAct(torch.autograd.Function):
                         save_invstd=sinv, relu_mask=mask, skip_res=skip_res, y_res=y_res, parts=parts)
         ctx.save_for_backward(x, mask, weight, smean, sinv)
         ctx.relu, ctx.has_skip = relu, skip is not None
+        if link is not None:
+            link.x, link.mask, link.mean = x, mask, smean
         return Y
 
     @staticmethod
@@ -88,12 +114,16 @@ class _BatchNormAct(torch.autograd.Function):
         if want_b:
             bias = ctx.bias_ref
             db = bias.grad if bias.grad is not None else torch.zeros_like(bias)
-        K.batchnorm_bwd(dY, None, x, weight, smean, sinv, ctx.relu, dX, dS, dw, db, relu_mask=mask)
+        parts = None
+        if ctx.link is not None:  # the reduction the consuming conv's dX epilogue wrote, if it did
+            parts = ctx.link.parts
+            ctx.link.release()
+        K.batchnorm_bwd(dY, None, x, weight, smean, sinv, ctx.relu, dX, dS, dw, db, relu_mask=mask, parts=parts)
         rw = dw if (want_w and weight.grad is None) else None
         rb = db if (want_b and ctx.bias_ref.grad is None) else None
         if ctx.sink is not None and dS is not None:  # conv1's dX GEMM adds it (EPI_ADD_RES)
             ctx.sink.g, dS = dS, None
-        return dX, rw, rb, dS, None, None, None, None, None, None
+        return dX, rw, rb, dS, None, None, None, None, None, None, None
 
 
 def _momentum(bn):
@@ -247,8 +277,12 @@ class BatchNorm2d(nn.BatchNorm2d):
             if self.training and self.track_running_stats:
                 # the statistics the producing conv's epilogue wrote (BN_STATS_FUSION), if any
                 parts = x.__dict__.pop("_mmu_bnparts", None)
-                return _with_res(_BatchNormAct.apply(x, self.weight, self.bias, skip, self, relu, skip_sink, skip_res,
-                                                     y_res, parts), y_res)
+                link = _BnLink() if BN_BWD_FUSION and torch.is_grad_enabled() else None
+                y = _BatchNormAct.apply(x, self.weight, self.bias, skip, self, relu, skip_sink, skip_res, y_res,
+                                        parts, link)
+                if link is not None:
+                    y._mmu_bnb = link
+                return _with_res(y, y_res)
             if not self.training and not (torch.is_grad_enabled() and (
                     x.requires_grad or self.weight.requires_grad or (skip is not None and skip.requires_grad))):
                 # the one-pass running-statistics kernel has no backward: a graph through an
@@ -321,9 +355,9 @@ class _ConvBF16(torch.autograd.Function):
     plus an AccumulateGrad add)."""
 
     @staticmethod
-    def forward(ctx, x, w, w16, stride, padding, flipped=None, stats=None):
+    def forward(ctx, x, w, w16, stride, padding, flipped=None, stats=None, link=None):
         ctx.save_for_backward(x, w16)
-        ctx.w, ctx.conf, ctx.flipped = w, (stride, padding), flipped
+        ctx.w, ctx.conf, ctx.flipped, ctx.link = w, (stride, padding), flipped, link
         cout = w16.shape[0]
         if _is_stem(w16, stride, padding):  # the 7x7 / 2 stem: mmu_stem_conv_fwd
             n, _, h, wd = x.shape
@@ -375,7 +409,7 @@ class _ConvBF16(torch.autograd.Function):
             dx, gw, _ = torch.ops.aten.convolution_backward(dy, x, w16, None, stride, padding, (1, 1), False, (0, 0),
                                                             1, (True, True, False))
             g.add_(gw)
-            return dx, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None
         if need_x and not mmu_x:
             dx = torch.ops.aten.convolution_backward(dy, x, w16, None, stride, padding, (1, 1), False, (0, 0), 1,
                                                      (True, False, False))[0]
@@ -383,7 +417,13 @@ class _ConvBF16(torch.autograd.Function):
             dx = torch.empty_like(x, memory_format=cl)
             # the store's flipped copy (refreshed with the bf16 filters), else one made here
             wf = ctx.flipped() if ctx.flipped is not None else w16.flip(2, 3).permute(1, 2, 3, 0).contiguous()
-            K.conv3x3_implicit(dy, wf, dx)
+            bnb = ctx.link.operands() if ctx.link is not None else None
+            if bnb is not None:  # + the backward reduction of the BatchNorm that produced x
+                table = K.bn_stats_table(dx.numel() // dx.shape[1], dx.shape[1], dx.device)
+                K.conv3x3_implicit(dy, wf, dx, bnb=bnb, table=table[0])
+                ctx.link.parts = table
+            else:
+                K.conv3x3_implicit(dy, wf, dx)
         if store_g:
             # straight into the gradient store, on the side stream
             def dw_side():
@@ -403,7 +443,7 @@ class _ConvBF16(torch.autograd.Function):
             if g is not None:
                 g.add_(rw)
                 rw = None
-        return dx, rw, None, None, None, None, None
+        return dx, rw, None, None, None, None, None, None
 
 
 class _SkipGrad:
@@ -433,6 +473,10 @@ def _conv_geo(w16, stride, padding):
 # rows: a data-parallel rank running B / N samples sets N to route its convs exactly as the single
 # device does at the global batch B (tests/test_dp_gpu.py: the sync-BN root cause)
 ROUTE_M_SCALE = 1
+# Route A/B switch (round 6): with the BatchNorm passes fused into the conv epilogues, an mmu
+# product also saves a BatchNorm pass.  MMU_ROUTE_FUSED=1 moves every shape-eligible 1x1 forward
+# and the 128-channel 3x3 forward onto mmu; 2 also the 64-channel 3x3 forward / data gradient.
+ROUTE_FUSED = int(os.environ.get("MMU_ROUTE_FUSED", "0"))
 
 
 def _mmu_conv(geo, xshape, cout):
@@ -452,8 +496,11 @@ def _mmu_conv(geo, xshape, cout):
     pad = ks // 2
     M = ROUTE_M_SCALE * n * ((h + 2 * pad - ks) // st + 1) * ((w + 2 * pad - ks) // st + 1)
     if ks == 3 and st == 1:
-        fwd = cin % 64 == 0 and cout % 128 == 0 and cout >= 256 and M >= 256
+        fwd = cin % 64 == 0 and cout % 128 == 0 and (cout >= 256 or ROUTE_FUSED >= 1) and M >= 256
         dx = cout % 64 == 0 and cin % 128 == 0 and M >= 256
+        if ROUTE_FUSED >= 2:
+            fwd = cin % 64 == 0 and cout % 64 == 0 and M >= 256
+            dx = cout % 64 == 0 and cin % 64 == 0 and M >= 256
         dw = cin % 256 == 0 and cout % 128 == 0 and M >= 1024
         return fwd, dx, dw
     if st == 1:  # 1x1 stride 1: _Conv1x1
@@ -477,7 +524,7 @@ def _mmu_1x1(cin, cout, M, H):
     brought it level with MIOpen's wrw, which also pays a bf16 -> f32 add into the store).
     mmu_gemm needs N % 128 == 0 for its output columns (and M-major A rows % 128 for dW)."""
     M = M * ROUTE_M_SCALE
-    fwd = cout % 128 == 0 and cin % 64 == 0 and 25088 <= M <= 50176 and (cin > cout or M < 50176)
+    fwd = cout % 128 == 0 and cin % 64 == 0 and (ROUTE_FUSED >= 1 or (25088 <= M <= 50176 and (cin > cout or M < 50176)))
     dx = cin % 128 == 0 and cout % 64 == 0 and (cin > cout or M >= 12544)
     dw = cin % 128 == 0 and cout % 128 == 0 and M <= 50176 and H <= 14
     return fwd, dx, dw
@@ -490,7 +537,7 @@ class _Conv1x1(torch.autograd.Function):
     The GEMMs are excluded from bench.py's BERT-layer GEMM timing (timing_paused)."""
 
     @staticmethod
-    def forward(ctx, x, w, w16, sink, stats=None):
+    def forward(ctx, x, w, w16, sink, stats=None, link=None):
         Nb, C, H, W = x.shape
         Co = w16.shape[0]
         M = Nb * H * W
@@ -506,7 +553,7 @@ class _Conv1x1(torch.autograd.Function):
         else:
             y = torch.ops.aten.convolution(x, w16, None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1)
         ctx.save_for_backward(x, w16)
-        ctx.w, ctx.sink, ctx.use = w, sink, (use_d, use_w)
+        ctx.w, ctx.sink, ctx.use, ctx.link = w, sink, (use_d, use_w), link
         return y
 
     @staticmethod
@@ -525,7 +572,14 @@ class _Conv1x1(torch.autograd.Function):
         with K.timing_paused():
             if need_x and use_d:
                 dx = torch.empty_like(x, memory_format=torch.channels_last)
-                epi = K.epilogue(K.EPI_ADD_RES, residual=_rows(skip)) if skip is not None else None
+                bnb = ctx.link.operands() if ctx.link is not None else None
+                if bnb is not None:  # + the backward reduction of the BatchNorm that produced x
+                    table = K.bn_stats_table(M, C, x.device)
+                    epi = K.epilogue(K.EPI_ADD_RES_BNB if skip is not None else K.EPI_STORE_BNB,
+                                     residual=_rows(skip) if skip is not None else None, colsum=table[0], bn=bnb)
+                    ctx.link.parts = table
+                else:
+                    epi = K.epilogue(K.EPI_ADD_RES, residual=_rows(skip)) if skip is not None else None
                 K.gemm(_rows(dy), Co, 1, w16.view(Co, C), C, 0, _rows(dx), C, M, C, Co, epi=epi)
                 skip = None
             elif need_x:
@@ -535,7 +589,7 @@ class _Conv1x1(torch.autograd.Function):
                 dx = gx if skip is None else gx + skip
                 if both:  # (one MIOpen call for both products when neither goes elsewhere)
                     ctx.w.grad.add_(gw)
-                    return dx, None, None, None, None
+                    return dx, None, None, None, None, None
             if need_w:
                 g = ctx.w.grad
                 if g is None:
@@ -553,7 +607,7 @@ class _Conv1x1(torch.autograd.Function):
                     _wgrad_run(dw, dy, x)
                 else:
                     dw()
-        return dx, rw, None, None, None
+        return dx, rw, None, None, None, None
 
 
 class StoreConv2d(nn.Conv2d):
@@ -600,17 +654,21 @@ class StoreConv2d(nn.Conv2d):
         N_, C, H, W = x.shape
         return _mmu_1x1(C, self.out_channels, N_ * H * W, H)[1]
 
-    def forward(self, x, sink=None):
+    def forward(self, x, sink=None, bnb=False):
+        """bnb: x is a training BatchNorm's output and this conv its only consumer (the gradient
+        of x is this conv's dX alone): the dX epilogue may write that BatchNorm's backward
+        reduction (BN_BWD_FUSION, _BnLink)"""
         w16 = self._compute_weight(x)
         if w16 is not None:
+            link = x.__dict__.get("_mmu_bnb") if bnb else None
             x = x.contiguous(memory_format=torch.channels_last)
             # a training forward (the BatchNorm after this conv uses batch statistics): the conv's
             # epilogue writes them when it runs on the mmu products (BN_STATS_FUSION)
             st = _BnStats() if BN_STATS_FUSION and self.training and torch.is_grad_enabled() else None
             if self._is_1x1():
-                y = _Conv1x1.apply(x, self.weight, w16, sink, st)
+                y = _Conv1x1.apply(x, self.weight, w16, sink, st, link)
             else:
-                y = _ConvBF16.apply(x, self.weight, w16, self.stride, self.padding, self._flipped_getter(), st)
+                y = _ConvBF16.apply(x, self.weight, w16, self.stride, self.padding, self._flipped_getter(), st, link)
             if st is not None and st.parts is not None:
                 y._mmu_bnparts = st.parts
             return y
@@ -691,9 +749,10 @@ class Bottleneck(nn.Module):
             skip = self.downsample[1](self.downsample[0](x), out_res=True)
         else:
             skip = self.downsample(x)
-        y = self.bn1(self.conv1(x, sink=sink), relu=True)
-        y = self.bn2(self.conv2(y), relu=True)
-        out = self.bn3(self.conv3(y), skip=skip, relu=True, skip_sink=sink, out_res=True)
+        # (x's gradient is conv1's dX alone when bn3 hands its skip gradient to the sink)
+        y = self.bn1(self.conv1(x, sink=sink, bnb=sink is not None), relu=True)
+        y = self.bn2(self.conv2(y, bnb=True), relu=True)
+        out = self.bn3(self.conv3(y, bnb=True), skip=skip, relu=True, skip_sink=sink, out_res=True)
         if getattr(skip, "_mmu_res", None) is not None:
             del skip._mmu_res  # read by this bn3 only: free the residue with the block
         return out

@@ -254,6 +254,11 @@ def _sync_bn_worker(rank, world, port, q, precision, backend="gloo", pin=False):
             # pin: the ranks route their convs (engine, gathered / MIOpen) as the single device does
             # at the global batch (resnet.ROUTE_M_SCALE)
             R.ROUTE_M_SCALE = world if (pin and ranks) else 1
+            # pin: the single device also forms its BatchNorm statistics in the BatchNorm's own pass,
+            # as the synchronised ranks do (the conv-epilogue statistics, BN_STATS_FUSION, are another
+            # summation order, whose ~1e-8 changes this trunk amplifies ~10x per stage to ~9e-3 of
+            # the gradient: profiles/r6_bn_fusion_chaos.txt)
+            R.BN_STATS_FUSION = not pin
             m, o = make(prec)
             bk = None
             if ranks:
@@ -351,7 +356,9 @@ def test_dp_sync_batchnorm_bf16_gap_is_conv_routing():
     noise from the single device (9.5e-3 vs 6e-4, round 5).  Routing every conv as the single
     device does at the global batch (resnet.ROUTE_M_SCALE = world) must bring the synchronised
     step back to the single device's own noise: gradient and post-step change within 2x the
-    reordered batch's (bar written before the run)."""
+    reordered batch's (bar written before the run).  Both sides form their BatchNorm statistics in
+    the BatchNorm's own pass (round 6: the conv-epilogue statistics are another summation order,
+    profiles/r6_bn_fusion_chaos.txt)."""
     for rank, _, _, _, _, _, _, gsd, g0, dsd, d0 in _spawn(_sync_bn_worker, 2, "bf16", "gloo", True):
         print(f"\n[dp sync-bn bf16, routing pinned] rank {rank}: vs the single device: grad {gsd:.3e} (reordered "
               f"batch {g0:.3e}), post-step change {dsd:.3e} (reordered batch {d0:.3e})")

@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared() if not hasattr(lib, n)]
     assert not missing, missing
     assert set(declared()) == set(_native.SIGNATURES), "binding table and header disagree"
-    assert _native.load().mmu_version() == 3
+    assert _native.load().mmu_version() == 4
 
 
 def test_epilogue_struct_layout_matches_header(tmp_path):

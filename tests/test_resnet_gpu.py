@@ -349,7 +349,7 @@ def test_batchnorm_momentum_none_cumulative_average_on_device(dev):
 
 
 @pytest.mark.parametrize("n,cin,cout,h,ks,st", [(256, 256, 256, 14, 3, 1), (4, 256, 256, 14, 3, 1),
-                                               (24, 128, 128, 28, 3, 1), (8, 512, 512, 13, 3, 2),
+                                               (24, 128, 128, 28, 3, 1), (8, 512, 512, 13, 3, 2), (8, 64, 64, 56, 3, 1),
                                                (16, 1024, 2048, 14, 1, 2)])
 def test_conv_stats_epilogue_matches_output(dev, n, cin, cout, h, ks, st):
     """mmu_conv_implicit_stats (MMU_EPI_STORE_STATS, round 6): the BatchNorm statistics table the
@@ -374,12 +374,13 @@ def test_conv_stats_epilogue_matches_output(dev, n, cin, cout, h, ks, st):
     torch.testing.assert_close(t[..., 1], (blocks * blocks).sum(1), rtol=1e-4, atol=1e-3)
 
 
-def test_gemm_stats_epilogue_and_bn_parts(dev):
+@pytest.mark.parametrize("M,C,Co", [(25088, 1024, 256), (25088, 512, 128), (200, 256, 256), (12544, 2048, 512)])
+def test_gemm_stats_epilogue_and_bn_parts(dev, M, C, Co):
     """the 1x1 conv forward's STORE_STATS GEMM, then mmu_batchnorm_fwd_parts on its table: the same
-    BatchNorm output / saved statistics / running statistics as mmu_batchnorm_fwd's own pass."""
+    BatchNorm output / saved statistics / running statistics as mmu_batchnorm_fwd's own pass
+    (big tiles; 128x128 tiles for 128 output channels or < 256 rows)."""
     from src import kernels as K
     torch.manual_seed(3)
-    M, C, Co = 25088, 1024, 256
     x = torch.randn(M, C, device=dev).to(torch.bfloat16)
     w = (torch.randn(Co, C, device=dev) * C ** -0.5).to(torch.bfloat16)
     y = torch.empty(M, Co, dtype=torch.bfloat16, device=dev)
@@ -389,7 +390,7 @@ def test_gemm_stats_epilogue_and_bn_parts(dev):
     t = table.view(nparts, Co, 2).sum(0)
     torch.testing.assert_close(t[:, 0], y.float().sum(0), rtol=1e-4, atol=1e-2)
     torch.testing.assert_close(t[:, 1], (y.float() ** 2).sum(0), rtol=1e-4, atol=1e-2)
-    Y4 = y.view(32, 28, 28, Co).permute(0, 3, 1, 2)  # channels-last [N, C, H, W] view of the rows
+    Y4 = y.view(M, 1, 1, Co).permute(0, 3, 1, 2)  # channels-last [N, C, H, W] view of the rows
     outs = []
     for parts in (None, (table, nparts)):
         Yo = torch.empty_like(Y4)
@@ -402,3 +403,98 @@ def test_gemm_stats_epilogue_and_bn_parts(dev):
         outs.append((Yo.float(), rm, rv, sm, si))
     for a, b in zip(outs[0], outs[1]):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-2 if a.dim() == 4 else 1e-6)
+
+
+def _bnb_reference(dx_rows, x_rows, mask, mean):
+    """the float2 [ceil(M/64)][C] table {sum g, sum g (x - mean)}, g = dx * relu bit (mmu.h *_BNB)"""
+    M, C = dx_rows.shape
+    bits = ((mask.view(M, C // 8, 1).int() >> torch.arange(8, device=mask.device, dtype=torch.int32)) & 1)
+    g = dx_rows.float() * bits.reshape(M, C).float()
+    h = g * (x_rows.float() - mean)
+    nparts = (M + 63) // 64
+    pad = nparts * 64 - M
+    g = torch.nn.functional.pad(g, (0, 0, 0, pad)).view(nparts, 64, C).sum(1)
+    h = torch.nn.functional.pad(h, (0, 0, 0, pad)).view(nparts, 64, C).sum(1)
+    return g, h
+
+
+def _bn_fwd_for_bnb(dev, n, C, hw, seed):
+    from src import kernels as K
+    torch.manual_seed(seed)
+    cl = torch.channels_last
+    x = (torch.randn(n, C, hw, hw, device=dev) * 2 + 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
+    Y = torch.empty_like(x)
+    wgt, bias = 1 + 0.1 * torch.randn(C, device=dev), 0.1 * torch.randn(C, device=dev)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    sm, si = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=dev)
+    K.batchnorm_fwd(x, Y, wgt, bias, rm, rv, True, 0.1, 1e-5, relu=True, save_mean=sm, save_invstd=si,
+                    relu_mask=mask)
+    return x, wgt, sm, si, mask
+
+
+def _check_bn_bwd_parts(dev, dx4, x, wgt, sm, si, mask, table, nparts):
+    """mmu_batchnorm_bwd_parts on the epilogue's table == mmu_batchnorm_bwd's own reduction"""
+    from src import kernels as K
+    C = x.shape[1]
+    outs = []
+    for parts in (None, (table, nparts)):
+        dX = torch.empty_like(x)
+        dw, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+        K.batchnorm_bwd(dx4, None, x, wgt, sm, si, True, dX, None, dw, db, relu_mask=mask, parts=parts)
+        outs.append((dX.float(), dw, db))
+    torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(outs[1][2], outs[0][2], rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(outs[1][0], outs[0][0], rtol=1e-2, atol=1e-3)
+
+
+@pytest.mark.parametrize("n,C,hw,K_,skip", [(32, 256, 28, 1024, False), (32, 256, 28, 1024, True),
+                                            (2, 128, 7, 512, True), (8, 512, 7, 2048, False)])
+def test_gemm_bnb_epilogue_and_bn_bwd_parts(dev, n, C, hw, K_, skip):
+    """the 1x1 conv data gradient dX = dY.W with the STORE_BNB / ADD_RES_BNB epilogue (round 6): dX
+    bit-identical to the plain STORE / ADD_RES product, the table = the BatchNorm backward's
+    reduction {sum g, sum g (x - mean)} of dX, and mmu_batchnorm_bwd_parts on it = mmu_batchnorm_bwd
+    (big 256x256 tiles, and the 128x128 tiles of a 98-row map)."""
+    from src import kernels as K
+    x, wgt, sm, si, mask = _bn_fwd_for_bnb(dev, n, C, hw, n + C + int(skip))
+    M = n * hw * hw
+    dyn = torch.randn(M, K_, device=dev).to(torch.bfloat16)
+    w = (torch.randn(K_, C, device=dev) * K_ ** -0.5).to(torch.bfloat16)
+    res = torch.randn(M, C, device=dev).to(torch.bfloat16) if skip else None
+    plain = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+    K.gemm(dyn, K_, 1, w, C, 0, plain, C, M, C, K_, epi=K.epilogue(K.EPI_ADD_RES, residual=res) if skip else None)
+    dx = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+    table, nparts = K.bn_stats_table(M, C, dev)
+    kind = K.EPI_ADD_RES_BNB if skip else K.EPI_STORE_BNB
+    K.gemm(dyn, K_, 1, w, C, 0, dx, C, M, C, K_, epi=K.epilogue(kind, residual=res, colsum=table, bn=(x, mask, sm)))
+    assert torch.equal(dx, plain)
+    g, h = _bnb_reference(dx, x.permute(0, 2, 3, 1).reshape(M, C), mask, sm)
+    t = table.view(nparts, C, 2)
+    torch.testing.assert_close(t[..., 0], g, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(t[..., 1], h, rtol=1e-4, atol=1e-3)
+    _check_bn_bwd_parts(dev, dx.view(n, hw, hw, C).permute(0, 3, 1, 2), x, wgt, sm, si, mask, table, nparts)
+
+
+@pytest.mark.parametrize("n,C,hw", [(32, 128, 28), (64, 256, 14), (4, 256, 14), (8, 512, 7), (8, 64, 56)])
+def test_conv3x3_bnb_epilogue_and_bn_bwd_parts(dev, n, C, hw):
+    """mmu_conv3x3_implicit_bnb (the 3x3 conv data gradient + the backward reduction of the
+    BatchNorm before the conv, round 6): dX bit-identical to mmu_conv3x3_implicit, the table against
+    dX, mmu_batchnorm_bwd_parts against mmu_batchnorm_bwd -- small tiles (128 channels), big tiles,
+    and split-K maps (a reduction pass over dX after the slab sum)."""
+    from src import kernels as K
+    x, wgt, sm, si, mask = _bn_fwd_for_bnb(dev, n, C, hw, 7 * n + C)
+    cl = torch.channels_last
+    dyn = torch.randn(n, C, hw, hw, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    wf = (torch.randn(C, 3, 3, C, device=dev) * (9 * C) ** -0.5).to(torch.bfloat16).contiguous()
+    plain = torch.empty(n, C, hw, hw, dtype=torch.bfloat16, device=dev, memory_format=cl)
+    K.conv3x3_implicit(dyn, wf, plain)
+    dx = torch.empty_like(plain)
+    M = n * hw * hw
+    table, nparts = K.bn_stats_table(M, C, dev)
+    K.conv3x3_implicit(dyn, wf, dx, bnb=(x, mask, sm), table=table)
+    assert torch.equal(dx, plain)
+    g, h = _bnb_reference(dx.permute(0, 2, 3, 1).reshape(M, C), x.permute(0, 2, 3, 1).reshape(M, C), mask, sm)
+    t = table.view(nparts, C, 2)
+    torch.testing.assert_close(t[..., 0], g, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(t[..., 1], h, rtol=1e-4, atol=1e-3)
+    _check_bn_bwd_parts(dev, dx, x, wgt, sm, si, mask, table, nparts)

@@ -17,7 +17,7 @@ from test_mmbt_gpu import GOLD, _train_step, fixture  # noqa: E402
 from src import resnet as R  # noqa: E402
 
 
-def torch_bn(x, w, b, skip, bn, relu, sink=None):
+def torch_bn(x, w, b, skip, bn, relu, sink=None, *_):
     # (MIOpen's NHWC batch-norm crashes in host code below batch 8: resnet.BatchNorm2d's guard)
     with torch.backends.cudnn.flags(enabled=x.shape[0] >= R.BatchNorm2d.MIOPEN_MIN_BATCH):
         y = F.batch_norm(x, bn.running_mean, bn.running_var, w, b, True, bn.momentum, bn.eps)
@@ -32,6 +32,8 @@ VARIANTS = {
     "hip, convs on MIOpen": {"_mmu_conv": lambda *a: (False, False, False), "_mmu_1x1": lambda *a: (False, False, False)},
     "hip, BN on torch": {"bn": True},
     "hip, stem on MIOpen": {"_is_stem": lambda *a: False},
+    "hip, no BN-bwd fusion": {"BN_BWD_FUSION": False},
+    "hip, no BN fusion": {"BN_BWD_FUSION": False, "BN_STATS_FUSION": False},
 }
 
 
