@@ -131,6 +131,10 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor,
 /* Sum `parts` rows of a [parts, N] f32 partial table into out[N] (+= if accumulate). */
 int mmu_colsum_reduce(const float* partial, int64_t parts, int64_t N, float* out,
                       int accumulate, mmu_stream_t stream);
+/* n (1..4) independent mmu_colsum_reduce jobs of one width N in one launch: job z sums parts[z]
+ * rows of partial[z] into out[z] (host arrays of n entries; the pointers are device memory). */
+int mmu_colsum_reduce_multi(int n, const float* const* partial, const int64_t* parts, float* const* out, int64_t N,
+                            int accumulate, mmu_stream_t stream);
 /* Column sums of a bf16 [M, N] matrix into out[N] f32 (+= if accumulate): the bias grads
  * of the FLAVA blocks' projections (src/model.py).  `partial` (may be NULL): f32 scratch
  * of at least ceil(M / 64) * N floats; with it the row blocks are sized for ~1 K

@@ -224,6 +224,21 @@ int mmu_colsum_reduce(const float* partial, int64_t parts, int64_t N, float* out
   return check_launch("mmu_colsum_reduce");
 }
 
+int mmu_colsum_reduce_multi(int n, const float* const* partial, const int64_t* parts, float* const* out, int64_t N,
+                            int accumulate, mmu_stream_t stream) {
+  if (n <= 0 || n > COLSUM_MULTI || !partial || !parts || !out || N <= 0)
+    return fail("mmu_colsum_reduce_multi: bad args (1 <= n <= %d)", COLSUM_MULTI);
+  ColsumJobs jobs{};
+  for (int z = 0; z < n; ++z) {
+    if (!partial[z] || !out[z] || parts[z] <= 0) return fail("mmu_colsum_reduce_multi: bad job %d", z);
+    jobs.part[z] = partial[z];
+    jobs.parts[z] = parts[z];
+    jobs.out[z] = out[z];
+  }
+  colsum_reduce_multi_launch(jobs, n, N, accumulate, (hipStream_t)stream);
+  return check_launch("mmu_colsum_reduce_multi");
+}
+
 int mmu_colsum_bf16(const void* X, int64_t M, int64_t N, int64_t ldx, float* partial, float* out, int accumulate,
                     mmu_stream_t stream) {
   if (!X || !out || M <= 0 || N <= 0 || N % 8 || ldx % 8) return fail("mmu_colsum_bf16: bad args");

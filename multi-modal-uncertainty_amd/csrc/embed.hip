@@ -227,10 +227,14 @@ void embed_bwd_launch(const EmbedBwdParams& q, hipStream_t s) {
   hipLaunchKernelGGL(embed_bwd_rows_kernel, dim3((unsigned)((p.Lout + 3) / 4), (unsigned)((q.B + EBW_B - 1) / EBW_B)),
                      dim3(256), 0, s, q, p);
   const float* part = q.ws;
-  colsum_reduce_launch(part, nblk, 768, q.d_ln_w, 1, s);
-  colsum_reduce_launch(part + nblk * 768, nblk, 768, q.d_ln_b, 1, s);
-  colsum_reduce_launch(part + 2 * nblk * 768, nblk, 768, q.d_type, 1, s);
-  colsum_reduce_launch(part + 3 * nblk * 768, nblk, 768, q.d_type + 768, 1, s);
+  ColsumJobs jobs{};
+  float* outs[4] = {q.d_ln_w, q.d_ln_b, q.d_type, q.d_type + 768};
+  for (int z = 0; z < 4; ++z) {
+    jobs.part[z] = part + z * nblk * 768;
+    jobs.parts[z] = nblk;
+    jobs.out[z] = outs[z];
+  }
+  colsum_reduce_multi_launch(jobs, 4, 768, 1, s);
 }
 
 // ---------------------------------------------------------------- AdaptiveAvgPool2d((n,1))

@@ -780,20 +780,51 @@ __global__ __launch_bounds__(512) void gemm_conva_kernel(GemmParams p) {
   gemm_big_body<true, true, EPI, false, 2>(p);
 }
 
-// {sum, sum of squares} per column and 64-row block of a bf16 [M][N] map into part (float2
-// [ceil(M / 64)][N]): the statistics table of MMU_EPI_STORE_STATS for a product whose epilogue
-// could not produce it (a split-K conv: its output is formed by splitk_reduce_bf16_kernel)
-__global__ __launch_bounds__(256) void stats64_kernel(const bf16* __restrict__ Y, int64_t M, int64_t N,
-                                                      float* __restrict__ part) {
-  __shared__ float red[2][8][256];
-  const int t = threadIdx.x, oc = t & 31, rs = t >> 5;
-  const int64_t n = (int64_t)blockIdx.y * 256 + 8 * oc, r0 = (int64_t)blockIdx.x * 64;
-  float a[8], b[8];
+// The split-K slab sum of a conv whose epilogue also tabulates (STORE_STATS / STORE_BNB): one block
+// per 64 rows x 64 columns sums the slabs in slice order into the bf16 C, as
+// splitk_reduce_bf16_kernel does, and forms the block's table row from the stored values:
+// {sum, sum of squares} of C (STATS) or {sum g, sum g (x - mean)} with g = C * ReLU mask (BNB) --
+// the float2 [ceil(M / 64)][N] layout of the epilogues, in the same pass (round 6; was a
+// reduce launch + a tabulating launch over C)
+template <bool BNB>
+__global__ __launch_bounds__(256) void splitk_reduce_tab_kernel(const GemmParams p) {
+  // block = 64 rows x 64 columns (grid ceil(M/64) x N/64: enough blocks for the small split-K maps);
+  // thread = one column octet (t & 7) x rows rs, rs + 32 (rs = t >> 3)
+  __shared__ float red[4][2][8][8];
+  const int t = threadIdx.x, oc = t & 7, rs = t >> 3, l = t & 63, w = t >> 6;
+  const int64_t M = p.M, N = p.N, n = (int64_t)blockIdx.y * 64 + 8 * oc, r0 = (int64_t)blockIdx.x * 64;
+  bf16* C = (bf16*)p.C;
+  float a[8], b[8], mu[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) a[e] = b[e] = 0.f;
-  if (n < N) {
-    for (int r = rs; r < 64 && r0 + r < M; r += 8) {
-      const bf16x8 v = *(const bf16x8*)(Y + (r0 + r) * N + n);
+  for (int e = 0; e < 8; ++e) a[e] = b[e] = mu[e] = 0.f;
+  if (BNB) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) mu[e] = p.bn_mean[n + e];
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int64_t m = r0 + rs + 32 * h;
+    if (m >= M) continue;
+    const int64_t o = m * N + n;
+    const float* sl = p.ws + o;
+    float4 lo = *(const float4*)sl, hi = *(const float4*)(sl + 4);
+    for (int k = 1; k < p.splitk; ++k) {
+      const float4 c = *(const float4*)(sl + k * M * N), d = *(const float4*)(sl + k * M * N + 4);
+      lo.x += c.x; lo.y += c.y; lo.z += c.z; lo.w += c.w;
+      hi.x += d.x; hi.y += d.y; hi.z += d.z; hi.w += d.w;
+    }
+    const bf16x8 v = {f2bf(lo.x), f2bf(lo.y), f2bf(lo.z), f2bf(lo.w), f2bf(hi.x), f2bf(hi.y), f2bf(hi.z), f2bf(hi.w)};
+    *(bf16x8*)(C + m * p.ldc + n) = v;
+    if (BNB) {
+      const bf16x8 x = *(const bf16x8*)(p.bn_x + o);
+      const uint32_t mk = p.bn_mask ? (uint32_t)p.bn_mask[o >> 3] : 0xFFu;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float g = ((mk >> e) & 1) ? bf2f(v[e]) : 0.f;
+        a[e] += g;
+        b[e] = fmaf(g, bf2f(x[e]) - mu[e], b[e]);
+      }
+    } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float y = bf2f(v[e]);
@@ -802,58 +833,26 @@ __global__ __launch_bounds__(256) void stats64_kernel(const bf16* __restrict__ Y
       }
     }
   }
+  // lanes sharing oc within a wave: xor 8, 16, 32; then the 4 waves through LDS
 #pragma unroll
-  for (int e = 0; e < 8; ++e) { red[0][e][t] = a[e]; red[1][e][t] = b[e]; }
-  __syncthreads();
-  if (rs == 0 && n < N) {
+  for (int e = 0; e < 8; ++e) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float sa = 0.f, sb = 0.f;
-      for (int k = 0; k < 8; ++k) { sa += red[0][e][32 * k + oc]; sb += red[1][e][32 * k + oc]; }
-      part[2 * ((int64_t)blockIdx.x * N + n + e)] = sa;
-      part[2 * ((int64_t)blockIdx.x * N + n + e) + 1] = sb;
+    for (int x = 8; x < 64; x <<= 1) {
+      a[e] += __shfl_xor(a[e], x, 64);
+      b[e] += __shfl_xor(b[e], x, 64);
     }
   }
-}
-
-// the MMU_EPI_STORE_BNB table of a split-K product, after its reduction: {sum g, sum g (x - mean)}
-// per column and 64-row block, g = dY * mask (stats64_kernel's layout)
-__global__ __launch_bounds__(256) void bnb64_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ X,
-                                                    const uint8_t* __restrict__ mask, const float* __restrict__ mean,
-                                                    int64_t M, int64_t N, float* __restrict__ part) {
-  __shared__ float red[2][8][256];
-  const int t = threadIdx.x, oc = t & 31, rs = t >> 5;
-  const int64_t n = (int64_t)blockIdx.y * 256 + 8 * oc, r0 = (int64_t)blockIdx.x * 64;
-  float a[8], b[8];
+  if (l < 8) {
 #pragma unroll
-  for (int e = 0; e < 8; ++e) a[e] = b[e] = 0.f;
-  if (n < N) {
-    float mu[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) mu[e] = mean[n + e];
-    for (int r = rs; r < 64 && r0 + r < M; r += 8) {
-      const int64_t o = (r0 + r) * N + n;
-      const bf16x8 v = *(const bf16x8*)(dY + o), x = *(const bf16x8*)(X + o);
-      const uint32_t mk = mask ? (uint32_t)mask[o >> 3] : 0xFFu;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float g = ((mk >> e) & 1) ? bf2f(v[e]) : 0.f;
-        a[e] += g;
-        b[e] = fmaf(g, bf2f(x[e]) - mu[e], b[e]);
-      }
-    }
+    for (int e = 0; e < 8; ++e) { red[w][0][oc][e] = a[e]; red[w][1][oc][e] = b[e]; }
   }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { red[0][e][t] = a[e]; red[1][e][t] = b[e]; }
   __syncthreads();
-  if (rs == 0 && n < N) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float sa = 0.f, sb = 0.f;
-      for (int k = 0; k < 8; ++k) { sa += red[0][e][32 * k + oc]; sb += red[1][e][32 * k + oc]; }
-      part[2 * ((int64_t)blockIdx.x * N + n + e)] = sa;
-      part[2 * ((int64_t)blockIdx.x * N + n + e) + 1] = sb;
-    }
+  if (t < 64) {  // thread (oc, e) = (t >> 3, t & 7) writes one column's pair
+    const int c = t >> 3, e = t & 7;
+    const float sa = red[0][0][c][e] + red[1][0][c][e] + red[2][0][c][e] + red[3][0][c][e];
+    const float sb = red[0][1][c][e] + red[1][1][c][e] + red[2][1][c][e] + red[3][1][c][e];
+    const int64_t col = (int64_t)blockIdx.y * 64 + 8 * c + e;
+    *(float2*)(p.colsum + 2 * ((int64_t)blockIdx.x * N + col)) = make_float2(sa, sb);
   }
 }
 
@@ -876,7 +875,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_bf16_kernel(const float* __
 
 void conv3x3_implicit_launch(const GemmParams& p, bool small, hipStream_t s) {
   // p.kind == MMU_EPI_STORE_STATS: the epilogue also writes the output's BatchNorm statistics
-  // table (p.colsum); split-K forms the output in the reduce kernel, so a stats pass follows it
+  // table (p.colsum); split-K forms the output in the reduce kernel, which then tabulates it
   // (p.kind == MMU_EPI_STORE_BNB, a data gradient: the reduction table of the BatchNorm before it)
   const bool stats = p.kind == MMU_EPI_STORE_STATS && p.splitk == 1;
   const bool bnb = p.kind == MMU_EPI_STORE_BNB && p.splitk == 1;
@@ -891,15 +890,16 @@ void conv3x3_implicit_launch(const GemmParams& p, bool small, hipStream_t s) {
     else hipLaunchKernelGGL(gemm_conva_kernel<MMU_EPI_STORE>, grid, dim3(512), 0, s, p);
   }
   if (p.splitk > 1) {
-    const int64_t q = p.M * p.N / 8;
-    hipLaunchKernelGGL(splitk_reduce_bf16_kernel, dim3((unsigned)((q + 255) / 256)), dim3(256), 0, s, p.ws,
-                       (bf16*)p.C, p.M, p.N, p.ldc, p.splitk);
-    if (p.kind == MMU_EPI_STORE_STATS)
-      hipLaunchKernelGGL(stats64_kernel, dim3((unsigned)((p.M + 63) / 64), (unsigned)((p.N + 255) / 256)), dim3(256),
-                         0, s, (const bf16*)p.C, p.M, p.N, p.colsum);
-    if (p.kind == MMU_EPI_STORE_BNB)
-      hipLaunchKernelGGL(bnb64_kernel, dim3((unsigned)((p.M + 63) / 64), (unsigned)((p.N + 255) / 256)), dim3(256),
-                         0, s, (const bf16*)p.C, p.bn_x, p.bn_mask, p.bn_mean, p.M, p.N, p.colsum);
+    const dim3 tab((unsigned)((p.M + 63) / 64), (unsigned)(p.N / 64));  // (N % 64 == 0: conv_implicit)
+    if (p.kind == MMU_EPI_STORE_STATS) {
+      hipLaunchKernelGGL(splitk_reduce_tab_kernel<false>, tab, dim3(256), 0, s, p);
+    } else if (p.kind == MMU_EPI_STORE_BNB) {
+      hipLaunchKernelGGL(splitk_reduce_tab_kernel<true>, tab, dim3(256), 0, s, p);
+    } else {
+      const int64_t q = p.M * p.N / 8;
+      hipLaunchKernelGGL(splitk_reduce_bf16_kernel, dim3((unsigned)((q + 255) / 256)), dim3(256), 0, s, p.ws,
+                         (bf16*)p.C, p.M, p.N, p.ldc, p.splitk);
+    }
   }
 }
 
@@ -1012,6 +1012,34 @@ void colsum_reduce_launch(const float* part, int64_t parts, int64_t N, float* ou
   hipLaunchKernelGGL(colsum_reduce_kernel,
                      dim3((unsigned)((N + 255) / 256), (unsigned)((parts + COLSUM_ROWS - 1) / COLSUM_ROWS)),
                      dim3(256), 0, s, part, parts, N, out);
+}
+
+// up to COLSUM_MULTI independent reductions of one width N in one launch (grid.z = the job): the
+// bias / LayerNorm-parameter gradients a BERT layer's backward forms together (round 6: 9 launches
+// per layer -> 3)
+__global__ __launch_bounds__(256) void colsum_reduce_multi_kernel(const ColsumJobs jobs, int64_t N) {
+  const int z = blockIdx.z;
+  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t parts = jobs.parts[z];
+  const int64_t r0 = (int64_t)blockIdx.y * COLSUM_ROWS;
+  if (n >= N || r0 >= parts) return;
+  const int64_t r1 = r0 + COLSUM_ROWS < parts ? r0 + COLSUM_ROWS : parts;
+  const float* part = jobs.part[z];
+  float s = 0.f;
+#pragma unroll 8
+  for (int64_t r = r0; r < r1; ++r) s += part[r * N + n];
+  atomicAdd(jobs.out[z] + n, s);
+}
+
+void colsum_reduce_multi_launch(const ColsumJobs& jobs, int n, int64_t N, int acc, hipStream_t s) {
+  int64_t most = 0;
+  for (int z = 0; z < n; ++z) {
+    if (!acc) (void)hipMemsetAsync(jobs.out[z], 0, sizeof(float) * N, s);
+    most = jobs.parts[z] > most ? jobs.parts[z] : most;
+  }
+  hipLaunchKernelGGL(colsum_reduce_multi_kernel,
+                     dim3((unsigned)((N + 255) / 256), (unsigned)((most + COLSUM_ROWS - 1) / COLSUM_ROWS), (unsigned)n),
+                     dim3(256), 0, s, jobs, N);
 }
 
 // column sums of a bf16 [M, N] matrix: block = 64 octets of columns x rpb rows (4 waves, 4

@@ -70,6 +70,13 @@ void gemm_launch(const GemmParams& p, bool a_kmajor, bool b_kmajor, bool f32out,
 void transpose_bf16_batched_launch(const int64_t* jobs, int n_jobs, int64_t max_rows, int64_t max_cols,
                                    hipStream_t s);
 void colsum_reduce_launch(const float* part, int64_t parts, int64_t N, float* out, int acc, hipStream_t s);
+constexpr int COLSUM_MULTI = 4;
+struct ColsumJobs {  // (passed by value: graph-capturable)
+  const float* part[COLSUM_MULTI];
+  int64_t parts[COLSUM_MULTI];
+  float* out[COLSUM_MULTI];
+};
+void colsum_reduce_multi_launch(const ColsumJobs& jobs, int n, int64_t N, int acc, hipStream_t s);
 void colsum_bf16_launch(const bf16* X, int64_t M, int64_t N, int64_t ld, float* part, float* out, int acc,
                         hipStream_t s);
 

@@ -38,6 +38,7 @@ SIGNATURES = {
     "mmu_gemm": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_i64, c_i64, c_i64,
                          c_i64, c_i64, c_i64, c_i64, ctypes.POINTER(Epilogue), c_vp]),
     "mmu_colsum_reduce": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_vp]),
+    "mmu_colsum_reduce_multi": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp]),
     "mmu_colsum_bf16": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i32, c_vp]),
     "mmu_transpose_bf16_batched": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_vp]),
     "mmu_attention_fwd": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_f32, c_u64, c_vp,

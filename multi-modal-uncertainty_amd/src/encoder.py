@@ -128,10 +128,6 @@ def encoder_stack(lws, X, X32, keymask, B, L, p_attn, p_hid, seeds_of, need_grad
     return outs if all_layers else outs[-1]
 
 
-def _reduce(part, out):
-    K.colsum_reduce(part, out, accumulate=True)
-
-
 DEFER_WGRAD = True
 # the deferred closures keep their input tensors (dY2, Hh, dZ, A, dAo, O, dqkv, X: ~3 GB per layer
 # at batch 256, L = 513) alive until the flush; above this many retained bytes the work deferred
@@ -228,9 +224,7 @@ def layer_backward(lw, saved, dY, keymask, B, L, p_attn, p_hid, seeds, wgrad):
     K.layernorm_bwd(dY, S2, mean2, rstd2, lw.ln2w, dS2, dY2, p_hid, seeds[2], pw, pb, pbias)
     if wgrad:
         def w2():
-            _reduce(pw, lw.g_ln2w)
-            _reduce(pb, lw.g_ln2b)
-            _reduce(pbias, lw.g_b2)
+            K.colsum_reduce_multi([(pw, lw.g_ln2w), (pb, lw.g_ln2b), (pbias, lw.g_b2)], accumulate=True)
             K.gemm(dY2, HID, False, Hh, FFN, False, lw.g_w2, FFN, HID, FFN, M, epi=acc)
         side.run(w2, pw, pb, pbias, dY2, Hh)
     dZ = torch.empty(M, FFN, dtype=bf16, device=dev)
@@ -247,9 +241,7 @@ def layer_backward(lw, saved, dY, keymask, B, L, p_attn, p_hid, seeds, wgrad):
     K.layernorm_bwd(dA, S1, mean1, rstd1, lw.ln1w, dS1, dAo, p_hid, seeds[1], pw1, pb1, pbias1)
     if wgrad:
         def wo():
-            _reduce(pw1, lw.g_ln1w)
-            _reduce(pb1, lw.g_ln1b)
-            _reduce(pbias1, lw.g_bo)
+            K.colsum_reduce_multi([(pw1, lw.g_ln1w), (pb1, lw.g_ln1b), (pbias1, lw.g_bo)], accumulate=True)
             K.gemm(dAo, HID, False, O, HID, False, lw.g_wo, HID, HID, HID, M, epi=acc)
         side.run(wo, pw1, pb1, pbias1, dAo, O)
     dO = torch.empty(M, HID, dtype=bf16, device=dev)

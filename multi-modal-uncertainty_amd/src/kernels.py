@@ -178,6 +178,23 @@ def gemm(A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, M, N_, K, epi=None, batch=1
     return C
 
 
+def colsum_reduce_multi(jobs, accumulate=False):
+    """[(partial [parts_z, N], out [N]), ...] (1..4 jobs of one width N): one launch
+    (mmu_colsum_reduce_multi)"""
+    n = len(jobs)
+    N_ = jobs[0][0].shape[1]
+    for part, out in jobs:
+        _dev_check(part, out)
+        if part.dtype != torch.float32 or out.dtype != torch.float32 or part.shape[1] != N_ or out.numel() != N_ \
+                or not part.is_contiguous() or not out.is_contiguous():
+            raise N.NativeError("colsum_reduce_multi: f32 contiguous [parts, N] partials / [N] outputs of one N")
+    parts_p = (ctypes.c_void_p * n)(*[p.data_ptr() for p, _ in jobs])
+    rows = (ctypes.c_int64 * n)(*[p.shape[0] for p, _ in jobs])
+    outs = (ctypes.c_void_p * n)(*[o.data_ptr() for _, o in jobs])
+    N.call("mmu_colsum_reduce_multi", n, ctypes.cast(parts_p, ctypes.c_void_p), ctypes.cast(rows, ctypes.c_void_p),
+           ctypes.cast(outs, ctypes.c_void_p), N_, int(accumulate), _stream(jobs[0][1]))
+
+
 def colsum_reduce(partial, out, accumulate=False):
     _dev_check(partial, out)
     N.call("mmu_colsum_reduce", _ptr(partial), partial.shape[0], partial.shape[1], _ptr(out), int(accumulate),
@@ -237,9 +254,8 @@ def attention_dbias_reduce(parts, batch, L, g_bqkv, heads=12):
     nqb, nkb = (L + 127) // 128, (L + 63) // 64
     H = heads * 64
     r0, r1 = nqb * batch, (nqb + nkb) * batch
-    colsum_reduce(parts[:r0], g_bqkv[:H], accumulate=True)
-    colsum_reduce(parts[r0:r1], g_bqkv[H:2 * H], accumulate=True)
-    colsum_reduce(parts[r1:], g_bqkv[2 * H:], accumulate=True)
+    colsum_reduce_multi([(parts[:r0], g_bqkv[:H]), (parts[r0:r1], g_bqkv[H:2 * H]), (parts[r1:], g_bqkv[2 * H:])],
+                        accumulate=True)
 
 
 def attention_bwd(qkv, keymask, O, dO, lse, delta, dqkv, batch, L, heads=12, drop_p=0.0, seed=0, dropmask=None,

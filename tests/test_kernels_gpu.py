@@ -1186,3 +1186,22 @@ def test_embed_bwd_matches_autograd(dev, B, T):
     for got, ref, name in zip(grads + [d_proj], [l_.grad for l_ in leaves], ("word", "pos", "type", "ln_w", "ln_b",
                                                                           "proj")):
         torch.testing.assert_close(got, ref, rtol=2e-3, atol=2e-3 * ref.abs().max().item(), msg=name)
+
+
+def test_colsum_reduce_multi_matches_sums(dev):
+    """mmu_colsum_reduce_multi (round 6): up to 4 column-sum reductions of one width in one launch,
+    each with its own row count, accumulating into its own output -- the per-job sums of the
+    partial rows, as separate mmu_colsum_reduce calls give them."""
+    from src import kernels as K
+    torch.manual_seed(0)
+    N_ = 768
+    parts = [torch.randn(r, N_, device=dev) for r in (5, 1, 37, 16)]
+    outs = [torch.randn(N_, device=dev) for _ in parts]
+    want = [o + p.sum(0) for o, p in zip(outs, parts)]
+    K.colsum_reduce_multi(list(zip(parts, outs)), accumulate=True)
+    for o, w in zip(outs, want):
+        torch.testing.assert_close(o, w, rtol=1e-5, atol=1e-4)
+    outs2 = [torch.randn(N_, device=dev) for _ in parts[:2]]
+    K.colsum_reduce_multi(list(zip(parts[:2], outs2)))
+    for o, p in zip(outs2, parts[:2]):
+        torch.testing.assert_close(o, p.sum(0), rtol=1e-5, atol=1e-4)
