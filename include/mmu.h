@@ -119,6 +119,10 @@ typedef struct mmu_epilogue {
   const void* bn_x;         /* STORE_BNB / ADD_RES_BNB only (ABI 4): see those kinds      */
   const uint8_t* bn_mask;
   const float* bn_mean;
+  const uint8_t* res_mask;  /* ADD_RES / ADD_RES_BNB (ABI 4, optional): the residual is gated by
+                               a ReLU mask [M, N/8] u8 (bit e of byte (m, n/8) keeps residual[m][n+e];
+                               needs ldr == N) -- an identity Bottleneck's skip gradient g = dY3 * mask3
+                               read from bn3's dY and mask instead of a materialised dSkip      */
 } mmu_epilogue;
 
 int mmu_gemm(const void* A, int64_t lda, int a_kmajor,

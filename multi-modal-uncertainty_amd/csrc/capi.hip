@@ -141,6 +141,7 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
     p.res_ln_mean = epi->res_ln_mean; p.res_ln_rstd = epi->res_ln_rstd;
     p.res_ln_w = epi->res_ln_w; p.res_ln_b = epi->res_ln_b; p.res_ln_bstride = epi->res_ln_bstride;
     p.bn_x = (const bf16*)epi->bn_x; p.bn_mask = epi->bn_mask; p.bn_mean = epi->bn_mean;
+    p.res_mask = epi->res_mask;
   }
   p.kind = kind;
   if (kind < 0 || kind > MMU_EPI_ADD_RES_BNB) return fail("mmu_gemm: bad epilogue kind %d", kind);
@@ -163,6 +164,8 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
   if (kind == MMU_EPI_DGELU && !p.aux) return fail("mmu_gemm: DGELU epilogue needs aux");
   if ((kind == MMU_EPI_BIAS_DROP_RES || kind == MMU_EPI_ADD_RES || kind == MMU_EPI_ADD_RES_BNB) && !p.residual)
     return fail("mmu_gemm: epilogue needs residual");
+  if (p.res_mask && ((kind != MMU_EPI_ADD_RES && kind != MMU_EPI_ADD_RES_BNB) || epi->ldr != N || batch != 1))
+    return fail("mmu_gemm: res_mask only with ADD_RES / ADD_RES_BNB, batch 1, ldr == N");
   if (p.accumulate && c_dtype != MMU_F32) return fail("mmu_gemm: accumulate needs f32 C");
   if (p.drop_p < 0.f || p.drop_p >= 1.f) return fail("mmu_gemm: drop_p out of range");
   // split-K for long-K / few-tile products (the weight gradients: K = tokens, M x N = a weight matrix)

@@ -257,6 +257,7 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
     }
     // the pass's residual / aux rows are requested up front: one memory latency per pass
     bf16x8 in[RES32 ? 1 : 2 * PJ];
+    uint32_t rmk[EPI == MMU_EPI_ADD_RES ? 2 * PJ : 1];  // residual gate (p.res_mask), 0xFF = none
     float4 in32[RES32 ? 2 * PJ : 1][2];
     float rmu[RES32 ? 2 * PJ : 1], rrs[RES32 ? 2 * PJ : 1];
 #pragma unroll
@@ -279,8 +280,10 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
         }
       } else if (LOADS && !slab && m < p.M) {
         in[it] = *(const bf16x8*)(src + in_l + d * lds_);
+        if (EPI == MMU_EPI_ADD_RES) rmk[it] = p.res_mask ? (uint32_t)p.res_mask[(in_l + d * lds_) >> 3] : 0xFFu;
       } else {
         in[it] = bf16x8{};
+        if (EPI == MMU_EPI_ADD_RES) rmk[it] = 0;
       }
     }
 #pragma unroll
@@ -336,6 +339,10 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
       } else {
 #pragma unroll
         for (int r = 0; r < 8; ++r) inf[r] = LOADS ? bf2f(in[RES32 ? 0 : it][r]) : 0.f;
+        if (EPI == MMU_EPI_ADD_RES) {
+#pragma unroll
+          for (int r = 0; r < 8; ++r) inf[r] = ((rmk[EPI == MMU_EPI_ADD_RES ? it : 0] >> r) & 1) ? inf[r] : 0.f;
+        }
       }
       void* cdst = OUT_F32 ? (void*)((float*)p.C + c_l + d * p.ldc) : (void*)((bf16*)p.C + c_l + d * p.ldc);
       epi_oct<EPI, OUT_F32>(p, cdst, (XST && aux) ? aux + x_l + d * p.ldx : nullptr,

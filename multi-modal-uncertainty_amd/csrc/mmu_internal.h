@@ -49,6 +49,7 @@ struct GemmParams {
   const bf16* bn_x;
   const uint8_t* bn_mask;
   const float* bn_mean;
+  const uint8_t* res_mask;  // ADD_RES: residual gated by a ReLU mask [M][N/8] (ldr == N)
 };
 void conv3x3_wgrad_launch(const GemmParams& p, hipStream_t s);
 void conv3x3_implicit_launch(const GemmParams& p, bool small, hipStream_t s);  // small: 128x128 tiles

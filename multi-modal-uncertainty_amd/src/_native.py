@@ -26,7 +26,7 @@ class Epilogue(ctypes.Structure):
                 ("aux_bstride", c_i64), ("colsum", c_vp), ("colsum_bstride", c_i64), ("drop_p", c_f32),
                 ("seed", c_u64), ("workspace", c_vp), ("workspace_floats", c_i64), ("res_ln_mean", c_vp),
                 ("res_ln_rstd", c_vp), ("res_ln_w", c_vp), ("res_ln_b", c_vp), ("res_ln_bstride", c_i64),
-                ("bn_x", c_vp), ("bn_mask", c_vp), ("bn_mean", c_vp)]
+                ("bn_x", c_vp), ("bn_mask", c_vp), ("bn_mean", c_vp), ("res_mask", c_vp)]
 
 
 # name -> (restype, argtypes); every entry must be exported by the library (tested on CPU)

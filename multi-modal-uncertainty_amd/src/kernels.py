@@ -47,11 +47,12 @@ def _want(t, dtype, name):
 
 def epilogue(kind=EPI_STORE, bias=None, residual=None, aux=None, colsum=None, drop_p=0.0, seed=0, accumulate=False,
              ldr=0, ldx=0, bias_bstride=0, res_bstride=0, aux_bstride=0, colsum_bstride=0, res_ln=None,
-             res_ln_bstride=0, bn=None):
+             res_ln_bstride=0, bn=None, res_mask=None):
     """res_ln = (mean, rstd, w, b): with BIAS_DROP_RES into an f32 C, the residual is the LayerNorm
     output recomputed from the f32 ``residual`` rows (the previous LayerNorm's input).
     bn = (x, relu_mask or None, mean): with STORE_BNB / ADD_RES_BNB, the BatchNorm whose dY the
-    product forms; colsum is then its backward reduction table (bn_stats_table of x's rows)."""
+    product forms; colsum is then its backward reduction table (bn_stats_table of x's rows).
+    res_mask (ADD_RES / ADD_RES_BNB): a ReLU mask [M*N/8] u8 gating the residual per element."""
     e = Epilogue()
     e.kind, e.accumulate = kind, int(accumulate)
     e.bias, e.bias_bstride = _ptr(bias), bias_bstride
@@ -71,6 +72,11 @@ def epilogue(kind=EPI_STORE, bias=None, residual=None, aux=None, colsum=None, dr
     if bn is not None:
         _bnb_check(*bn, "epilogue bn")
         e.bn_x, e.bn_mask, e.bn_mean = (_ptr(t) for t in bn)
+    if res_mask is not None:
+        if res_mask.dtype != torch.uint8 or not res_mask.is_contiguous() or residual is None \
+                or res_mask.numel() * 8 != residual.numel():
+            raise N.NativeError("epilogue res_mask: contiguous uint8 with numel = residual.numel() / 8")
+        e.res_mask = _ptr(res_mask)
     return e
 
 

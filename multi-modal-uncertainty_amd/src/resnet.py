@@ -37,6 +37,10 @@ BN_STATS_FUSION = os.environ.get("MMU_BN_STATS_FUSION", "1") != "0"
 # mmu_conv3x3_implicit_bnb), so the BatchNorm backward skips its reduction pass
 # (round 6; MMU_BN_BWD_FUSION=0 turns it off, for A/Bs)
 BN_BWD_FUSION = os.environ.get("MMU_BN_BWD_FUSION", "1") != "0"
+# An identity Bottleneck's skip gradient g = dY3 * mask3 is read by conv1's dX epilogue from bn3's dY
+# and ReLU mask (res_mask) instead of being written out by bn3's backward (round 6;
+# MMU_SKIP_MASKED=0: the materialised dSkip, for A/Bs)
+SKIP_MASKED = os.environ.get("MMU_SKIP_MASKED", "1") != "0"
 
 
 class _BnStats:
@@ -107,6 +111,11 @@ class _BatchNormAct(torch.autograd.Function):
         dY = dY.contiguous(memory_format=torch.channels_last)
         dX = torch.empty_like(x)
         dS = torch.empty_like(x) if ctx.has_skip and ctx.needs_input_grad[3] else None
+        # an identity block's bn3 (sink + ReLU mask): the skip gradient g = dY * mask is not written
+        # out; conv1's dX epilogue reads dY and the mask instead (res_mask, SKIP_MASKED)
+        gated = SKIP_MASKED and dS is not None and ctx.sink is not None and mask is not None and ctx.relu
+        if gated:
+            dS = None
         want_w, want_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
         # straight into the flat gradient store when it exists (no AccumulateGrad pass)
         dw = (weight.grad if weight.grad is not None else torch.zeros_like(weight)) if want_w else None
@@ -123,6 +132,8 @@ class _BatchNormAct(torch.autograd.Function):
         rb = db if (want_b and ctx.bias_ref.grad is None) else None
         if ctx.sink is not None and dS is not None:  # conv1's dX GEMM adds it (EPI_ADD_RES)
             ctx.sink.g, dS = dS, None
+        elif gated:
+            ctx.sink.g = (dY, mask)
         return dX, rw, rb, dS, None, None, None, None, None, None, None
 
 
@@ -455,6 +466,13 @@ class _SkipGrad:
         self.g = None
 
 
+def _mask_bits(mask, like):
+    """a ReLU mask (u8, bit e of byte i = element 8i+e of the channels-last map) as a 0/1 tensor
+    shaped / laid out like ``like`` ([N, C, H, W] channels-last)"""
+    bits = (mask.view(-1, 1) >> torch.arange(8, device=mask.device, dtype=torch.uint8)) & 1
+    return bits.view(like.shape[0], like.shape[2], like.shape[3], like.shape[1]).permute(0, 3, 1, 2).to(like.dtype)
+
+
 def _rows(t):
     """[N, C, H, W] channels-last -> its [N*H*W, C] row-major view."""
     return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
@@ -565,9 +583,11 @@ class _Conv1x1(torch.autograd.Function):
         Co = w16.shape[0]
         M = Nb * H * W
         dy = dy.contiguous(memory_format=torch.channels_last)
-        skip = None
+        skip = rmask = None
         if ctx.sink is not None:
             skip, ctx.sink.g = ctx.sink.g, None
+            if isinstance(skip, tuple):  # (bn3's dY, its ReLU mask): the gated skip gradient
+                skip, rmask = skip
         dx = rw = None
         with K.timing_paused():
             if need_x and use_d:
@@ -576,16 +596,20 @@ class _Conv1x1(torch.autograd.Function):
                 if bnb is not None:  # + the backward reduction of the BatchNorm that produced x
                     table = K.bn_stats_table(M, C, x.device)
                     epi = K.epilogue(K.EPI_ADD_RES_BNB if skip is not None else K.EPI_STORE_BNB,
-                                     residual=_rows(skip) if skip is not None else None, colsum=table[0], bn=bnb)
+                                     residual=_rows(skip) if skip is not None else None, colsum=table[0], bn=bnb,
+                                     res_mask=rmask)
                     ctx.link.parts = table
                 else:
-                    epi = K.epilogue(K.EPI_ADD_RES, residual=_rows(skip)) if skip is not None else None
+                    epi = (K.epilogue(K.EPI_ADD_RES, residual=_rows(skip), res_mask=rmask)
+                           if skip is not None else None)
                 K.gemm(_rows(dy), Co, 1, w16.view(Co, C), C, 0, _rows(dx), C, M, C, Co, epi=epi)
                 skip = None
             elif need_x:
                 both = need_w and not use_w and ctx.w.grad is not None and not _side_wgrad(dy)
                 gx, gw, _ = torch.ops.aten.convolution_backward(dy, x, w16, None, (1, 1), (0, 0), (1, 1), False,
                                                                 (0, 0), 1, (True, both, False))
+                if rmask is not None:
+                    skip = skip * _mask_bits(rmask, skip)
                 dx = gx if skip is None else gx + skip
                 if both:  # (one MIOpen call for both products when neither goes elsewhere)
                     ctx.w.grad.add_(gw)

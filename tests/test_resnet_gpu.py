@@ -498,3 +498,42 @@ def test_conv3x3_bnb_epilogue_and_bn_bwd_parts(dev, n, C, hw):
     torch.testing.assert_close(t[..., 0], g, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(t[..., 1], h, rtol=1e-4, atol=1e-3)
     _check_bn_bwd_parts(dev, dx, x, wgt, sm, si, mask, table, nparts)
+
+
+@pytest.mark.parametrize("bnb", [False, True])
+def test_gemm_add_res_gated_by_relu_mask(dev, bnb):
+    """ADD_RES / ADD_RES_BNB with res_mask (round 6): the residual gated element-wise by a ReLU mask --
+    an identity Bottleneck's skip gradient dY3 * mask3 read inside conv1's dX epilogue -- equals the
+    plain epilogue on the materialised product, bit for bit, and the BNB table follows the output."""
+    from src import kernels as K
+    from src.resnet import _mask_bits
+    torch.manual_seed(11)
+    n, C, hw, K_ = 8, 256, 14, 1024
+    M = n * hw * hw
+    x, wgt, sm, si, mask = _bn_fwd_for_bnb(dev, n, C, hw, 5)
+    dy3 = torch.randn(n, C, hw, hw, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y3 = torch.randn(n, C, hw, hw, device=dev)
+    mask3 = torch.empty(M * C // 8, dtype=torch.uint8, device=dev)
+    # a ReLU mask from a real BN pass on an unrelated map
+    xb = y3.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    K.batchnorm_fwd(xb, torch.empty_like(xb), None, None, None, None, True, 0.1, 1e-5, relu=True,
+                    save_mean=torch.empty(C, device=dev), save_invstd=torch.empty(C, device=dev), relu_mask=mask3)
+    g3 = (dy3 * _mask_bits(mask3, dy3)).contiguous(memory_format=torch.channels_last)
+    rows = lambda t: t.permute(0, 2, 3, 1).reshape(M, C)
+    dyn = torch.randn(M, K_, device=dev).to(torch.bfloat16)
+    w = (torch.randn(K_, C, device=dev) * K_ ** -0.5).to(torch.bfloat16)
+    plain = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+    K.gemm(dyn, K_, 1, w, C, 0, plain, C, M, C, K_, epi=K.epilogue(K.EPI_ADD_RES, residual=rows(g3)))
+    out = torch.empty_like(plain)
+    if bnb:
+        table, nparts = K.bn_stats_table(M, C, dev)
+        epi = K.epilogue(K.EPI_ADD_RES_BNB, residual=rows(dy3), res_mask=mask3, colsum=table, bn=(x, mask, sm))
+    else:
+        epi = K.epilogue(K.EPI_ADD_RES, residual=rows(dy3), res_mask=mask3)
+    K.gemm(dyn, K_, 1, w, C, 0, out, C, M, C, K_, epi=epi)
+    assert torch.equal(out, plain)
+    if bnb:
+        g, h = _bnb_reference(out, rows(x), mask, sm)
+        t = table.view(nparts, C, 2)
+        torch.testing.assert_close(t[..., 0], g, rtol=1e-4, atol=1e-3)
+        torch.testing.assert_close(t[..., 1], h, rtol=1e-4, atol=1e-3)
