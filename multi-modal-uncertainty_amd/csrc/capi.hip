@@ -3,6 +3,7 @@
 // stream, and reports failures through a thread-local message (mmu_last_error).
 #include <stdarg.h>
 #include <stdio.h>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -60,6 +61,28 @@ std::pair<hipEvent_t, hipEvent_t> take_events() {
     (void)hipEventCreate(&ev.second);
   }
   return ev;
+}
+// per-(device, stream) f32 scratch for the split tail rows of mmu_gemm: 32 MiB, allocated on first
+// use outside stream capture (NULL: the product runs without the tail split)
+constexpr int64_t TAIL_WS_FLOATS = 8ll << 20;
+float* tail_workspace(int64_t floats, hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, float*> bufs;
+  if (floats > TAIL_WS_FLOATS) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = bufs.find({dev, s});
+  if (it != bufs.end()) return it->second;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+  void* b = nullptr;
+  if (hipMalloc(&b, sizeof(float) * TAIL_WS_FLOATS) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  bufs[{dev, s}] = (float*)b;
+  return (float*)b;
 }
 }  // namespace
 
@@ -190,6 +213,61 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
       p.ws = epi->workspace;
     }
   }
+  // 256 x 384 tiling (gemm_wide_kernel): both operands K-major, N % 384 == 0, no split-K, and at
+  // least MMU_GEMM_WIDE_MIN_TILES of its tiles (default 4 per CU: the bench's M = 131 k rows;
+  // fewer, larger tiles leave CUs idle on small products).  MMU_GEMM_WIDE=0 turns it off.
+  // (read per call, ~1 us: tests switch them inside one process)
+  const char* wide_env = getenv("MMU_GEMM_WIDE");
+  const char* wide_min_env = getenv("MMU_GEMM_WIDE_MIN_TILES");
+  const int wide_mode = wide_env ? atoi(wide_env) : 1;
+  const int64_t wide_min = wide_min_env ? (int64_t)atoll(wide_min_env) : (int64_t)1024;
+  // (the dGELU product stays on 256 x 256: its aux-row loads and column-sum atomics per 64-row
+  // block ran it 15-22 % slower on the wide tile, profiles/r6_gemm_wide_ab.txt)
+  const bool tail_kind = kind == MMU_EPI_STORE || kind == MMU_EPI_BIAS_GELU || kind == MMU_EPI_BIAS_DROP_RES ||
+                         kind == MMU_EPI_DGELU || kind == MMU_EPI_ADD_RES;
+  const bool wide_kind = tail_kind && kind != MMU_EPI_DGELU;
+  // Default rule (MMU_GEMM_WIDE=1), same-box A/B: the wide products N >= 2304 (QKV -3 %, FFN1 + GELU
+  // -8 % with the split tail); N = 768 stays on 256 x 256 (equal or 2 % slower: its 1026 wide tiles
+  // end in a round of 2).  MMU_GEMM_WIDE=2 takes every kind and width (tests).
+  const bool wide = (wide_mode == 2 ? tail_kind : wide_mode == 1 && wide_kind && N >= 2304) && big && a_kmajor &&
+                    b_kmajor && N % 384 == 0 && p.splitk == 1 &&
+                    2 * (M + 256) * lda < (1ll << 32) - 4096 && 2 * (N + 384) * ldb < (1ll << 32) - 4096 &&
+                    (M + 255) / 256 * (N / 384) * batch >= wide_min;
+  if (wide) {
+    p.tiles_m = (int)((M + 255) / 256);
+    p.tiles_n = (int)(N / 384);
+    p.group_m = p.tiles_n <= 2 ? 1 : (kind != MMU_EPI_DGELU ? 8 : 2);
+  }
+  // Split tail rows: when the last round of 256-row tiles holds whole tile rows and is at most an
+  // eighth full (M = 256 x 513 at batch 256: 1026 wide / 1539 big tiles on 256 CUs), those rows
+  // run as split-K partial products of the small tiling into a per-stream f32 scratch, and
+  // splitk_epilogue_kernel sums them and applies the same epilogue.  On by default for the wide
+  // tiling (MMU_GEMM_TAIL=1), whose tail round is 1.5 big tiles long; 2 = for the 256 x 256 tiling
+  // too (tests: there it costs +10-20 us, the 256^2 tail round is short), 0 = off.
+  const char* tail_env = getenv("MMU_GEMM_TAIL");
+  const int tail_mode = tail_env ? atoi(tail_env) : 1;
+  int64_t tail_rows = 0, m_main = M, tail_chunk = K;
+  int tail_split = 1;
+  float* tail_ws = nullptr;
+  if ((tail_mode == 2 || (tail_mode == 1 && wide)) && big && batch == 1 && p.splitk == 1 && tail_kind &&
+      a_kmajor && K >= 512) {
+    const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n, left = tiles % 256;
+    if (tiles > 256 && left > 0 && left % p.tiles_n == 0 && left * 8 <= 256) {
+      m_main = (int64_t)(p.tiles_m - left / p.tiles_n) * 256;
+      tail_rows = M - m_main;
+      const int64_t st = (tail_rows + 127) / 128 * (N / 128);  // small tiles over the tail rows
+      int64_t sk = 256 / st;
+      if (sk > K / 256) sk = K / 256;  // >= 4 K-steps per slice
+      if (sk < 1) sk = 1;
+      tail_chunk = ((K + sk - 1) / sk + 63) / 64 * 64;
+      tail_split = (int)((K + tail_chunk - 1) / tail_chunk);
+      tail_ws = tail_workspace((int64_t)tail_split * tail_rows * N, (hipStream_t)stream);
+      if (!tail_ws) {
+        tail_rows = 0;
+        m_main = M;
+      }
+    }
+  }
   hipStream_t s = (hipStream_t)stream;
   bool timed;
   std::pair<hipEvent_t, hipEvent_t> ev;
@@ -201,7 +279,27 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
     ev = take_events();
     (void)hipEventRecord(ev.first, s);
   }
-  gemm_launch(p, a_kmajor != 0, b_kmajor != 0, c_dtype == MMU_F32, big, (int)batch, s);
+  {
+    GemmParams pm = p;
+    if (tail_rows) pm.tiles_m = (int)(m_main / 256);
+    if (!(wide && gemm_wide_launch(pm, c_dtype == MMU_F32, (int)batch, s)))
+      gemm_launch(pm, a_kmajor != 0, b_kmajor != 0, c_dtype == MMU_F32, big, (int)batch, s);
+  }
+  if (tail_rows) {
+    GemmParams pt = p;
+    pt.A = p.A + m_main * lda;
+    pt.M = tail_rows;
+    pt.kind = MMU_EPI_STORE;
+    pt.accumulate = 0;
+    pt.splitk = tail_split;
+    pt.kchunk = tail_chunk;
+    pt.ws = tail_ws;
+    pt.tiles_m = (int)((tail_rows + 127) / 128);
+    pt.tiles_n = (int)(N / 128);
+    pt.group_m = 1;
+    gemm_launch(pt, true, b_kmajor != 0, true, false, 1, s);
+    splitk_epilogue_launch(p, c_dtype == MMU_F32, tail_ws, m_main, tail_rows, tail_split, s);
+  }
   if (p.splitk > 1) splitk_reduce_launch(p, (int)batch, s);
   if (timed) {
     (void)hipEventRecord(ev.second, s);

@@ -787,6 +787,95 @@ __global__ __launch_bounds__(512) void gemm_conva_kernel(GemmParams p) {
   gemm_big_body<true, true, EPI, false, 2>(p);
 }
 
+// ================================================================ wide: 256x384, LDS-DMA (round 6)
+// The BERT products with both operands K-major and N % 384 == 0 (QKV 2304, W1 3072, Wo / W2 /
+// the data gradients 768) on a 256 x 384 x 64 tile: 80 KiB per stage, the 2-stage ring fills all
+// 160 KiB of LDS.  Per 64-deep K-step a CU moves 80 KiB into LDS for 1.5x the MACs of the 256^2
+// tile's 64 KiB (76.8 vs 64 MAC per filled byte): the 256^2 K loop is bound by that fill (DESIGN
+// §3 GEMM), not by the MFMAs.  8 waves as 4 (M) x 2 (N), 64 x 192 per wave: 48 accumulators of
+// 16x16, A fragments held per k-half, B fragments streamed 4 at a time.  The epilogue is the
+// shared one, three 64-column blocks per wave.
+constexpr int WBM = 256, WBN = 384;
+constexpr int W_TA = WBM * BKT * 2;   // 32 KiB
+constexpr int W_TB = WBN * BKT * 2;   // 48 KiB
+constexpr int W_STAGE = W_TA + W_TB;  // 80 KiB
+
+// P x 1 KiB pieces per wave of a K-major [8 * 8 * P rows][64 k] tile (image as dma_tile<true>)
+template <int P>
+static __device__ __forceinline__ void dma_kmaj(char* s, __amdgpu_buffer_rsrc_t rsrc, int64_t ld, int64_t r0,
+                                                int64_t k0, int w, int l) {
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const int piece = w * P + i;
+    const int row = piece * 8 + (l >> 3), c = (l & 7) ^ (row & 7);
+    const uint32_t src = (uint32_t)(((r0 + row) * ld + k0 + 8 * c) * 2);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (MMU_LDS(void)*)(s + piece * 1024), 16, src, 0, 0, 0);
+  }
+}
+
+template <int EPI, bool OUT_F32>
+__global__ __launch_bounds__(512) void gemm_wide_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * W_STAGE];
+  const int t = threadIdx.x, l = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  int tm, tn, slice;
+  int64_t z;
+  block_tile(p, z, slice, tm, tn);
+  const int64_t m0 = (int64_t)tm * WBM, n0 = (int64_t)tn * WBN;
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + z * p.sA), 0, (int)(uint32_t)(p.M * p.lda * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.B + z * p.sB), 0, (int)(uint32_t)(p.N * p.ldb * 2), 0x00020000);
+  f32x4 acc[3][4][4];  // [64-column block][n-subtile][m-subtile]
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[c][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (int)(p.K / BKT);  // (host: K % 64 == 0, no split-K)
+  dma_kmaj<4>(smem, ra, p.lda, m0, 0, w, l);
+  dma_kmaj<6>(smem + W_TA, rb, p.ldb, n0, 0, w, l);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* sa = smem + (kt & 1) * W_STAGE;
+    const char* sb = sa + W_TA;
+    if (kt + 1 < nk) {
+      char* d = smem + ((kt + 1) & 1) * W_STAGE;
+      const int64_t k1 = (int64_t)(kt + 1) * BKT;
+      dma_kmaj<4>(d, ra, p.lda, m0, k1, w, l);
+      dma_kmaj<6>(d + W_TA, rb, p.ldb, n0, k1, w, l);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fa[j] = s_frag<true, 512>(sa, 64 * wm + 16 * j, ks, l);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        bf16x8 fb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fb[i] = s_frag<true, 512>(sb, 192 * wn + 64 * c + 16 * i, ks, l);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[c][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[c][i][j], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // 32-row epilogue passes (16 for the f32 hidden-stream residual): the other blocks' 128
+  // accumulators stay live beside a pass's prefetched rows
+  constexpr int PJ = (OUT_F32 && EPI == MMU_EPI_BIAS_DROP_RES) ? 1 : 2;
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+    epilogue_block<EPI, OUT_F32, 4, PJ>(p, z, 0, m0 + 64 * wm, n0 + 192 * wn + 64 * c, acc[c], l, smem + w * 16384);
+}
+
 // The split-K slab sum of a conv whose epilogue also tabulates (STORE_STATS / STORE_BNB): one block
 // per 64 rows x 64 columns sums the slabs in slice order into the bf16 C, as
 // splitk_reduce_bf16_kernel does, and forms the block's table row from the stored values:
@@ -932,6 +1021,82 @@ static void launch_e(const GemmParams& p, bool ak, bool bk, bool big, int batch,
   else if (ak && !bk) launch_t<true, false, EPI, F32>(p, big, batch, s);
   else if (!ak && !bk) launch_t<false, false, EPI, F32>(p, big, batch, s);
   else launch_t<false, true, EPI, F32>(p, big, batch, s);
+}
+
+// ---------------------------------------------------------------- split tail rows (round 6)
+// The last tile row of a product whose last round of tiles is nearly empty (M = 256 x 513 at
+// batch 256: 1026 tiles of 256 x 384 on 256 CUs) runs as split-K partial products of the small
+// tiling into f32 slabs; this kernel sums a 64 x 64 block's slabs in slice order straight into the
+// MFMA accumulator layout -- acc[i][j], lane l = C[m0 + 16 j + (l & 15)][n0 + 16 i + 4 (l >> 4) + 0..3]
+// -- and runs the shared epilogue on it, so every epilogue kind finishes the tail rows exactly as
+// the tile kernels do (only the f32 summation order of the K slices differs).
+template <int EPI, bool OUT_F32>
+__global__ __launch_bounds__(64) void splitk_epilogue_kernel(GemmParams p, const float* __restrict__ slabs,
+                                                             int64_t m_base, int64_t rows, int splitk) {
+  __shared__ __attribute__((aligned(16))) char ws[16384];
+  const int l = threadIdx.x;
+  const int64_t mr = (int64_t)blockIdx.x * 64, n0 = (int64_t)blockIdx.y * 64;
+  const int64_t slab = rows * p.N;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t r = mr + 16 * j + (l & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (r < rows) {
+        const float* s = slabs + r * p.N + n0 + 16 * i + 4 * (l >> 4);
+        a = *(const f32x4*)s;
+        for (int k = 1; k < splitk; ++k) a += *(const f32x4*)(s + k * slab);
+      }
+      acc[i][j] = a;
+    }
+  }
+  epilogue_block<EPI, OUT_F32, 4>(p, 0, 0, m_base + mr, n0, acc, l, ws);
+}
+
+bool splitk_epilogue_launch(const GemmParams& p, bool f32out, const float* slabs, int64_t m_base, int64_t rows,
+                            int splitk, hipStream_t s) {
+  const dim3 grid((unsigned)((rows + 63) / 64), (unsigned)(p.N / 64)), blk(64);
+  switch (p.kind) {
+    case MMU_EPI_STORE:
+      if (f32out) hipLaunchKernelGGL((splitk_epilogue_kernel<MMU_EPI_STORE, true>), grid, blk, 0, s, p, slabs, m_base, rows, splitk);
+      else hipLaunchKernelGGL((splitk_epilogue_kernel<MMU_EPI_STORE, false>), grid, blk, 0, s, p, slabs, m_base, rows, splitk);
+      return true;
+    case MMU_EPI_BIAS_GELU:
+      hipLaunchKernelGGL((splitk_epilogue_kernel<MMU_EPI_BIAS_GELU, false>), grid, blk, 0, s, p, slabs, m_base, rows, splitk);
+      return true;
+    case MMU_EPI_BIAS_DROP_RES:
+      if (f32out) hipLaunchKernelGGL((splitk_epilogue_kernel<MMU_EPI_BIAS_DROP_RES, true>), grid, blk, 0, s, p, slabs, m_base, rows, splitk);
+      else hipLaunchKernelGGL((splitk_epilogue_kernel<MMU_EPI_BIAS_DROP_RES, false>), grid, blk, 0, s, p, slabs, m_base, rows, splitk);
+      return true;
+    case MMU_EPI_DGELU:
+      hipLaunchKernelGGL((splitk_epilogue_kernel<MMU_EPI_DGELU, false>), grid, blk, 0, s, p, slabs, m_base, rows, splitk);
+      return true;
+    case MMU_EPI_ADD_RES:
+      hipLaunchKernelGGL((splitk_epilogue_kernel<MMU_EPI_ADD_RES, false>), grid, blk, 0, s, p, slabs, m_base, rows, splitk);
+      return true;
+    default: return false;
+  }
+}
+
+// the 256 x 384 tiling (host: both operands K-major, N % 384 == 0, no split-K; kinds below)
+bool gemm_wide_launch(const GemmParams& p, bool f32out, int batch, hipStream_t s) {
+  const dim3 grid(p.tiles_m * p.tiles_n, 1, batch), blk(512);
+  switch (p.kind) {
+    case MMU_EPI_STORE:
+      if (f32out) hipLaunchKernelGGL((gemm_wide_kernel<MMU_EPI_STORE, true>), grid, blk, 0, s, p);
+      else hipLaunchKernelGGL((gemm_wide_kernel<MMU_EPI_STORE, false>), grid, blk, 0, s, p);
+      return true;
+    case MMU_EPI_BIAS_GELU: hipLaunchKernelGGL((gemm_wide_kernel<MMU_EPI_BIAS_GELU, false>), grid, blk, 0, s, p); return true;
+    case MMU_EPI_BIAS_DROP_RES:
+      if (f32out) hipLaunchKernelGGL((gemm_wide_kernel<MMU_EPI_BIAS_DROP_RES, true>), grid, blk, 0, s, p);
+      else hipLaunchKernelGGL((gemm_wide_kernel<MMU_EPI_BIAS_DROP_RES, false>), grid, blk, 0, s, p);
+      return true;
+    case MMU_EPI_DGELU: hipLaunchKernelGGL((gemm_wide_kernel<MMU_EPI_DGELU, false>), grid, blk, 0, s, p); return true;
+    case MMU_EPI_ADD_RES: hipLaunchKernelGGL((gemm_wide_kernel<MMU_EPI_ADD_RES, false>), grid, blk, 0, s, p); return true;
+    default: return false;
+  }
 }
 
 void gemm_launch(const GemmParams& p, bool ak, bool bk, bool f32out, bool big, int batch, hipStream_t s) {

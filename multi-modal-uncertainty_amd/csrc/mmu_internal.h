@@ -68,6 +68,9 @@ void stem_wgrad_launch(const StemParams& p, float* dW, int accumulate, float* ws
 
 void splitk_reduce_launch(const GemmParams& p, int batch, hipStream_t s);
 void gemm_launch(const GemmParams& p, bool a_kmajor, bool b_kmajor, bool f32out, bool big, int batch, hipStream_t s);
+bool gemm_wide_launch(const GemmParams& p, bool f32out, int batch, hipStream_t s);
+bool splitk_epilogue_launch(const GemmParams& p, bool f32out, const float* slabs, int64_t m_base, int64_t rows,
+                            int splitk, hipStream_t s);
 void transpose_bf16_batched_launch(const int64_t* jobs, int n_jobs, int64_t max_rows, int64_t max_cols,
                                    hipStream_t s);
 void colsum_reduce_launch(const float* part, int64_t parts, int64_t N, float* out, int acc, hipStream_t s);

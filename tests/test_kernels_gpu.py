@@ -1205,3 +1205,143 @@ def test_colsum_reduce_multi_matches_sums(dev):
     K.colsum_reduce_multi(list(zip(parts[:2], outs2)))
     for o, p in zip(outs2, parts[:2]):
         torch.testing.assert_close(o, p.sum(0), rtol=1e-5, atol=1e-4)
+
+
+# ---------------------------------------------------------------- 256 x 384 tiling (round 6)
+@pytest.fixture
+def wide_gemm(monkeypatch):
+    """route every eligible product (both operands K-major, N % 384 == 0) to gemm_wide_kernel"""
+    monkeypatch.setenv("MMU_GEMM_WIDE", "2")  # (2: the dGELU product too)
+    monkeypatch.setenv("MMU_GEMM_WIDE_MIN_TILES", "1")
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256 * 257, 768, 3072), (16416, 3072, 768), (256 * 65 + 32, 768, 2304),
+                                     (16416, 2304, 768)])
+def test_gemm_wide_tail_round_shapes(dev, wide_gemm, M, N, Kd):
+    test_gemm_tail_round_shapes(dev, M, N, Kd)
+
+
+@pytest.mark.parametrize("M,N", [(256 * 257, 768), (256 * 64 + 32, 3072)])
+def test_gemm_wide_epilogues_exact_first_and_last_tile_rows(dev, wide_gemm, M, N):
+    test_gemm_epilogues_exact_first_and_last_tile_rows(dev, M, N)
+
+
+def test_gemm_wide_streams_and_batches(dev, wide_gemm):
+    test_gemm_many_tiles_every_element(dev, True, True)
+    test_gemm_bias_dropout_residual_f32_stream(dev)
+    test_gemm_residual_recomputed_layernorm(dev)
+    test_gemm_partial_last_wave(dev, 768)
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256 * 129 + 96, 768, 768), (4096, 3072, 768), (2 * 1536, 2304, 768)])
+def test_gemm_wide_bitwise_equals_big_tiles(dev, monkeypatch, M, N, Kd):
+    """Every output element accumulates the same 16x16x32 MFMAs in the same k order on both
+    tilings, so the 256 x 384 kernel's results equal the 256 x 256 kernel's bit for bit, for
+    every epilogue (dropout draws by global element index, colsum by float atomics excepted:
+    those are compared to a tolerance)."""
+    k = K()
+    A, B = rnd(M, Kd, dev=dev, seed=151), rnd(N, Kd, dev=dev, seed=152, scale=0.1)
+    bias = torch.randn(N, device=dev) * 0.1
+    R16 = rnd(M, N, dev=dev, seed=153)
+    S = torch.randn(M, N, device=dev) * 2.0 + 0.7
+    mean = S.mean(-1).contiguous()
+    rstd = torch.rsqrt(S.var(-1, unbiased=False) + 1e-12).contiguous()
+    w, b = torch.randn(N, device=dev), torch.randn(N, device=dev)
+    aux_in = (torch.rand(M, N, device=dev) + 0.5).to(torch.bfloat16)
+
+    def run():
+        outs = []
+        o = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        k.gemm(A, Kd, True, B, Kd, True, o, N, M, N, Kd, epi=k.epilogue(k.EPI_STORE, bias=bias))
+        outs.append(o)
+        o, z = torch.empty(M, N, dtype=torch.bfloat16, device=dev), torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        k.gemm(A, Kd, True, B, Kd, True, o, N, M, N, Kd, epi=k.epilogue(k.EPI_BIAS_GELU, bias=bias, aux=z))
+        outs += [o, z]
+        f = torch.empty(M, N, dtype=torch.float32, device=dev)
+        k.gemm(A, Kd, True, B, Kd, True, f, N, M, N, Kd,
+               epi=k.epilogue(k.EPI_BIAS_DROP_RES, bias=bias, residual=S, drop_p=0.1, seed=9, res_ln=(mean, rstd, w, b)))
+        outs.append(f)
+        o = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        k.gemm(A, Kd, True, B, Kd, True, o, N, M, N, Kd,
+               epi=k.epilogue(k.EPI_BIAS_DROP_RES, bias=bias, residual=R16, drop_p=0.1, seed=10))
+        outs.append(o)
+        o, cs = torch.empty(M, N, dtype=torch.bfloat16, device=dev), torch.zeros(N, device=dev)
+        k.gemm(A, Kd, True, B, Kd, True, o, N, M, N, Kd, epi=k.epilogue(k.EPI_DGELU, aux=aux_in, colsum=cs))
+        outs += [o]
+        o = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        k.gemm(A, Kd, True, B, Kd, True, o, N, M, N, Kd, epi=k.epilogue(k.EPI_ADD_RES, residual=R16))
+        outs.append(o)
+        f = torch.full((M, N), 0.5, dtype=torch.float32, device=dev)
+        k.gemm(A, Kd, True, B, Kd, True, f, N, M, N, Kd, epi=k.epilogue(k.EPI_STORE, accumulate=True))
+        outs.append(f)
+        torch.cuda.synchronize()
+        return outs, cs
+
+    monkeypatch.setenv("MMU_GEMM_TAIL", "0")  # (the split tail sums K in another order)
+    monkeypatch.setenv("MMU_GEMM_WIDE", "0")
+    ref, cs_ref = run()
+    monkeypatch.setenv("MMU_GEMM_WIDE", "2")
+    monkeypatch.setenv("MMU_GEMM_WIDE_MIN_TILES", "1")
+    got, cs_got = run()
+    for i, (g, r) in enumerate(zip(got, ref)):
+        assert torch.equal(g, r), f"output {i} differs: max {(g.float() - r.float()).abs().max().item():.3e}"
+    torch.testing.assert_close(cs_got, cs_ref, rtol=1e-4, atol=1e-4 * cs_ref.abs().max().item())
+
+
+@pytest.mark.parametrize("wide", ["0", "2"])
+@pytest.mark.parametrize("M,N,Kd", [(256 * 257, 768, 3072), (256 * 64 + 32, 3072, 768), (256 * 65 + 32, 768, 2304)])
+def test_gemm_split_tail_matches_whole_tiles(dev, monkeypatch, wide, M, N, Kd):
+    """The split tail rows (the last tile row of a nearly empty last round as split-K partial
+    products + splitk_epilogue_kernel) against the same product on whole tiles
+    (MMU_GEMM_TAIL=0): every epilogue kind, on the tail rows and on all rows; only the f32 sum
+    order of the K slices differs, so f32 outputs agree to f32 rounding and bf16 outputs to one
+    bf16 rounding step.  Dropout keeps are the same draws (global element index)."""
+    k = K()
+    monkeypatch.setenv("MMU_GEMM_WIDE", wide)
+    monkeypatch.setenv("MMU_GEMM_WIDE_MIN_TILES", "1")
+    A, B = rnd(M, Kd, dev=dev, seed=161), rnd(N, Kd, dev=dev, seed=162, scale=0.1)
+    bias = torch.randn(N, device=dev) * 0.1
+    R16 = rnd(M, N, dev=dev, seed=163)
+    S = torch.randn(M, N, device=dev) * 2.0 + 0.7
+    mean = S.mean(-1).contiguous()
+    rstd = torch.rsqrt(S.var(-1, unbiased=False) + 1e-12).contiguous()
+    w, b = torch.randn(N, device=dev), torch.randn(N, device=dev)
+    aux_in = (torch.rand(M, N, device=dev) + 0.5).to(torch.bfloat16)
+
+    def run():
+        outs = []
+        o = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        k.gemm(A, Kd, True, B, Kd, True, o, N, M, N, Kd, epi=k.epilogue(k.EPI_STORE, bias=bias))
+        outs.append(o)
+        o, z = torch.empty(M, N, dtype=torch.bfloat16, device=dev), torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        k.gemm(A, Kd, True, B, Kd, True, o, N, M, N, Kd, epi=k.epilogue(k.EPI_BIAS_GELU, bias=bias, aux=z))
+        outs += [o, z]
+        f = torch.empty(M, N, dtype=torch.float32, device=dev)
+        k.gemm(A, Kd, True, B, Kd, True, f, N, M, N, Kd,
+               epi=k.epilogue(k.EPI_BIAS_DROP_RES, bias=bias, residual=S, drop_p=0.1, seed=9, res_ln=(mean, rstd, w, b)))
+        outs.append(f)
+        o, cs = torch.empty(M, N, dtype=torch.bfloat16, device=dev), torch.zeros(N, device=dev)
+        k.gemm(A, Kd, True, B, Kd, True, o, N, M, N, Kd, epi=k.epilogue(k.EPI_DGELU, aux=aux_in, colsum=cs))
+        outs.append(o)
+        o = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        k.gemm(A, Kd, True, B, Kd, True, o, N, M, N, Kd, epi=k.epilogue(k.EPI_ADD_RES, residual=R16))
+        outs.append(o)
+        f2 = torch.full((M, N), 0.5, dtype=torch.float32, device=dev)
+        k.gemm(A, Kd, True, B, Kd, True, f2, N, M, N, Kd, epi=k.epilogue(k.EPI_STORE, accumulate=True))
+        outs.append(f2)
+        torch.cuda.synchronize()
+        return outs, cs
+
+    monkeypatch.setenv("MMU_GEMM_TAIL", "0")
+    ref, cs_ref = run()
+    monkeypatch.setenv("MMU_GEMM_TAIL", "2")  # (2: the 256 x 256 tiling too)
+    got, cs_got = run()
+    tail = slice(M - 256, M)
+    for i, (g, r) in enumerate(zip(got, ref)):
+        g, r = g.float(), r.float()
+        assert torch.equal(g[: M - 256], r[: M - 256]), f"output {i}: rows before the tail changed"
+        if i in (3, 6):  # f32 outputs
+            torch.testing.assert_close(g[tail], r[tail], rtol=1e-5, atol=1e-5 * r.abs().max().item())
+        else:
+            torch.testing.assert_close(g[tail], r[tail], rtol=1e-2, atol=1e-2 * r.abs().max().item())
+    torch.testing.assert_close(cs_got, cs_ref, rtol=1e-4, atol=1e-4 * cs_ref.abs().max().item())
