@@ -4,6 +4,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <map>
+#include <tuple>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -65,14 +66,15 @@ std::pair<hipEvent_t, hipEvent_t> take_events() {
 // per-(device, stream) f32 scratch for the split tail rows of mmu_gemm: 32 MiB, allocated on first
 // use outside stream capture (NULL: the product runs without the tail split)
 constexpr int64_t TAIL_WS_FLOATS = 8ll << 20;
-float* tail_workspace(int64_t floats, hipStream_t s) {
+// (slot 0: the split tail's slabs, slot 1: the column-sum partial rows)
+float* tail_workspace(int64_t floats, hipStream_t s, int slot = 0) {
   static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, float*> bufs;
+  static std::map<std::tuple<int, hipStream_t, int>, float*> bufs;
   if (floats > TAIL_WS_FLOATS) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> lk(mu);
-  auto it = bufs.find({dev, s});
+  auto it = bufs.find({dev, s, slot});
   if (it != bufs.end()) return it->second;
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
@@ -81,7 +83,7 @@ float* tail_workspace(int64_t floats, hipStream_t s) {
     (void)hipGetLastError();
     return nullptr;
   }
-  bufs[{dev, s}] = (float*)b;
+  bufs[{dev, s, slot}] = (float*)b;
   return (float*)b;
 }
 }  // namespace
@@ -279,6 +281,21 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
     ev = take_events();
     (void)hipEventRecord(ev.first, s);
   }
+  // column sums as partial rows (no float atomics: 50 us of the 0.74 ms dZ product at batch 256,
+  // 180 us on the wide tile; profiles/r6_gemm_colsum_ab.txt), folded by one colsum_reduce launch.
+  // Rows of 16 NJ per wave block: 128 on the 256 x 256 tile, 64 on the others.  MMU_GEMM_CS_PART=0: atomics.
+  const char* csp_env = getenv("MMU_GEMM_CS_PART");
+  const bool cs_rows_ok = p.colsum && batch == 1 && p.splitk == 1 && kind != MMU_EPI_STORE_STATS &&
+                          kind != MMU_EPI_STORE_BNB && kind != MMU_EPI_ADD_RES_BNB && (!csp_env || atoi(csp_env) != 0);
+  const int cs_rows_main = (big && !wide) ? 128 : 64;
+  const int64_t cs_parts_main = (m_main + cs_rows_main - 1) / cs_rows_main;
+  const int64_t cs_parts = cs_parts_main + (tail_rows + 63) / 64;
+  float* cs_part = cs_rows_ok ? tail_workspace(cs_parts * N, s, 1) : nullptr;
+  if (cs_part) {
+    p.cs_part = cs_part;
+    p.cs_m0 = 0;
+    p.cs_rows = cs_rows_main;
+  }
   {
     GemmParams pm = p;
     if (tail_rows) pm.tiles_m = (int)(m_main / 256);
@@ -297,9 +314,17 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
     pt.tiles_m = (int)((tail_rows + 127) / 128);
     pt.tiles_n = (int)(N / 128);
     pt.group_m = 1;
+    pt.cs_part = nullptr;
     gemm_launch(pt, true, b_kmajor != 0, true, false, 1, s);
-    splitk_epilogue_launch(p, c_dtype == MMU_F32, tail_ws, m_main, tail_rows, tail_split, s);
+    GemmParams pe = p;
+    if (cs_part) {
+      pe.cs_part = cs_part + cs_parts_main * N;
+      pe.cs_m0 = m_main;
+      pe.cs_rows = 64;
+    }
+    splitk_epilogue_launch(pe, c_dtype == MMU_F32, tail_ws, m_main, tail_rows, tail_split, s);
   }
+  if (cs_part) colsum_reduce_launch(cs_part, cs_parts, N, p.colsum, 1, s);
   if (p.splitk > 1) splitk_reduce_launch(p, (int)batch, s);
   if (timed) {
     (void)hipEventRecord(ev.second, s);

@@ -395,9 +395,16 @@ static __device__ __forceinline__ void epilogue_block(const GemmParams& p, int64
       cs[e] = s;
     }
     if (rr == 0) {
-      float* out = p.colsum + z * p.colsum_bstride + n;
+      if (p.cs_part) {  // this wave block's partial row (16 NJ rows), folded by colsum_reduce_kernel
+        if (mw >= p.M) return;  // (a block wholly past M has no table row)
+        float4* d = (float4*)(p.cs_part + ((mw - p.cs_m0) / p.cs_rows) * p.N + n);
+        d[0] = make_float4(cs[0], cs[1], cs[2], cs[3]);
+        d[1] = make_float4(cs[4], cs[5], cs[6], cs[7]);
+      } else {
+        float* out = p.colsum + z * p.colsum_bstride + n;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) atomicAdd(out + e, cs[e]);
+        for (int e = 0; e < 8; ++e) atomicAdd(out + e, cs[e]);
+      }
     }
   }
 }

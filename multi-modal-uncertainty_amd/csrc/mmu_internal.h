@@ -50,6 +50,11 @@ struct GemmParams {
   const uint8_t* bn_mask;
   const float* bn_mean;
   const uint8_t* res_mask;  // ADD_RES: residual gated by a ReLU mask [M][N/8] (ldr == N)
+  // column sums (colsum, batch 1) as plain stores of per-wave-block partial rows instead of float
+  // atomics: row (m_wave - cs_m0) / cs_rows of the [parts][N] table cs_part (the host folds it)
+  float* cs_part;
+  int64_t cs_m0;
+  int cs_rows;
 };
 void conv3x3_wgrad_launch(const GemmParams& p, hipStream_t s);
 void conv3x3_implicit_launch(const GemmParams& p, bool small, hipStream_t s);  // small: 128x128 tiles

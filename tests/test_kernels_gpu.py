@@ -1345,3 +1345,27 @@ def test_gemm_split_tail_matches_whole_tiles(dev, monkeypatch, wide, M, N, Kd):
         else:
             torch.testing.assert_close(g[tail], r[tail], rtol=1e-2, atol=1e-2 * r.abs().max().item())
     torch.testing.assert_close(cs_got, cs_ref, rtol=1e-4, atol=1e-4 * cs_ref.abs().max().item())
+
+
+@pytest.mark.parametrize("M,N,Kd,wide", [(256 * 257, 3072, 768, "1"), (300, 256, 128, "1"), (256 * 64 + 32, 3072, 768, "2"),
+                                         (256 * 257, 768, 3072, "2")])
+def test_gemm_colsum_partial_rows_match_atomics(dev, monkeypatch, M, N, Kd, wide):
+    """Column sums of the dGELU product as per-wave-block partial rows folded by one reduce launch
+    (the default) against the float-atomic epilogue (MMU_GEMM_CS_PART=0), on the 256 x 256, small,
+    wide and split-tail paths; the accumulate semantics (the sums are ADDED to colsum) kept."""
+    k = K()
+    monkeypatch.setenv("MMU_GEMM_WIDE", wide)
+    monkeypatch.setenv("MMU_GEMM_WIDE_MIN_TILES", "1")
+    A, B = rnd(M, Kd, dev=dev, seed=171), rnd(N, Kd, dev=dev, seed=172, scale=0.1)
+    aux = (torch.rand(M, N, device=dev) + 0.5).to(torch.bfloat16)
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("MMU_GEMM_CS_PART", flag)
+        o, cs = torch.empty(M, N, dtype=torch.bfloat16, device=dev), torch.full((N,), 1.0, device=dev)
+        k.gemm(A, Kd, True, B, Kd, True, o, N, M, N, Kd, epi=k.epilogue(k.EPI_DGELU, aux=aux, colsum=cs))
+        outs.append((o, cs))
+    assert torch.equal(outs[0][0], outs[1][0])
+    dg = (A.float() @ B.float().t()) * aux.float()
+    for _, cs in outs:
+        torch.testing.assert_close(cs, dg.sum(0) + 1.0, rtol=2e-3, atol=2e-3 * dg.abs().sum(0).max().item())
+    torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-4, atol=1e-4 * outs[0][1].abs().max().item())

@@ -107,6 +107,10 @@ def main():
          lambda: K.gemm(dY, HID, True, W2t, HID, True, out3072, FFN, M, FFN, HID,
                         epi=K.epilogue(K.EPI_DGELU, aux=Zs, colsum=cs)),
          lambda: torch.matmul(dY, W2)),
+        ("bwd dZ   B=W2^T kmaj, no colsum", M, FFN, HID,
+         lambda: K.gemm(dY, HID, True, W2t, HID, True, out3072, FFN, M, FFN, HID,
+                        epi=K.epilogue(K.EPI_DGELU, aux=Zs)),
+         lambda: torch.matmul(dY, W2)),
         ("bwd dA   B=W1^T kmaj", M, HID, FFN,
          lambda: K.gemm(dZ, FFN, True, W1t, FFN, True, out768, HID, M, HID, FFN,
                         epi=K.epilogue(K.EPI_ADD_RES, residual=dY)),
