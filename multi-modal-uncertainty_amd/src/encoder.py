@@ -23,6 +23,8 @@ gradient buffer (src/params.py) and skipped when the layer is frozen
 (src/framework.py:284-285 toggles requires_grad).
 """
 
+import os
+
 import torch
 
 from . import kernels as K
@@ -147,17 +149,19 @@ def _defer_budget(dev):
     return torch.cuda.get_device_properties(dev).total_memory // 4
 
 
-def _flush_deferred(dev):
-    """Issue the deferred weight-gradient work (and the DP hooks after it) on the side stream,
-    behind everything the main stream has enqueued so far -- the whole encoder dX chain -- so
-    it runs beside what follows (embedding backward, the ResNet trunk's backward)."""
-    items = _deferred.pop(dev, None)
-    _deferred_bytes.pop(dev, None)
-    if not items:
-        return
-    main = torch.cuda.current_stream(dev)
+# INTERLEAVE (MMU_WGRAD_INTERLEAVE=1): at the end of the encoder's data-gradient chain the deferred
+# work is not issued at once but item by item from the trunk's BatchNorm backwards
+# (K.side_pump, called by src/resnet.py), the rest when the backward ends.  A HIP graph replays
+# its nodes in capture order, so the all-at-once flush runs the ~200 weight-gradient kernels
+# before the first trunk kernel even at batch 32, where they would fit beside the trunk's
+# short BatchNorm / conv kernels (profiles/r6_wgrad_interleave_ab.txt).
+INTERLEAVE = os.environ.get("MMU_WGRAD_INTERLEAVE", "0") != "0"
+_pending = {}  # per device: flushed items not yet issued (INTERLEAVE)
+
+
+def _issue(dev, items):
+    """the items on the side stream (which already waits for the encoder's dX chain)"""
     side = K.side_stream(dev)
-    side.wait_stream(main)
     with torch.cuda.stream(side):
         e0 = _mark()
         for fn, tensors in items:
@@ -166,7 +170,36 @@ def _flush_deferred(dev):
             fn()
         if e0 is not None:
             _block_extra.append((e0, _mark()))
+
+
+def _flush_deferred(dev, interleave=False):
+    """Issue the deferred weight-gradient work (and the DP hooks after it) on the side stream,
+    behind everything the main stream has enqueued so far -- the whole encoder dX chain -- so
+    it runs beside what follows (embedding backward, the ResNet trunk's backward); with
+    `interleave` it is handed to pump_deferred instead."""
+    items = _deferred.pop(dev, None)
+    _deferred_bytes.pop(dev, None)
+    if not items:
+        return
+    main = torch.cuda.current_stream(dev)
+    side = K.side_stream(dev)
+    side.wait_stream(main)
+    if interleave:
+        _pending.setdefault(dev, []).extend(items)
+    else:
+        _issue(dev, items)
     K.join_at_backward_end(main, side)
+
+
+def pump_deferred(dev, n=1):
+    """issue up to n of the flushed items (INTERLEAVE) on the side stream"""
+    items = _pending.get(dev)
+    if items:
+        _pending[dev] = items[n:]
+        _issue(dev, items[:n])
+
+
+K.set_side_pump(pump_deferred)
 
 
 def _defer(dev, fn, tensors):
@@ -177,7 +210,9 @@ def _defer(dev, fn, tensors):
         def at_end():  # (nothing may stay deferred past the backward)
             if dev in _deferred:
                 _flush_deferred(dev)
-                torch.cuda.current_stream(dev).wait_stream(K.side_stream(dev))
+            if _pending.get(dev):
+                _issue(dev, _pending.pop(dev))
+            torch.cuda.current_stream(dev).wait_stream(K.side_stream(dev))
 
         torch.autograd.Variable._execution_engine.queue_callback(at_end)
     items.append((fn, tensors))
@@ -335,7 +370,7 @@ class BertLayerFunction(torch.autograd.Function):
             if hook is not None:  # the bucket all-reduce follows the layer's deferred work
                 _defer(side.dev, lambda: hook(lw), ())
             if flush:
-                _flush_deferred(side.dev)
+                _flush_deferred(side.dev, INTERLEAVE)
         elif wgrad and hook is not None:
             hook(lw)
         return (dX,) + (None,) * 13

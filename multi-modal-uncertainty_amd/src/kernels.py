@@ -139,6 +139,21 @@ def side_stream(dev):
     return s
 
 
+_side_pump = None
+
+
+def set_side_pump(fn):
+    """src/encoder.py's pump_deferred: deferred side-stream work issued piecewise"""
+    global _side_pump
+    _side_pump = fn
+
+
+def side_pump(dev, n=1):
+    """issue up to n pieces of the encoder's flushed weight-gradient work (interleave mode)"""
+    if _side_pump is not None:
+        _side_pump(dev, n)
+
+
 def side_stream_if_any(dev):
     """the device's side stream if one was created, else None"""
     return _side.get(torch.device(dev))

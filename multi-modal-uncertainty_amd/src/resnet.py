@@ -108,6 +108,7 @@ class _BatchNormAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dY):
         x, mask, weight, smean, sinv = ctx.saved_tensors
+        K.side_pump(dY.device, WGRAD_PUMP)  # (encoder INTERLEAVE: its weight-gradient work beside ours)
         dY = dY.contiguous(memory_format=torch.channels_last)
         dX = torch.empty_like(x)
         dS = torch.empty_like(x) if ctx.has_skip and ctx.needs_input_grad[3] else None
@@ -214,6 +215,7 @@ class _SyncBatchNormAct(torch.autograd.Function):
     def backward(ctx, dY):
         import torch.distributed as dist
         x, saved, weight, mean, invstd = ctx.saved_tensors
+        K.side_pump(x.device, WGRAD_PUMP)
         C = x.shape[1]
         want_w, want_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
         bias = ctx.bias_ref
@@ -327,7 +329,8 @@ def _is_stem(w16, stride, padding):
     return (tuple(w16.shape) == (64, 3, 7, 7) and tuple(stride) == (2, 2) and tuple(padding) == (3, 3))
 
 
-SIDE_WGRAD_MIN_BATCH = 128
+WGRAD_PUMP = int(os.environ.get("MMU_WGRAD_PUMP", "1"))  # deferred BERT items issued per BatchNorm backward
+SIDE_WGRAD_MIN_BATCH = int(os.environ.get("MMU_SIDE_WGRAD_MIN_BATCH", "128"))
 
 
 def _side_wgrad(t):
