@@ -18,7 +18,7 @@ import json
 import re
 from collections import defaultdict
 
-GEMM = re.compile(r"mmu::gemm_(big|small|pipe)_kernel")
+GEMM = re.compile(r"mmu::gemm_(big|small|pipe|wide)_kernel")
 
 
 def per_dispatch(path, counter):

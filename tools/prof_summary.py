@@ -82,7 +82,7 @@ def main():
             inside = True
         elif "embed_bwd" in k:
             inside = False
-        elif inside and re.search(r"gemm_big_kernel", k):
+        elif inside and re.search(r"gemm_(big|wide)_kernel", k):
             bert.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     if bert:
         lines += ["", f"BERT-layer GEMM launches (big-tile `mmu_gemm` between embed_fwd and embed_bwd; what "
