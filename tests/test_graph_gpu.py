@@ -159,4 +159,11 @@ def test_graph_replay_equals_eager_steps(dev, full):
         assert abs(a - b) <= max(1e-5 * abs(b), 3 * l_ee), (losses_a, losses_b, losses_c)
     assert len(set(losses_a)) == 3, "consecutive replays drew the same dropout masks"
     assert moved > 0
-    assert d <= max(1e-4, 3 * d_ee), (d, d_ee)
+    # full model: the eager step's own spread is bimodal -- one float-atomic order flip in the first
+    # optimizer steps moves the 4-step update by ~9e-3 or not at all (12 samples, with and without the
+    # downsample sink: replay vs eager 4.3e-4 ... 9.1e-3, eager vs eager 1.4e-3 ... 9.0e-3,
+    # profiles/r6_graph_floor.txt), so two eager runs can agree while the replay sits in the other
+    # mode; the bar is 3x the spread measured here or, on the full model, 2x the largest spread
+    # recorded there
+    full_floor = 1.8e-2 if full else 0.0
+    assert d <= max(1e-4, 3 * d_ee, full_floor), (d, d_ee)
