@@ -329,6 +329,8 @@ def _is_stem(w16, stride, padding):
     return (tuple(w16.shape) == (64, 3, 7, 7) and tuple(stride) == (2, 2) and tuple(padding) == (3, 3))
 
 
+# downsample blocks: conv1's dX epilogue adds the downsample conv's dX (no autograd sum) -- MMU_DS_SINK=0: off
+DS_SINK = os.environ.get("MMU_DS_SINK", "1") != "0"
 WGRAD_PUMP = int(os.environ.get("MMU_WGRAD_PUMP", "1"))  # deferred BERT items issued per BatchNorm backward
 SIDE_WGRAD_MIN_BATCH = int(os.environ.get("MMU_SIDE_WGRAD_MIN_BATCH", "128"))
 
@@ -369,9 +371,9 @@ class _ConvBF16(torch.autograd.Function):
     plus an AccumulateGrad add)."""
 
     @staticmethod
-    def forward(ctx, x, w, w16, stride, padding, flipped=None, stats=None, link=None):
+    def forward(ctx, x, w, w16, stride, padding, flipped=None, stats=None, link=None, sink_out=None):
         ctx.save_for_backward(x, w16)
-        ctx.w, ctx.conf, ctx.flipped, ctx.link = w, (stride, padding), flipped, link
+        ctx.w, ctx.conf, ctx.flipped, ctx.link, ctx.sink_out = w, (stride, padding), flipped, link, sink_out
         cout = w16.shape[0]
         if _is_stem(w16, stride, padding):  # the 7x7 / 2 stem: mmu_stem_conv_fwd
             n, _, h, wd = x.shape
@@ -396,6 +398,10 @@ class _ConvBF16(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        return _hand_dx(ctx, _ConvBF16._bwd(ctx, dy)) + (None,)
+
+    @staticmethod
+    def _bwd(ctx, dy):
         x, w16 = ctx.saved_tensors
         stride, padding = ctx.conf
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
@@ -461,12 +467,29 @@ class _ConvBF16(torch.autograd.Function):
 
 
 class _SkipGrad:
-    """The gradient of an identity-skip Bottleneck's residual input, handed from bn3's
-    backward to conv1's backward (which autograd always runs later: conv1 feeds bn3)."""
-    __slots__ = ("g",)
+    """The gradient of a Bottleneck's residual input, handed to conv1's backward, whose dX GEMM
+    adds it in its epilogue (EPI_ADD_RES[_BNB]) instead of autograd summing two gradients of x:
+    * identity blocks: bn3's backward hands dY3 (and its ReLU mask); autograd always runs it
+      before conv1's (conv1 feeds bn3);
+    * downsample blocks (ds = True): the downsample conv's backward hands its dX.  The block
+      builds that branch after conv3, so autograd (later-created nodes first) runs it before
+      conv1's backward; should it not, conv1 marks the sink done and the downsample conv returns
+      its dX to autograd as usual (and conv1 then writes no BatchNorm reduction for x: its dX
+      is not x's whole gradient)."""
+    __slots__ = ("g", "ds", "done")
 
-    def __init__(self):
-        self.g = None
+    def __init__(self, ds=False):
+        self.g, self.ds, self.done = None, ds, False
+
+
+def _hand_dx(ctx, out):
+    """a downsample conv's backward: its dX goes to the block's sink (conv1 adds it) when conv1
+    has not run yet"""
+    so = ctx.sink_out
+    if so is None or out[0] is None or so.done:
+        return out
+    so.g = out[0].contiguous(memory_format=torch.channels_last)
+    return (None,) + tuple(out[1:])
 
 
 def _mask_bits(mask, like):
@@ -558,7 +581,7 @@ class _Conv1x1(torch.autograd.Function):
     The GEMMs are excluded from bench.py's BERT-layer GEMM timing (timing_paused)."""
 
     @staticmethod
-    def forward(ctx, x, w, w16, sink, stats=None, link=None):
+    def forward(ctx, x, w, w16, sink, stats=None, link=None, sink_out=None):
         Nb, C, H, W = x.shape
         Co = w16.shape[0]
         M = Nb * H * W
@@ -574,11 +597,15 @@ class _Conv1x1(torch.autograd.Function):
         else:
             y = torch.ops.aten.convolution(x, w16, None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1)
         ctx.save_for_backward(x, w16)
-        ctx.w, ctx.sink, ctx.use, ctx.link = w, sink, (use_d, use_w), link
+        ctx.w, ctx.sink, ctx.use, ctx.link, ctx.sink_out = w, sink, (use_d, use_w), link, sink_out
         return y
 
     @staticmethod
     def backward(ctx, dy):
+        return _hand_dx(ctx, _Conv1x1._bwd(ctx, dy)) + (None,)
+
+    @staticmethod
+    def _bwd(ctx, dy):
         x, w16 = ctx.saved_tensors
         use_d, use_w = ctx.use
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
@@ -587,15 +614,18 @@ class _Conv1x1(torch.autograd.Function):
         M = Nb * H * W
         dy = dy.contiguous(memory_format=torch.channels_last)
         skip = rmask = None
+        late_ds = False
         if ctx.sink is not None:
             skip, ctx.sink.g = ctx.sink.g, None
+            ctx.sink.done = True
+            late_ds = ctx.sink.ds and skip is None  # (the downsample's dX comes through autograd)
             if isinstance(skip, tuple):  # (bn3's dY, its ReLU mask): the gated skip gradient
                 skip, rmask = skip
         dx = rw = None
         with K.timing_paused():
             if need_x and use_d:
                 dx = torch.empty_like(x, memory_format=torch.channels_last)
-                bnb = ctx.link.operands() if ctx.link is not None else None
+                bnb = ctx.link.operands() if ctx.link is not None and not late_ds else None
                 if bnb is not None:  # + the backward reduction of the BatchNorm that produced x
                     table = K.bn_stats_table(M, C, x.device)
                     epi = K.epilogue(K.EPI_ADD_RES_BNB if skip is not None else K.EPI_STORE_BNB,
@@ -681,7 +711,7 @@ class StoreConv2d(nn.Conv2d):
         N_, C, H, W = x.shape
         return _mmu_1x1(C, self.out_channels, N_ * H * W, H)[1]
 
-    def forward(self, x, sink=None, bnb=False):
+    def forward(self, x, sink=None, bnb=False, sink_out=None):
         """bnb: x is a training BatchNorm's output and this conv its only consumer (the gradient
         of x is this conv's dX alone): the dX epilogue may write that BatchNorm's backward
         reduction (BN_BWD_FUSION, _BnLink)"""
@@ -693,14 +723,15 @@ class StoreConv2d(nn.Conv2d):
             # epilogue writes them when it runs on the mmu products (BN_STATS_FUSION)
             st = _BnStats() if BN_STATS_FUSION and self.training and torch.is_grad_enabled() else None
             if self._is_1x1():
-                y = _Conv1x1.apply(x, self.weight, w16, sink, st, link)
+                y = _Conv1x1.apply(x, self.weight, w16, sink, st, link, sink_out)
             else:
-                y = _ConvBF16.apply(x, self.weight, w16, self.stride, self.padding, self._flipped_getter(), st, link)
+                y = _ConvBF16.apply(x, self.weight, w16, self.stride, self.padding, self._flipped_getter(), st, link,
+                                    sink_out)
             if st is not None and st.parts is not None:
                 y._mmu_bnparts = st.parts
             return y
-        if sink is not None:
-            raise RuntimeError("StoreConv2d: a skip-gradient sink needs the bf16 1x1 path")
+        if sink is not None or sink_out is not None:
+            raise RuntimeError("StoreConv2d: a skip-gradient sink needs the bf16 path")
         return super().forward(x)
 
 
@@ -765,10 +796,24 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         sink = None
-        if (self.downsample is None and self.training and self.bn3.track_running_stats and x.is_cuda
-                and x.dtype == torch.bfloat16 and self.conv1.takes_skip_grad(x)):
+        ds_pair = (isinstance(self.downsample, nn.Sequential) and len(self.downsample) == 2
+                   and isinstance(self.downsample[0], StoreConv2d) and isinstance(self.downsample[1], BatchNorm2d))
+        if (self.training and self.bn3.track_running_stats and x.is_cuda and x.dtype == torch.bfloat16
+                and (self.downsample is None or (DS_SINK and ds_pair and self.downsample[0]._compute_weight(x) is not None))
+                and self.conv1.takes_skip_grad(x)):
             x = x.contiguous(memory_format=torch.channels_last)
-            sink = _SkipGrad()
+            sink = _SkipGrad(ds=self.downsample is not None)
+        if sink is not None and sink.ds:
+            # the downsample branch after conv3: autograd (later-created nodes first) then runs its
+            # backward before conv1's, and conv1's dX epilogue adds the downsample's dX (_SkipGrad)
+            y = self.bn1(self.conv1(x, sink=sink, bnb=True), relu=True)
+            y = self.bn2(self.conv2(y, bnb=True), relu=True)
+            y = self.conv3(y, bnb=True)
+            skip = self.downsample[1](self.downsample[0](x, sink_out=sink), out_res=True)
+            out = self.bn3(y, skip=skip, relu=True, out_res=True)
+            if getattr(skip, "_mmu_res", None) is not None:
+                del skip._mmu_res
+            return out
         if self.downsample is None:
             skip = x
         elif isinstance(self.downsample, nn.Sequential) and len(self.downsample) == 2 and isinstance(
