@@ -102,21 +102,30 @@ def layer_forward(lw, X, R, keymask, B, L, p_attn, p_hid, seeds, save, res_ln=No
            epi=K.epilogue(K.EPI_BIAS_DROP_RES, bias=lw.b2, residual=S1, drop_p=p_hid, seed=seeds[2],
                           res_ln=(mean1, rstd1, lw.ln1w, lw.ln1b)))
     Y = torch.empty(M, HID, dtype=bf16, device=dev)
-    Y32 = torch.empty(M, HID, dtype=f32, device=dev) if out32 else None
+    Y32 = torch.empty(M, HID, dtype=f32, device=dev) if out32 is True else None
     mean2 = torch.empty(M, dtype=f32, device=dev)
     rstd2 = torch.empty(M, dtype=f32, device=dev)
     K.layernorm_fwd_f32(S2, lw.ln2w, lw.ln2b, Y, Y32, mean2, rstd2)
+    if out32 == "cls":  # only the [CLS] rows' f32 output (the pooler's input): the same kernel on them
+        S2c = S2.view(B, L, HID)[:, 0].contiguous()
+        Y32 = torch.empty(B, HID, dtype=f32, device=dev)
+        K.layernorm_fwd_f32(S2c, lw.ln2w, lw.ln2b, torch.empty(B, HID, dtype=bf16, device=dev), Y32)
     saved = (X, qkv, O, lse, dmask, S1, mean1, rstd1, A, Z, Hh, S2, mean2, rstd2) if save else None
     return Y, S2, mean2, rstd2, saved, Y32
 
 
-def encoder_stack(lws, X, X32, keymask, B, L, p_attn, p_hid, seeds_of, need_grad, hook=None, all_layers=False):
+def encoder_stack(lws, X, X32, keymask, B, L, p_attn, p_hid, seeds_of, need_grad, hook=None, all_layers=False,
+                  cls_only=False):
     """Run the fused layers over (X bf16, X32 f32 embedding rows); returns the f32 hidden
-    state of the last layer, or of every layer (all_layers)."""
+    state of the last layer, or of every layer (all_layers); with cls_only only the last layer's
+    [CLS] rows [B, 768] (the pooler's input: no f32 copy of the other B (L - 1) rows, and no
+    [B L, 768] f32 zero gradient for them in the backward)."""
     R, rln, outs = X32, None, []
     n = len(lws)
     for i, lw in enumerate(lws):
         out32 = all_layers or i == n - 1
+        if out32 and cls_only and not all_layers:
+            out32 = "cls"
         if need_grad:
             # (layer 0's backward is the encoder's last: it flushes the deferred weight gradients)
             X, R, mu, rs, Y32 = BertLayerFunction.apply(X, R, lw.anchor, lw, keymask, B, L, p_attn, p_hid,
@@ -358,7 +367,12 @@ class BertLayerFunction(torch.autograd.Function):
         lw, keymask, B, L, p_attn, p_hid, seeds, hook, flush = ctx.meta
         wgrad = lw.trainable()
         if dY32 is not None and dY32.numel():
-            dY = dY32.to(bf16) if dY is None else dY + dY32.to(bf16)
+            if dY32.shape[0] == B and B * L != B:  # out32 "cls": the gradient of the [CLS] rows only
+                g = torch.zeros(B * L, HID, dtype=bf16, device=dY32.device) if dY is None else dY.clone()
+                g.view(B, L, HID)[:, 0] += dY32.to(bf16)
+                dY = g
+            else:
+                dY = dY32.to(bf16) if dY is None else dY + dY32.to(bf16)
         if dY is None:
             return (None,) * 14
         e0 = _mark()

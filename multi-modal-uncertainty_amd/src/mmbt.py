@@ -17,6 +17,8 @@ What runs where on the GPU:
   pooler + classifier   torch f32 (768x768, 768x101 on one row per sample)
 No CPU fallback: the encoder path raises on CPU tensors.
 """
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -25,6 +27,9 @@ from . import kernels as K
 from .encoder import LayerWeights, encoder_stack
 from .params import ParamStore
 from .resnet import StoreConv2d, resnet152_trunk
+
+# the encoder hands the pooler only the last layer's [CLS] rows (MMU_CLS_ONLY=0: all rows, round 5)
+CLS_ONLY = os.environ.get("MMU_CLS_ONLY", "1") != "0"
 
 BERT_CONFIGS = {
     # name: (layers, hidden, heads, intermediate, vocab, max_pos, type_vocab)
@@ -442,8 +447,8 @@ class MultimodalBertEncoder(nn.Module):
         return (X, X32), km, L
 
     def _encode(self, XX, km, nb, L):
-        """(X bf16, X32 f32) [nb*L, 768], km [nb, L] -> last hidden [nb*L, 768] f32 (the f32
-        hidden stream; see src/encoder.py)."""
+        """(X bf16, X32 f32) [nb*L, 768], km [nb, L] -> the last layer's [CLS] rows [nb, 768] f32
+        (all the pooler reads of the f32 hidden stream; see src/encoder.py)."""
         X, X32 = XX
         act = self._dropout_active()
         p_attn, p_hid = (self.attn_dropout, self.hidden_dropout) if act else (0.0, 0.0)
@@ -451,10 +456,12 @@ class MultimodalBertEncoder(nn.Module):
         need_grad = torch.is_grad_enabled() and (X.requires_grad or any(lw.trainable() for lw in self._lw))
         return encoder_stack(self._lw, X, X32, km, nb, L, p_attn, p_hid,
                              lambda i: (_mix(base, 3 * i), _mix(base, 3 * i + 1), _mix(base, 3 * i + 2)),
-                             need_grad, self._grad_ready_hook)
+                             need_grad, self._grad_ready_hook, cls_only=CLS_ONLY)
 
     def _pool(self, X, nb, L):
-        return self.pooler(X.view(nb, L, 768))
+        """the pooler on the [CLS] rows: X is the last layer's [nb, 768] [CLS] rows (_encode) or
+        its whole [nb * L, 768] output"""
+        return self.pooler(X.view(nb, L, 768) if X.shape[0] != nb or L == 1 else X.view(nb, 1, 768))
 
     # ---------------------------------------------------------------- reference forwards
     def forward(self, input_txt, attention_mask, segment, input_img):
