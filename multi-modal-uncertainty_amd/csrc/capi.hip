@@ -263,7 +263,8 @@ int mmu_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ld
       if (sk < 1) sk = 1;
       tail_chunk = ((K + sk - 1) / sk + 63) / 64 * 64;
       tail_split = (int)((K + tail_chunk - 1) / tail_chunk);
-      tail_ws = tail_workspace((int64_t)tail_split * tail_rows * N, (hipStream_t)stream);
+      // (a single slice would make the small kernel store its raw product into C: no split then)
+      tail_ws = tail_split >= 2 ? tail_workspace((int64_t)tail_split * tail_rows * N, (hipStream_t)stream) : nullptr;
       if (!tail_ws) {
         tail_rows = 0;
         m_main = M;
