@@ -164,7 +164,12 @@ def _defer_budget(dev):
 # its nodes in capture order, so the all-at-once flush runs the ~200 weight-gradient kernels
 # before the first trunk kernel even at batch 32, where they would fit beside the trunk's
 # short BatchNorm / conv kernels (profiles/r6_wgrad_interleave_ab.txt).
-INTERLEAVE = os.environ.get("MMU_WGRAD_INTERLEAVE", "0") != "0"
+# MMU_WGRAD_INTERLEAVE=2: the first trunk BatchNorm backward issues ALL of it, behind everything the
+# main stream has enqueued by then (the embedding and image-projection backward then run without the
+# side stream's weight-gradient GEMMs holding every CU)
+# (default 2: -0.37 ms at batch 256, neutral at 32, profiles/r6_wgrad_flush_late_ab.txt; 0 = round 5)
+INTERLEAVE = os.environ.get("MMU_WGRAD_INTERLEAVE", "2") != "0"
+INTERLEAVE_ALL = os.environ.get("MMU_WGRAD_INTERLEAVE", "2") == "2"
 _pending = {}  # per device: flushed items not yet issued (INTERLEAVE)
 
 
@@ -201,9 +206,13 @@ def _flush_deferred(dev, interleave=False):
 
 
 def pump_deferred(dev, n=1):
-    """issue up to n of the flushed items (INTERLEAVE) on the side stream"""
+    """issue up to n of the flushed items (INTERLEAVE) on the side stream (INTERLEAVE_ALL: all of
+    them, after the main stream's work so far)"""
     items = _pending.get(dev)
     if items:
+        if INTERLEAVE_ALL:
+            K.side_stream(dev).wait_stream(torch.cuda.current_stream(dev))
+            n = len(items)
         _pending[dev] = items[n:]
         _issue(dev, items[:n])
 
